@@ -1,0 +1,304 @@
+#!/usr/bin/env python3
+"""Device-resident range-coder throughput on MI355X (BASELINE.json metric).
+
+One step = compress the whole packet batch, then decompress it back
+(config C2: 65536 x 1200 B uniform-random packets per GPU, inputs resident in
+HBM).  value = sum of uncompressed payload bytes of all ranks x steps / max
+over ranks of the timed region, in GiB/s.
+
+Multi-GPU (torchrun, one rank per GPU): every rank owns an independent
+65536-packet shard (config C5, distinct seeds) and no collective runs inside
+the timed region -- packets are independent (compress.c:252-265), so this is
+weak scaling.  The RCCL scatter/gather of a batch from rank 0 is timed
+separately and reported in "rccl_scatter_gather".
+
+Extra fields: "roofline" (dominant kernel, algorithmic HBM bytes / measured
+kernel time vs 8 TB/s), "cpu_baseline" (reference compress.c on host cores,
+rank 0 only), "pcie_inclusive" (H2D + kernels + D2H from pinned memory).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6.3 TB/s achievable
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
+    p.add_argument("--packets", type=int, default=65536)
+    p.add_argument("--size", type=int, default=1200)
+    p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-pcie", action="store_true")
+    p.add_argument("--no-rccl", action="store_true")
+    return p.parse_args()
+
+
+def make_batch(kind, n, size, rank):
+    from enet_amd import synth
+    seed = synth.SEED + rank
+    if kind == "c2":
+        return synth.random_batch(n, size, seed=seed)
+    if kind == "c3":
+        return synth.gamestate_batch(n, size, seed=(synth.SEED ^ 0x47414D45) + rank)
+    return synth.mixed_batch(n, seed=(synth.SEED ^ 0x4D495845) + rank)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from enet_amd import RangeCoder
+
+    d, o, l = make_batch(args.workload, args.packets, args.size, rank)
+    n = len(l)
+    max_len = int(l.max())
+    din = torch.from_numpy(d).to(dev)
+    doff = torch.from_numpy(o.astype(np.int64)).to(dev)
+    dlen = torch.from_numpy(l.astype(np.int32)).to(dev)
+    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+    coff = torch.zeros(n, dtype=torch.int64, device=dev)
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+    cout = torch.empty(int(coff[-1] + cap[-1]), dtype=torch.uint8, device=dev)
+    clen = torch.zeros(n, dtype=torch.int32, device=dev)
+    dout = torch.empty_like(din)
+    dl = torch.zeros(n, dtype=torch.int32, device=dev)
+    coder = RangeCoder()
+    stream = torch.cuda.current_stream(dev)
+    in_bytes = int(l.sum(dtype=np.uint64))
+
+    # size the decoder's LDS staging from the actual compressed lengths
+    coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=max_len, stream=stream)
+    torch.cuda.synchronize()
+    dec_max_len = int(clen.max().item())
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=max_len, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        coder.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=dec_max_len, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness guard for the timed configuration
+    ok = bool(torch.equal(dl, dlen)) and bool(torch.equal(dout, din))
+    comp_bytes = int(clen.to(torch.int64).sum().item())
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    t_comp = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps / 1e3
+    t_dec = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps / 1e3
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    total_bytes = in_bytes * world * args.steps
+    value = total_bytes / elapsed / GIB
+
+    # roofline of the dominant kernel (whichever of compress/decompress is slower)
+    # algorithmic bytes per launch: compress reads N + offsets, writes C + lengths;
+    # decompress reads C + offsets, writes N + lengths (2(N+C) per round trip)
+    meta = n * (8 + 4 + 8 + 4 + 4)
+    alg_c = in_bytes + comp_bytes + meta
+    alg_d = comp_bytes + in_bytes + meta
+    dom_is_dec = t_dec >= t_comp
+    t_dom = t_dec if dom_is_dec else t_comp
+    alg = alg_d if dom_is_dec else alg_c
+    achieved = alg / t_dom / 1e9
+    roofline = {
+        "kernel": "rc_decompress_wave" if dom_is_dec else "rc_compress_wave",
+        "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": None,
+        "alg_bytes_per_launch": alg, "launch_ms": round(t_dom * 1e3, 4),
+        "compress_ms": round(t_comp * 1e3, 4), "decompress_ms": round(t_dec * 1e3, 4),
+    }
+
+    result = {
+        "metric": "GiB/s device-resident range-coder (de)compress, 64Ki×1200B pkts, 1/2/4/8 GPU",
+        "value": round(value, 4),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": {"c2": "C2 65536x1200B uniform-random, compress+decompress round trip",
+                                "c3": "C3 65536x1200B game-state, compress+decompress round trip",
+                                "c4": "C4 mixed 64-1392B random, compress+decompress round trip"}[args.workload],
+                   "packets_per_gpu": n, "packet_bytes": args.size if args.workload != "c4" else "64-1392",
+                   "parallelism": f"shard{world}", "out_cap": "2N+64"},
+        "bit_exact_roundtrip": ok,
+        "compression_ratio": round(comp_bytes / in_bytes, 5),
+        "compress_GiBps": round(in_bytes / t_comp / GIB, 4),
+        "decompress_GiBps": round(in_bytes / t_dec / GIB, 4),
+        "roofline": roofline,
+    }
+
+    if rank == 0 and world == 1 and not args.no_pcie:
+        result["pcie_inclusive"] = pcie_inclusive(coder, d, o, l, args)
+
+    if world > 1 and not args.no_rccl:
+        rs = rccl_scatter_gather(dist, dev, din, cout, clen, coff, world, rank)
+        if rank == 0:
+            result["rccl_scatter_gather"] = rs
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(d, o, l, args.cpu_threads)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    coder.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def pcie_inclusive(coder, d, o, l, args):
+    """Rate including H2D of the input and D2H of the output through pinned
+    staging (the reference path starts and ends in host memory)."""
+    from enet_amd import get_lib
+    import ctypes as C
+    lib = get_lib()
+    n = len(l)
+    cap = (2 * l.astype(np.int64) + 64).astype(np.uint32)
+    coff = np.zeros(n, np.uint64)
+    coff[1:] = np.cumsum(cap[:-1], dtype=np.uint64)
+    cout = np.zeros(int(coff[-1] + cap[-1]), np.uint8)
+    clen = np.zeros(n, np.uint32)
+    dout = np.zeros_like(d)
+    dlen = np.zeros(n, np.uint32)
+    lcap = l.astype(np.uint32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    reps = 3
+    best_c = best_d = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc = lib.enet_rc_compress_batch_host(coder.ctx, p(d), p(o), p(lcap), n, p(cout), p(coff), p(cap), p(clen))
+        t1 = time.perf_counter()
+        rc |= lib.enet_rc_decompress_batch_host(coder.ctx, p(cout), p(coff), p(clen), n, p(dout), p(o), p(lcap), p(dlen))
+        t2 = time.perf_counter()
+        assert rc == 0
+        best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
+    ok = bool(np.array_equal(dlen, lcap) and np.array_equal(dout, d))
+    nb = float(l.sum(dtype=np.uint64))
+    return {"value": round(nb / (best_c + best_d) / GIB, 4), "unit": "GiB/s",
+            "compress_GiBps": round(nb / best_c / GIB, 4), "decompress_GiBps": round(nb / best_d / GIB, 4),
+            "bit_exact": ok, "note": "host pinned staging memcpy + H2D + kernels + D2H + host memcpy, best of 3"}
+
+
+def rccl_scatter_gather(dist, dev, din, cout, clen, coff, world, rank):
+    """Times an RCCL scatter of one shard per rank from rank 0 and the gather
+    of the compressed shards back (grouped send/recv over xGMI)."""
+    import torch
+    shard = din.numel()
+    send = torch.empty(shard * world, dtype=torch.uint8, device=dev) if rank == 0 else None
+    recv = torch.empty(shard, dtype=torch.uint8, device=dev)
+    times = []
+    for it in range(4):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ops = []
+        if rank == 0:
+            for r in range(1, world):
+                ops.append(dist.P2POp(dist.isend, send[r * shard:(r + 1) * shard], r))
+            recv.copy_(send[:shard])
+        else:
+            ops.append(dist.P2POp(dist.irecv, recv, 0))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        # gather compressed payload sizes then payloads (padded to the max)
+        tot = clen.to(torch.int64).sum().view(1)
+        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(sizes, tot)
+        mx = int(max(s.item() for s in sizes))
+        buf = torch.empty(mx, dtype=torch.uint8, device=dev)
+        buf[: int(tot.item())].copy_(cout[: int(tot.item())])
+        ops = []
+        if rank == 0:
+            gathered = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world - 1)]
+            for r in range(1, world):
+                ops.append(dist.P2POp(dist.irecv, gathered[r - 1], r))
+        else:
+            ops.append(dist.P2POp(dist.isend, buf, 0))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        if it > 0:
+            times.append((t1 - t0, t2 - t1))
+    sc = min(t[0] for t in times)
+    ga = min(t[1] for t in times)
+    return {"scatter_ms": round(sc * 1e3, 3), "gather_ms": round(ga * 1e3, 3),
+            "scatter_GBps": round(shard * (world - 1) / sc / 1e9, 2),
+            "note": "rank0 -> ranks grouped isend/irecv (RCCL over xGMI), not in the timed region"}
+
+
+def cpu_baseline(d, o, l, threads):
+    """Reference compress.c (oracle/_ref, built from the reference sources) or,
+    if absent, the oracle restatement, timed round trip on host cores."""
+    from oracle.pyoracle import cpu_roundtrip, have_reference
+    kind = "reference" if have_reference() else "port"
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    n = len(l)
+    r = cpu_roundtrip(d, o, l, threads, kind=kind)
+    nb = float(l.sum(dtype=np.uint64))
+    t = r["t_compress"] + r["t_decompress"]
+    try:
+        model = [x for x in open("/proc/cpuinfo").read().splitlines() if x.startswith("model name")][0].split(":")[1].strip()
+    except Exception:
+        model = "unknown"
+    return {"value": round(nb / t / GIB, 5), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{n} packets x {int(l.max())} B (the same synthetic batch), one context per thread",
+            "compress_GiBps": round(nb / r["t_compress"] / GIB, 5),
+            "decompress_GiBps": round(nb / r["t_decompress"] / GIB, 5),
+            "mismatches": int(r["mismatches"]), "cpu": model}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,1 +1,136 @@
+"""enet_amd -- MI355X-native drop-in for ENet's range-coder packet compressor.
 
+The product is ``enet_amd/lib/libenet_rc_amd.so`` (C host shim + gfx950 HIP
+kernels, C ABI in ``include/enet_rc_amd.h``).  This Python package is a thin
+ctypes front end used by the tests and the benchmark:
+
+* :class:`RangeCoder` mirrors the reference's ``ENetCompressor`` plugin
+  (``enet_range_coder_create/compress/decompress/destroy``, enet.h:603-606):
+  same arguments, same ``0``-on-failure convention.
+* :func:`compress_batch` / :func:`decompress_batch` run whole packet batches
+  resident in device memory (torch tensors on ``cuda``), one wavefront per
+  packet.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+from ._lib import ENetBuffer, get_lib
+
+__all__ = ["RangeCoder", "compress_batch", "decompress_batch", "get_lib", "ENetBuffer"]
+
+
+class RangeCoder:
+    """One coder context: ``enet_range_coder_create`` (compress.c:48-56)."""
+
+    def __init__(self):
+        self.lib = lib = get_lib()
+        self.ctx = lib.enet_range_coder_create()
+        if not self.ctx:
+            raise RuntimeError("enet_range_coder_create failed (no usable HIP device?)")
+
+    def close(self):
+        if self.ctx:
+            self.lib.enet_range_coder_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- reference per-datagram surface (compress.c:246, :498) ---------------
+    def compress_gather(self, backing: bytes, spans: Sequence[tuple], in_limit: int, out_limit: int):
+        """Gather-list compress; ``spans`` = [(start, length)] into ``backing``.
+        Returns ``(return_value, bytes)`` like the reference call."""
+        buf = C.create_string_buffer(bytes(backing) + b"\0" * 8)
+        base = C.addressof(buf)
+        arr = (ENetBuffer * max(1, len(spans)))()
+        for i, (s, l) in enumerate(spans):
+            arr[i].data = base + s
+            arr[i].dataLength = l
+        out = C.create_string_buffer(max(1, out_limit))
+        r = self.lib.enet_range_coder_compress(self.ctx, arr, len(spans), in_limit, C.addressof(out), out_limit)
+        return int(r), out.raw[: r]
+
+    def compress(self, data: bytes, out_limit: Optional[int] = None, in_limit: Optional[int] = None):
+        if out_limit is None:
+            out_limit = 2 * len(data) + 64
+        if in_limit is None:
+            in_limit = len(data)
+        return self.compress_gather(data, [(0, len(data))], in_limit, out_limit)
+
+    def decompress(self, data: bytes, out_limit: int = 4096):
+        src = C.create_string_buffer(bytes(data) + b"\0")
+        out = C.create_string_buffer(max(1, out_limit))
+        r = self.lib.enet_range_coder_decompress(self.ctx, C.addressof(src), len(data), C.addressof(out), out_limit)
+        return int(r), out.raw[: r]
+
+    # -- batch surface ---------------------------------------------------------
+    def _batch(self, fn, inp, in_off, in_len, max_len, out, out_off, out_cap, out_len, stream):
+        import torch
+        for t in (inp, in_off, in_len, out, out_off, out_cap, out_len):
+            if not (t.is_cuda and t.is_contiguous()):
+                raise ValueError("batch tensors must be contiguous device tensors")
+        assert inp.dtype == torch.uint8 and out.dtype == torch.uint8
+        assert in_off.dtype == torch.int64 and out_off.dtype == torch.int64
+        assert in_len.dtype == torch.int32 and out_cap.dtype == torch.int32 and out_len.dtype == torch.int32
+        n = in_len.numel()
+        if stream is None:
+            stream = torch.cuda.current_stream(inp.device)
+        rc = fn(self.ctx, inp.data_ptr(), in_off.data_ptr(), in_len.data_ptr(), n, int(max_len),
+                out.data_ptr(), out_off.data_ptr(), out_cap.data_ptr(), out_len.data_ptr(),
+                C.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"enet_rc batch failed: HIP error {rc}")
+
+    def compress_batch(self, inp, in_off, in_len, out, out_off, out_cap, out_len, max_len=0, stream=None):
+        self._batch(self.lib.enet_rc_compress_batch_device, inp, in_off, in_len, max_len, out, out_off,
+                    out_cap, out_len, stream)
+
+    def decompress_batch(self, inp, in_off, in_len, out, out_off, out_cap, out_len, max_len=0, stream=None):
+        self._batch(self.lib.enet_rc_decompress_batch_device, inp, in_off, in_len, max_len, out, out_off,
+                    out_cap, out_len, stream)
+
+    def last_exact_count(self) -> int:
+        return int(self.lib.enet_rc_last_exact_count(self.ctx))
+
+
+def _caps_offsets(caps):
+    import torch
+    off = torch.zeros_like(caps, dtype=torch.int64)
+    if caps.numel() > 1:
+        off[1:] = torch.cumsum(caps[:-1].to(torch.int64), 0)
+    return off
+
+
+def compress_batch(coder: RangeCoder, inp, in_off, in_len, max_len: int, out_cap=None):
+    """Allocates outputs (default capacity 2N+64 per packet) and compresses.
+    Returns ``(out, out_off, out_cap, out_len)`` device tensors."""
+    import torch
+    if out_cap is None:
+        out_cap = (2 * in_len.to(torch.int64) + 64).to(torch.int32)
+    out_off = _caps_offsets(out_cap)
+    total = int(out_off[-1].item() + out_cap[-1].item()) if out_cap.numel() else 0
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=inp.device)
+    out_len = torch.empty_like(in_len)
+    coder.compress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, max_len)
+    return out, out_off, out_cap, out_len
+
+
+def decompress_batch(coder: RangeCoder, inp, in_off, in_len, out_cap, max_len: int = 0):
+    import torch
+    out_off = _caps_offsets(out_cap)
+    total = int(out_off[-1].item() + out_cap[-1].item()) if out_cap.numel() else 0
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=inp.device)
+    out_len = torch.empty_like(in_len)
+    coder.decompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, max_len)
+    return out, out_off, out_len

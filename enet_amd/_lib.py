@@ -1,0 +1,80 @@
+"""ctypes binding of libenet_rc_amd.so (the C ABI declared in include/enet_rc_amd.h).
+
+The library is the product: HIP kernels + C host shim.  There is no Python or
+CPU fallback; if the library is missing this module raises at import time.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+try:  # load torch's HIP runtime first so the library and torch share one runtime
+    import torch  # noqa: F401
+except ImportError:  # the C ABI itself does not need torch
+    pass
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libenet_rc_amd.so")
+HEADER = os.path.join(ROOT, "include", "enet_rc_amd.h")
+
+
+class ENetBuffer(C.Structure):
+    """include/enet/unix.h:30-34 (iovec layout)."""
+    _fields_ = [("data", C.c_void_p), ("dataLength", C.c_size_t)]
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          f"or `make -C enet_amd/csrc`")
+    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
+    lib.enet_range_coder_create.restype = vp
+    lib.enet_range_coder_create.argtypes = []
+    lib.enet_range_coder_destroy.restype = None
+    lib.enet_range_coder_destroy.argtypes = [vp]
+    lib.enet_range_coder_compress.restype = sz
+    lib.enet_range_coder_compress.argtypes = [vp, C.POINTER(ENetBuffer), sz, sz, vp, sz]
+    lib.enet_range_coder_decompress.restype = sz
+    lib.enet_range_coder_decompress.argtypes = [vp, vp, sz, vp, sz]
+    lib.enet_host_compress_with_range_coder.restype = C.c_int
+    lib.enet_host_compress_with_range_coder.argtypes = [vp]
+    batch_dev = [vp, vp, vp, vp, sz, u32, vp, vp, vp, vp, vp]
+    batch_host = [vp, vp, vp, vp, sz, vp, vp, vp, vp]
+    for name, args in (("enet_rc_compress_batch_device", batch_dev),
+                       ("enet_rc_decompress_batch_device", batch_dev),
+                       ("enet_rc_compress_batch_host", batch_host),
+                       ("enet_rc_decompress_batch_host", batch_host)):
+        f = getattr(lib, name)
+        f.restype = C.c_int
+        f.argtypes = args
+    lib.enet_rc_last_exact_count.restype = u32
+    lib.enet_rc_last_exact_count.argtypes = [vp]
+    lib.enet_rc_version.restype = C.c_char_p
+    lib.enet_rc_version.argtypes = []
+    lib.rc_hip_lds_bytes.restype = u32
+    lib.rc_hip_lds_bytes.argtypes = [u32]
+    return lib
+
+
+_LIB = None
+
+
+def get_lib() -> C.CDLL:
+    """Loads the product library on first use; raises if it is not built."""
+    global _LIB
+    if _LIB is None:
+        _LIB = _load()
+    return _LIB
+
+
+def header_symbols() -> list:
+    """Function names declared by include/enet_rc_amd.h."""
+    with open(HEADER) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", text, flags=re.M)
+    skip = {"compress", "decompress", "destroy", "if", "typedef"}
+    return sorted({n for n in names if n not in skip and not n.startswith("_")})

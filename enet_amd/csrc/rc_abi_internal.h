@@ -1,0 +1,52 @@
+/*
+ * rc_abi_internal.h -- descriptors shared by the C host shim (rc_host.c) and
+ * the HIP launch code (rc_kernels.hip).  Plain C, plain pointers.
+ */
+#ifndef ENET_RC_ABI_INTERNAL_H
+#define ENET_RC_ABI_INTERNAL_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One batch of independent packets, all pointers in device memory.
+ * packet i: in[in_off[i] .. in_off[i]+in_len[i]) -> out[out_off[i] .. +out_cap[i]);
+ * out_len[i] receives what enet_range_coder_{compress,decompress} would return. */
+typedef struct {
+    const uint8_t  *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    uint8_t        *out;
+    const uint64_t *out_off;
+    const uint32_t *out_cap;
+    uint32_t       *out_len;
+    uint32_t        n;
+    uint32_t        max_len;   /* upper bound of in_len[] used to size LDS; longer packets take the exact path */
+} rc_batch_dev;
+
+/* Device workspace owned by a coder context. */
+typedef struct {
+    uint32_t *flag_list;    /* [n_cap] packets routed to the exact path */
+    uint32_t *counters;     /* [4]: 0 = flagged count, 1 = work queue head (fast), 2 = exact queue head */
+    void     *exact_pool;   /* exact_slots * RC_EXACT_POOL_BYTES */
+    uint32_t  exact_slots;
+    uint32_t  n_cap;
+} rc_workspace_dev;
+
+#define RC_EXACT_POOL_BYTES 98304u   /* 4096 nodes x 16 B (compress.c:42-46) + 4096 x 8 B rescale frames */
+
+/* Launchers (rc_kernels.hip).  Return 0 or a hipError_t value. Stream-ordered, no host sync. */
+int rc_hip_compress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
+int rc_hip_decompress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
+
+/* Kernel introspection for bench/profiling. */
+const char *rc_hip_fast_kernel_name(int decompress);
+uint32_t    rc_hip_lds_bytes(uint32_t max_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

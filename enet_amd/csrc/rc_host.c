@@ -1,0 +1,285 @@
+/*
+ * rc_host.c -- C host side of the MI355X range coder.
+ *
+ * Implements the reference's compressor plugin surface (enet.h:323-335,
+ * :574, :603-606) on top of the HIP kernels in rc_kernels.hip:
+ *   - a coder context owns a HIP stream, a device workspace and pinned
+ *     staging;
+ *   - the per-datagram entry points run a one-packet batch on the GPU (the
+ *     gather list is flattened on the host exactly as compress.c:275-284
+ *     consumes it);
+ *   - the batch entry points hand whole packet batches to the kernels.
+ * There is no CPU coder in this library: if no HIP device is usable,
+ * enet_range_coder_create() returns NULL and the batch calls fail.
+ */
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "enet_rc_amd.h"
+#include "rc_abi_internal.h"
+
+/* ENet's allocator and host hook, resolved from libenet when it is linked
+ * (callbacks.c:37-52, host.c:294-304). */
+extern void *enet_malloc(size_t) __attribute__((weak));
+extern void enet_free(void *) __attribute__((weak));
+extern void enet_host_compress(ENetHost *, const ENetCompressor *) __attribute__((weak));
+
+#define EXACT_SLOTS 256u            /* concurrent exact-path packets (64 KiB pool each) */
+
+typedef struct {
+    int device;
+    hipStream_t stream;
+    rc_workspace_dev ws;            /* flag list sized n_cap */
+    /* device staging for host-pointer calls */
+    uint8_t *d_stage;
+    size_t d_stage_cap;
+    uint8_t *h_stage;               /* pinned */
+    size_t h_stage_cap;
+    uint32_t last_exact;
+} rc_ctx;
+
+static void *ctx_alloc(size_t n) { return enet_malloc ? enet_malloc(n) : malloc(n); }
+static void ctx_release(void *p) { if (enet_free) enet_free(p); else free(p); }
+
+static int ws_reserve(rc_ctx *c, size_t n)
+{
+    if (n <= c->ws.n_cap) return 0;
+    size_t cap = c->ws.n_cap ? c->ws.n_cap : 1024;
+    while (cap < n) cap *= 2;
+    uint32_t *fl = NULL;
+    if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) return -1;
+    if (c->ws.flag_list) {
+        hipStreamSynchronize(c->stream);
+        hipFree(c->ws.flag_list);
+    }
+    c->ws.flag_list = fl;
+    c->ws.n_cap = (uint32_t) cap;
+    return 0;
+}
+
+static int stage_reserve(rc_ctx *c, size_t bytes)
+{
+    if (bytes <= c->d_stage_cap && bytes <= c->h_stage_cap) return 0;
+    size_t cap = 1u << 16;
+    while (cap < bytes) cap *= 2;
+    hipStreamSynchronize(c->stream);
+    if (c->d_stage) hipFree(c->d_stage);
+    if (c->h_stage) hipHostFree(c->h_stage);
+    c->d_stage = NULL; c->h_stage = NULL; c->d_stage_cap = c->h_stage_cap = 0;
+    if (hipMalloc((void **) &c->d_stage, cap) != hipSuccess) return -1;
+    if (hipHostMalloc((void **) &c->h_stage, cap, 0) != hipSuccess) return -1;
+    c->d_stage_cap = c->h_stage_cap = cap;
+    return 0;
+}
+
+void *enet_range_coder_create(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return NULL;
+    rc_ctx *c = (rc_ctx *) ctx_alloc(sizeof(rc_ctx));
+    if (!c) return NULL;
+    memset(c, 0, sizeof *c);
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) goto fail;
+    if (hipMalloc((void **) &c->ws.counters, 16) != hipSuccess) goto fail;
+    c->ws.exact_slots = EXACT_SLOTS;
+    if (hipMalloc(&c->ws.exact_pool, (size_t) EXACT_SLOTS * RC_EXACT_POOL_BYTES) != hipSuccess) goto fail;
+    if (ws_reserve(c, 1024) != 0) goto fail;
+    if (stage_reserve(c, 1u << 16) != 0) goto fail;
+    return c;
+fail:
+    enet_range_coder_destroy(c);
+    return NULL;
+}
+
+void enet_range_coder_destroy(void *context)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c) return;
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->ws.flag_list) hipFree(c->ws.flag_list);
+    if (c->ws.counters) hipFree(c->ws.counters);
+    if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
+    if (c->d_stage) hipFree(c->d_stage);
+    if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->stream) hipStreamDestroy(c->stream);
+    ctx_release(c);
+}
+
+static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
+                      const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                      const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+                      void *stream)
+{
+    if (!c) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    if (ws_reserve(c, n) != 0) return (int) hipErrorOutOfMemory;
+    rc_batch_dev b;
+    b.in = in; b.in_off = in_off; b.in_len = in_len;
+    b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;
+    b.n = (uint32_t) n;
+    b.max_len = max_len;
+    return decompress ? rc_hip_decompress(&b, &c->ws, stream ? stream : (void *) c->stream)
+                      : rc_hip_compress(&b, &c->ws, stream ? stream : (void *) c->stream);
+}
+
+int enet_rc_compress_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                                  const uint32_t *in_len, size_t n, uint32_t max_len,
+                                  uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                                  uint32_t *out_len, void *stream)
+{
+    return run_device((rc_ctx *) context, 0, in, in_off, in_len, n, max_len, out, out_off,
+                      out_cap, out_len, stream);
+}
+
+int enet_rc_decompress_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                                    const uint32_t *in_len, size_t n, uint32_t max_len,
+                                    uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                                    uint32_t *out_len, void *stream)
+{
+    return run_device((rc_ctx *) context, 1, in, in_off, in_len, n, max_len, out, out_off,
+                      out_cap, out_len, stream);
+}
+
+/* Host-memory batch: [in | in_off | in_len | out_off | out_cap | out_len | out]
+ * packed into one pinned buffer, one H2D, kernels, one D2H of out_len+out. */
+static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
+                    const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
+                    const uint32_t *out_cap, uint32_t *out_len)
+{
+    if (!c) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    uint64_t in_bytes = 0, out_bytes = 0;
+    uint32_t max_len = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t e = in_off[i] + in_len[i];
+        if (e > in_bytes) in_bytes = e;
+        uint64_t f = out_off[i] + out_cap[i];
+        if (f > out_bytes) out_bytes = f;
+        if (in_len[i] > max_len) max_len = in_len[i];
+    }
+    size_t a_in = 0;
+    size_t a_ioff = (a_in + in_bytes + 15) & ~(size_t) 15;
+    size_t a_ilen = a_ioff + n * 8;
+    size_t a_ooff = (a_ilen + n * 4 + 15) & ~(size_t) 15;
+    size_t a_ocap = a_ooff + n * 8;
+    size_t a_olen = (a_ocap + n * 4 + 15) & ~(size_t) 15;
+    size_t a_out = (a_olen + n * 4 + 15) & ~(size_t) 15;
+    size_t total = a_out + out_bytes + 16;
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    if (stage_reserve(c, total) != 0) return (int) hipErrorOutOfMemory;
+    uint8_t *h = c->h_stage, *d = c->d_stage;
+    memcpy(h + a_in, in, in_bytes);
+    memcpy(h + a_ioff, in_off, n * 8);
+    memcpy(h + a_ilen, in_len, n * 4);
+    memcpy(h + a_ooff, out_off, n * 8);
+    memcpy(h + a_ocap, out_cap, n * 4);
+    hipError_t err = hipMemcpyAsync(d, h, a_olen, hipMemcpyHostToDevice, c->stream);
+    if (err != hipSuccess) return (int) err;
+    int rc = run_device(c, decompress, d + a_in, (const uint64_t *) (d + a_ioff),
+                        (const uint32_t *) (d + a_ilen), n, max_len, d + a_out,
+                        (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_ocap),
+                        (uint32_t *) (d + a_olen), NULL);
+    if (rc != 0) return rc;
+    err = hipMemcpyAsync(h + a_olen, d + a_olen, total - 16 - a_olen, hipMemcpyDeviceToHost, c->stream);
+    if (err != hipSuccess) return (int) err;
+    err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
+    if (err != hipSuccess) return (int) err;
+    err = hipStreamSynchronize(c->stream);
+    if (err != hipSuccess) return (int) err;
+    memcpy(out_len, h + a_olen, n * 4);
+    for (size_t i = 0; i < n; ++i)
+        if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
+    return 0;
+}
+
+int enet_rc_compress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                                const uint32_t *in_len, size_t n, uint8_t *out,
+                                const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
+{
+    return run_host((rc_ctx *) context, 0, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+}
+
+int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                                  const uint32_t *in_len, size_t n, uint8_t *out,
+                                  const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
+{
+    return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+}
+
+/* --------------------------------------------------------- per-datagram ABI */
+
+size_t enet_range_coder_compress(void *context, const ENetBuffer *inBuffers, size_t inBufferCount,
+                                 size_t inLimit, enet_uint8 *outData, size_t outLimit)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (c == NULL || inBufferCount <= 0 || inLimit <= 0) return 0;      /* compress.c:257-258 */
+    /* Flatten the gather list the way compress.c:275-284 walks it: the first
+     * buffer may be empty (skipped); every later buffer contributes at least
+     * one byte, its data[0], even when its length is 0. */
+    size_t total = inBuffers[0].dataLength;
+    for (size_t i = 1; i < inBufferCount; ++i)
+        total += inBuffers[i].dataLength ? inBuffers[i].dataLength : 1;
+    if (total > 0xFFFFFFFFu || outLimit > 0xFFFFFFFFu) return 0;
+    uint8_t *flat = (uint8_t *) malloc(total ? total : 1);
+    if (!flat) return 0;
+    size_t pos = 0;
+    memcpy(flat, inBuffers[0].data, inBuffers[0].dataLength);
+    pos = inBuffers[0].dataLength;
+    for (size_t i = 1; i < inBufferCount; ++i) {
+        size_t l = inBuffers[i].dataLength;
+        if (l) { memcpy(flat + pos, inBuffers[i].data, l); pos += l; }
+        else flat[pos++] = *(const uint8_t *) inBuffers[i].data;
+    }
+    uint64_t ioff = 0, ooff = 0;
+    uint32_t ilen = (uint32_t) total, ocap = (uint32_t) outLimit, olen = 0;
+    int rc = 0;
+    if (total == 0) { free(flat); return 0; }   /* only empty buffers: compress.c flushes nothing */
+    rc = enet_rc_compress_batch_host(c, flat, &ioff, &ilen, 1, outData, &ooff, &ocap, &olen);
+    free(flat);
+    return rc == 0 ? (size_t) olen : 0;
+}
+
+size_t enet_range_coder_decompress(void *context, const enet_uint8 *inData, size_t inLimit,
+                                   enet_uint8 *outData, size_t outLimit)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (c == NULL || inLimit <= 0) return 0;                             /* compress.c:513-514 */
+    if (inLimit > 0xFFFFFFFFu) return 0;
+    uint64_t ioff = 0, ooff = 0;
+    uint32_t ilen = (uint32_t) inLimit, ocap = (uint32_t) (outLimit > 0xFFFFFFFFu ? 0xFFFFFFFFu : outLimit);
+    uint32_t olen = 0;
+    int rc = enet_rc_decompress_batch_host(c, inData, &ioff, &ilen, 1, outData, &ooff, &ocap, &olen);
+    return rc == 0 ? (size_t) olen : 0;
+}
+
+int enet_host_compress_with_range_coder(ENetHost *host)
+{
+    ENetCompressor compressor;
+    if (!enet_host_compress) return -1;
+    memset(&compressor, 0, sizeof compressor);
+    compressor.context = enet_range_coder_create();
+    if (compressor.context == NULL) return -1;
+    compressor.compress = enet_range_coder_compress;
+    compressor.decompress = enet_range_coder_decompress;
+    compressor.destroy = enet_range_coder_destroy;
+    enet_host_compress(host, &compressor);
+    return 0;
+}
+
+uint32_t enet_rc_last_exact_count(void *context)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c) return 0;
+    uint32_t v = 0;
+    hipStreamSynchronize(c->stream);
+    if (hipMemcpy(&v, c->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return v;
+}
+
+const char *enet_rc_version(void) { return "enet_rc_amd 0.1 (gfx950)"; }

@@ -16,7 +16,10 @@ def pytest_configure(config):
 @pytest.fixture(scope="session", autouse=True)
 def _built_oracle():
     """The oracle library is test infrastructure; build it if missing."""
+    import subprocess
     so = os.path.join(ROOT, "oracle", "liboracle.so")
     if not os.path.exists(so):
-        import subprocess
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "oracle"])
+    lib = os.path.join(ROOT, "enet_amd", "lib", "libenet_rc_amd.so")
+    if not os.path.exists(lib):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "enet_amd", "csrc")])
