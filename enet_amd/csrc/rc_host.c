@@ -124,8 +124,8 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;
     b.n = (uint32_t) n;
     b.max_len = max_len;
-    return decompress ? rc_hip_decompress(&b, &c->ws, stream ? stream : (void *) c->stream)
-                      : rc_hip_compress(&b, &c->ws, stream ? stream : (void *) c->stream);
+    /* stream is a hipStream_t; NULL is HIP's default (null) stream */
+    return decompress ? rc_hip_decompress(&b, &c->ws, stream) : rc_hip_compress(&b, &c->ws, stream);
 }
 
 int enet_rc_compress_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
@@ -184,7 +184,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     int rc = run_device(c, decompress, d + a_in, (const uint64_t *) (d + a_ioff),
                         (const uint32_t *) (d + a_ilen), n, max_len, d + a_out,
                         (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_ocap),
-                        (uint32_t *) (d + a_olen), NULL);
+                        (uint32_t *) (d + a_olen), (void *) c->stream);
     if (rc != 0) return rc;
     err = hipMemcpyAsync(h + a_olen, d + a_olen, total - 16 - a_olen, hipMemcpyDeviceToHost, c->stream);
     if (err != hipSuccess) return (int) err;
@@ -277,7 +277,7 @@ uint32_t enet_rc_last_exact_count(void *context)
     rc_ctx *c = (rc_ctx *) context;
     if (!c) return 0;
     uint32_t v = 0;
-    hipStreamSynchronize(c->stream);
+    hipDeviceSynchronize();
     if (hipMemcpy(&v, c->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
     return v;
 }
