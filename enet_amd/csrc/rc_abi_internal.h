@@ -34,13 +34,23 @@ typedef struct {
     void     *exact_pool;   /* exact_slots * RC_EXACT_POOL_BYTES */
     uint32_t  exact_slots;
     uint32_t  n_cap;
+    void     *lane_pool;    /* lane_slots * lane_region bytes: per-lane order-1/2 model regions */
+    uint32_t  lane_slots;   /* lanes with a region (multiple of 256) */
+    uint32_t  lane_region;  /* bytes per region */
+    uint32_t  kernel;       /* RC_KERNEL_* */
 } rc_workspace_dev;
+
+#define RC_KERNEL_LANE 0u   /* one packet per lane (default) */
+#define RC_KERNEL_WAVE 1u   /* one packet per wavefront */
 
 #define RC_EXACT_POOL_BYTES 98304u   /* 4096 nodes x 16 B (compress.c:42-46) + 4096 x 8 B rescale frames */
 
 /* Launchers (rc_kernels.hip).  Return 0 or a hipError_t value. Stream-ordered, no host sync. */
 int rc_hip_compress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
 int rc_hip_decompress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
+
+/* Per-lane region size the lane kernels need for packets up to max_len bytes. */
+uint32_t rc_hip_lane_region_bytes(uint32_t max_len);
 
 /* Kernel introspection for bench/profiling. */
 const char *rc_hip_fast_kernel_name(int decompress);

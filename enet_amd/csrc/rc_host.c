@@ -60,6 +60,27 @@ static int ws_reserve(rc_ctx *c, size_t n)
     return 0;
 }
 
+/* Per-lane model regions for the lane kernels: one per packet in flight
+ * (at most one per lane of a full chip wave set; larger batches loop). */
+#define MAX_LANE_SLOTS 65536u
+
+static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
+{
+    uint32_t region = rc_hip_lane_region_bytes(max_len ? max_len : 4096);
+    size_t slots = n < MAX_LANE_SLOTS ? n : MAX_LANE_SLOTS;
+    slots = (slots + 255) & ~(size_t) 255;
+    if (slots <= c->ws.lane_slots && region <= c->ws.lane_region) return 0;
+    if (slots < c->ws.lane_slots) slots = c->ws.lane_slots;
+    if (region < c->ws.lane_region) region = c->ws.lane_region;
+    hipDeviceSynchronize();
+    if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
+    c->ws.lane_pool = NULL; c->ws.lane_slots = 0; c->ws.lane_region = 0;
+    if (hipMalloc(&c->ws.lane_pool, slots * (size_t) region) != hipSuccess) return -1;
+    c->ws.lane_slots = (uint32_t) slots;
+    c->ws.lane_region = region;
+    return 0;
+}
+
 static int stage_reserve(rc_ctx *c, size_t bytes)
 {
     if (bytes <= c->d_stage_cap && bytes <= c->h_stage_cap) return 0;
@@ -88,6 +109,10 @@ void *enet_range_coder_create(void)
     c->ws.exact_slots = EXACT_SLOTS;
     if (hipMalloc(&c->ws.exact_pool, (size_t) EXACT_SLOTS * RC_EXACT_POOL_BYTES) != hipSuccess) goto fail;
     if (ws_reserve(c, 1024) != 0) goto fail;
+    {
+        const char *k = getenv("ENET_RC_KERNEL");
+        c->ws.kernel = (k && strcmp(k, "wave") == 0) ? RC_KERNEL_WAVE : RC_KERNEL_LANE;
+    }
     if (stage_reserve(c, 1u << 16) != 0) goto fail;
     return c;
 fail:
@@ -103,6 +128,7 @@ void enet_range_coder_destroy(void *context)
     if (c->ws.flag_list) hipFree(c->ws.flag_list);
     if (c->ws.counters) hipFree(c->ws.counters);
     if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
+    if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
     if (c->d_stage) hipFree(c->d_stage);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -119,6 +145,7 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     if (n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
     if (ws_reserve(c, n) != 0) return (int) hipErrorOutOfMemory;
+    if (c->ws.kernel == RC_KERNEL_LANE && lanes_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
     rc_batch_dev b;
     b.in = in; b.in_off = in_off; b.in_len = in_len;
     b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;

@@ -1041,9 +1041,12 @@ uint32_t lds_bytes_for(uint32_t max_len)
 
 extern "C" uint32_t rc_hip_lds_bytes(uint32_t max_len) { return lds_bytes_for(max_len); }
 
+extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
+                                  void* stream);   // rc_lane.hip
+
 extern "C" const char* rc_hip_fast_kernel_name(int decompress)
 {
-    return decompress ? "rc_decompress_wave" : "rc_compress_wave";
+    return decompress ? "rc_decompress_lane" : "rc_compress_lane";
 }
 
 static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
@@ -1053,18 +1056,23 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     if (b->n > ws->n_cap) return static_cast<int>(hipErrorInvalidValue);
     hipError_t err = hipMemsetAsync(ws->counters, 0, 4 * sizeof(uint32_t), st);
     if (err != hipSuccess) return static_cast<int>(err);
-    uint32_t max_len = b->max_len ? b->max_len : 4096;
-    uint32_t stage = stage_bytes_for(max_len);
-    uint32_t lds = lds_bytes_for(max_len);
-    if (stage + kInStage + 4096 > lds) {            // absurd max_len: everything goes exact
-        stage = 16; lds = 16384;
+    if (ws->kernel == RC_KERNEL_LANE) {
+        const int rc = rc_hip_lane_launch(decompress ? 1 : 0, b, ws, stream);
+        if (rc != 0) return rc;
+    } else {
+        uint32_t max_len = b->max_len ? b->max_len : 4096;
+        uint32_t stage = stage_bytes_for(max_len);
+        uint32_t lds = lds_bytes_for(max_len);
+        if (stage + kInStage + 4096 > lds) {        // absurd max_len: everything goes exact
+            stage = 16; lds = 16384;
+        }
+        if (decompress)
+            hipLaunchKernelGGL(rc_decompress_wave, dim3(b->n), dim3(64), lds, st, *b, *ws, stage, lds);
+        else
+            hipLaunchKernelGGL(rc_compress_wave, dim3(b->n), dim3(64), lds, st, *b, *ws, stage, lds);
+        err = hipGetLastError();
+        if (err != hipSuccess) return static_cast<int>(err);
     }
-    if (decompress)
-        hipLaunchKernelGGL(rc_decompress_wave, dim3(b->n), dim3(64), lds, st, *b, *ws, stage, lds);
-    else
-        hipLaunchKernelGGL(rc_compress_wave, dim3(b->n), dim3(64), lds, st, *b, *ws, stage, lds);
-    err = hipGetLastError();
-    if (err != hipSuccess) return static_cast<int>(err);
     const uint32_t blocks = ws->exact_slots / 64 ? ws->exact_slots / 64 : 1;
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_exact, dim3(blocks), dim3(64), 0, st, *b, *ws);

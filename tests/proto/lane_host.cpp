@@ -1,0 +1,25 @@
+// TEST ONLY: host build of rc_lane.hip's per-lane compress/decompress.
+#define RC_LANE_HOST_TEST 1
+#include <stdlib.h>
+#include <string.h>
+#include "../../enet_amd/csrc/rc_lane.hip"
+
+static uint8_t g_root[304] __attribute__((aligned(16)));
+
+extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t cap,
+                             uint32_t max_len, uint32_t* out_len)
+{
+    static uint8_t* region = nullptr;
+    static uint32_t region_bytes = 0;
+    uint32_t need = rc_hip_lane_region_bytes(max_len);
+    if (need > region_bytes) { free(region); region = (uint8_t*) aligned_alloc(256, need); region_bytes = need; }
+    uint64_t ioff = 0, ooff = 0;
+    uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0};
+    rc_batch_dev b = { in, &ioff, &len, out, &ooff, &cap, out_len, 1, max_len };
+    rc_workspace_dev ws = {};
+    ws.flag_list = flags; ws.counters = counters; ws.lane_region = need; ws.lane_pool = region;
+    *out_len = 0xFFFFFFFFu;
+    if (decompress) decompress_one(b, ws, 0, region, g_root);
+    else compress_one(b, ws, 0, region, g_root);
+    return counters[0] ? 1 : 0;   // 1 = routed to the exact path
+}

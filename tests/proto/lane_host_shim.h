@@ -1,0 +1,21 @@
+/* TEST ONLY: lets tests/proto/lane_host.cpp compile the per-lane logic of
+ * enet_amd/csrc/rc_lane.hip for the host, to check it against the golden
+ * fixtures without a GPU.  Never part of the product library. */
+#pragma once
+#include <stdint.h>
+#include <algorithm>
+#define __device__
+#define __forceinline__ inline
+struct uint4 { uint32_t x, y, z, w; };
+inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
+inline uint32_t host_sad_u8(uint32_t a, uint32_t b, uint32_t acc)
+{
+    for (int i = 0; i < 4; ++i) {
+        int x = (a >> (8 * i)) & 0xFF, y = (b >> (8 * i)) & 0xFF;
+        acc += (uint32_t) (x > y ? x - y : y - x);
+    }
+    return acc;
+}
+#define __builtin_amdgcn_sad_u8 host_sad_u8
+using std::min;
+inline uint32_t atomicAdd(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
