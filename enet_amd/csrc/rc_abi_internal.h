@@ -38,6 +38,7 @@ typedef struct {
     uint32_t  lane_slots;   /* lanes with a region (multiple of 256) */
     uint32_t  lane_region;  /* bytes per region */
     uint32_t  kernel;       /* RC_KERNEL_* */
+    uint32_t  lane_active;  /* lane kernels: packets per wavefront (64, 32 or 16) */
 } rc_workspace_dev;
 
 #define RC_KERNEL_LANE 0u   /* one packet per lane (default) */

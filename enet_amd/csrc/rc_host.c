@@ -112,6 +112,9 @@ void *enet_range_coder_create(void)
     {
         const char *k = getenv("ENET_RC_KERNEL");
         c->ws.kernel = (k && strcmp(k, "wave") == 0) ? RC_KERNEL_WAVE : RC_KERNEL_LANE;
+        const char *a = getenv("ENET_RC_LANES");
+        c->ws.lane_active = 64;
+        if (a && (atoi(a) == 32 || atoi(a) == 16)) c->ws.lane_active = (uint32_t) atoi(a);
     }
     if (stage_reserve(c, 1u << 16) != 0) goto fail;
     return c;

@@ -53,9 +53,6 @@ constexpr uint32_t kTotalLimit = kBot - 0x100;
 
 constexpr uint32_t kBlock = 256;             // lanes (packets) per workgroup
 constexpr uint32_t kRootStride = 304;        // LDS bytes per lane; 76 dwords (76/4 odd: b128 conflict-free)
-constexpr uint32_t kO1Rec = 64, kO1Inl = 12, kO1MinLog = 5;   // ext blocks start at 32 entries
-constexpr uint32_t kO2Rec = 32, kO2Inl = 4, kO2MinLog = 3;    // ext blocks start at 8 entries
-constexpr uint32_t kArenaBase = 256 * kO1Rec;                 // order-2 records + ext blocks follow
 
 DEV uint32_t val_of(uint32_t e) { return e & 0xFF; }
 DEV uint32_t cnt_of(uint32_t e) { return (e >> 8) & 0xFF; }
@@ -157,83 +154,135 @@ DEV uint32_t root_rescale(uint8_t* r)
 }
 
 // ---------------------------------------------------- order 1/2 records (HBM)
+// o1 record, 64 B, direct-mapped by the context byte:
+//     w0 = esc | len << 16, w1 = ext offset (0 = entries inline), 14 inline entries
+// o2 record, 8 B, bump-allocated so that the records touched by consecutive
+//     steps share HBM sectors:
+//     w0 = esc | len << 16, w1 = the only entry while len <= 1, else ext offset
+// entry = value | count << 8 | link << 16, link = o2 record index (offset / 8):
+//     in an o1 entry the context (prev, value); in an o2 entry the suffix
+//     context (compress.c's `parent`, :294-295, :615).
+// total is not stored: total = esc + sum(counts) holds after every update of
+// compress.c (:309-312) and every rescale (:107-112).  A freshly allocated o2
+// record is never zero-filled or loaded: its first visit is the very next
+// step, which knows it is empty.
+
+constexpr uint32_t kO1Rec = 64, kO1Inl = 14, kO1MinCap = 32;
+constexpr uint32_t kO2Rec = 8, kO2Inl = 1, kO2MinCap = 4;
+constexpr uint32_t kArenaBase = 256 * kO1Rec;
 
 template <uint32_t INL>
-struct Rec {
-    uint32_t off, esc, tot, len, extlog, ext;
-    uint32_t e[INL];
-};
+struct Rec { uint32_t off, esc, len, ext; uint32_t e[INL]; };
 
-struct Hit { uint32_t k, under, cnt, link, val; bool found; };
+struct Hit { uint32_t k, under, cnt, link, val, tot; bool found; };
 
-template <uint32_t INL>
-DEV void rec_load(const uint8_t* reg, uint32_t off, Rec<INL>& r)
+DEV uint32_t cap_for(uint32_t len, uint32_t mincap)
 {
-    const uint4* p = reinterpret_cast<const uint4*>(reg + off);
-    const uint4 h = p[0];
-    r.off = off;
-    r.esc = h.x & 0xFFFF; r.tot = h.x >> 16;
-    r.len = h.y & 0xFFFF; r.extlog = h.y >> 16;
-    r.ext = h.z;
-#pragma unroll
-    for (uint32_t c = 0; c < INL / 4; ++c) {
-        const uint4 q = p[1 + c];
-        r.e[4 * c] = q.x; r.e[4 * c + 1] = q.y; r.e[4 * c + 2] = q.z; r.e[4 * c + 3] = q.w;
-    }
+    return len <= mincap ? mincap : (1u << (32 - __builtin_clz(len - 1)));
 }
 
-template <uint32_t INL>
-DEV void rec_store(uint8_t* reg, const Rec<INL>& r)
+DEV void o1_load(const uint8_t* reg, uint32_t x, Rec<kO1Inl>& r)
+{
+    const uint4* p = reinterpret_cast<const uint4*>(reg + x * kO1Rec);
+    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    r.off = x * kO1Rec; r.esc = q0.x & 0xFFFF; r.len = q0.x >> 16; r.ext = q0.y;
+    r.e[0] = q0.z; r.e[1] = q0.w;
+    r.e[2] = q1.x; r.e[3] = q1.y; r.e[4] = q1.z; r.e[5] = q1.w;
+    r.e[6] = q2.x; r.e[7] = q2.y; r.e[8] = q2.z; r.e[9] = q2.w;
+    r.e[10] = q3.x; r.e[11] = q3.y; r.e[12] = q3.z; r.e[13] = q3.w;
+}
+
+DEV void o1_store(uint8_t* reg, const Rec<kO1Inl>& r)
 {
     uint4* p = reinterpret_cast<uint4*>(reg + r.off);
-    p[0] = make_uint4(r.esc | (r.tot << 16), r.len | (r.extlog << 16), r.ext, 0u);
+    p[0] = make_uint4(r.esc | (r.len << 16), r.ext, r.e[0], r.e[1]);
     if (r.ext == 0) {
-#pragma unroll
-        for (uint32_t c = 0; c < INL / 4; ++c)
-            p[1 + c] = make_uint4(r.e[4 * c], r.e[4 * c + 1], r.e[4 * c + 2], r.e[4 * c + 3]);
+        p[1] = make_uint4(r.e[2], r.e[3], r.e[4], r.e[5]);
+        p[2] = make_uint4(r.e[6], r.e[7], r.e[8], r.e[9]);
+        p[3] = make_uint4(r.e[10], r.e[11], r.e[12], r.e[13]);
     }
 }
 
-// Encoder-side lookup of v: k = first entry >= v, under = counts below, found/cnt/link.
+DEV void o2_load(const uint8_t* reg, uint32_t idx, Rec<kO2Inl>& r)
+{
+    const uint2 q = *reinterpret_cast<const uint2*>(reg + idx * kO2Rec);
+    r.off = idx * kO2Rec; r.esc = q.x & 0xFFFF; r.len = q.x >> 16;
+    r.ext = r.len >= 2 ? q.y : 0u;
+    r.e[0] = r.len >= 2 ? 0u : q.y;
+}
+
+DEV void o2_fresh(uint32_t idx, Rec<kO2Inl>& r)
+{
+    r.off = idx * kO2Rec; r.esc = 0; r.len = 0; r.ext = 0; r.e[0] = 0;
+}
+
+DEV void o2_store(uint8_t* reg, const Rec<kO2Inl>& r)
+{
+    *reinterpret_cast<uint2*>(reg + r.off) = make_uint2(r.esc | (r.len << 16), r.ext ? r.ext : r.e[0]);
+}
+
+// Encoder-side lookup of v (compress.c:159-199, minimum 0): k = first entry >= v,
+// under = counts below, found/cnt/link, tot = esc + all counts (before update).
 template <uint32_t INL>
 DEV Hit rec_find(const uint8_t* reg, const Rec<INL>& r, uint32_t v)
 {
-    Hit h = { 0u, 0u, 0u, 0u, v, false };
+    Hit h = { 0u, 0u, 0u, 0u, v, 0u, false };
+    uint32_t sum = 0;
     if (r.ext == 0) {
 #pragma unroll
         for (uint32_t t = 0; t < INL; ++t) {
             const uint32_t e = r.e[t];
             const bool in = t < r.len;
+            const uint32_t c = in ? cnt_of(e) : 0u;
             const bool lt = in && val_of(e) < v;
             const bool eq = in && val_of(e) == v;
-            h.under += lt ? cnt_of(e) : 0u;
+            sum += c;
+            h.under += lt ? c : 0u;
             h.k += lt ? 1u : 0u;
             h.found = h.found || eq;
-            h.cnt = eq ? cnt_of(e) : h.cnt;
+            h.cnt = eq ? c : h.cnt;
             h.link = eq ? (e >> 16) : h.link;
         }
     } else {
         const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-        for (uint32_t c = 0; c < r.len; c += 4) {
-            const uint4 q = *reinterpret_cast<const uint4*>(ep + c);
-            bool stop = false;
+        for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
+            const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
 #pragma unroll
             for (uint32_t t = 0; t < 4; ++t) {
                 const uint32_t e = pick4(t, q);
-                const bool in = c + t < r.len && !stop;
+                const bool in = c0 + t < r.len;
+                const uint32_t c = in ? cnt_of(e) : 0u;
                 const bool lt = in && val_of(e) < v;
                 const bool eq = in && val_of(e) == v;
-                h.under += lt ? cnt_of(e) : 0u;
+                sum += c;
+                h.under += lt ? c : 0u;
                 h.k += lt ? 1u : 0u;
                 h.found = h.found || eq;
-                h.cnt = eq ? cnt_of(e) : h.cnt;
+                h.cnt = eq ? c : h.cnt;
                 h.link = eq ? (e >> 16) : h.link;
-                stop = stop || (in && !lt);
             }
-            if (stop) break;
         }
     }
+    h.tot = (r.esc + sum) & 0xFFFF;
     return h;
+}
+
+template <uint32_t INL>
+DEV uint32_t rec_total(const uint8_t* reg, const Rec<INL>& r)
+{
+    uint32_t sum = 0;
+    if (r.ext == 0) {
+#pragma unroll
+        for (uint32_t t = 0; t < INL; ++t) sum += t < r.len ? cnt_of(r.e[t]) : 0u;
+    } else {
+        const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
+        for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
+            const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) sum += c0 + t < r.len ? cnt_of(pick4(t, q)) : 0u;
+        }
+    }
+    return (r.esc + sum) & 0xFFFF;
 }
 
 // Decoder search (compress.c:373-416, minimum 0): entry whose interval holds code.
@@ -276,7 +325,7 @@ DEV bool rec_search(const uint8_t* reg, const Rec<INL>& r, uint32_t code, Hit& h
     return found;
 }
 
-// count[k] += d (old count `cnt`)
+// count[k] = cnt + d
 template <uint32_t INL>
 DEV void rec_bump(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t cnt, uint32_t d)
 {
@@ -288,8 +337,8 @@ DEV void rec_bump(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t cnt, uint32_t 
     }
 }
 
-// Insert entry `ne` at position k; grows into a (bigger) extension block when full.
-template <uint32_t INL, uint32_t MINLOG>
+// Insert entry `ne` at position k; moves to / grows an extension block when full.
+template <uint32_t INL, uint32_t MINCAP>
 DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t& bump, uint32_t end)
 {
     if (r.ext == 0 && r.len < INL) {
@@ -299,16 +348,16 @@ DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t
             r.e[t] = (static_cast<uint32_t>(t) > k) ? prev : (static_cast<uint32_t>(t) == k ? ne : r.e[t]);
         }
     } else {
-        const uint32_t cap = r.ext ? (1u << r.extlog) : INL;
-        if (r.len < cap) {
+        const uint32_t cap = r.ext ? cap_for(r.len, MINCAP) : INL;
+        if (r.ext != 0 && r.len < cap) {
             uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
             for (uint32_t j = r.len; j > k; --j) ep[j] = ep[j - 1];
             ep[k] = ne;
         } else {
-            const uint32_t nlog = r.ext ? r.extlog + 1 : MINLOG;
-            const uint32_t bytes = 4u << nlog;
-            if (bump + bytes > end) return false;
-            uint32_t* np = reinterpret_cast<uint32_t*>(reg + bump);
+            const uint32_t ncap = r.ext ? 2 * cap : MINCAP;
+            const uint32_t at = (bump + 15) & ~15u;
+            if (at + 4 * ncap > end) return false;
+            uint32_t* np = reinterpret_cast<uint32_t*>(reg + at);
             if (r.ext == 0) {
 #pragma unroll
                 for (uint32_t t = 0; t < INL; ++t) np[t + (t >= k ? 1u : 0u)] = r.e[t];
@@ -317,16 +366,15 @@ DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t
                 for (uint32_t j = 0; j < r.len; ++j) np[j + (j >= k ? 1u : 0u)] = ep[j];
             }
             np[k] = ne;
-            r.ext = bump;
-            r.extlog = nlog;
-            bump += bytes;
+            r.ext = at;
+            bump = at + 4 * ncap;
         }
     }
     r.len += 1;
     return true;
 }
 
-// Set the link of entry k (an order-2 entry created before its suffix was known).
+// Link of entry k (an o2 entry created before its suffix context was known).
 template <uint32_t INL>
 DEV void rec_set_link(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t link)
 {
@@ -342,82 +390,154 @@ DEV void rec_set_link(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t link)
 template <uint32_t INL>
 DEV void rec_rescale(uint8_t* reg, Rec<INL>& r)
 {
-    uint32_t sum = 0;
     if (r.ext == 0) {
 #pragma unroll
         for (uint32_t t = 0; t < INL; ++t) {
             const uint32_t e = r.e[t];
             uint32_t c = cnt_of(e);
             c -= c >> 1;
-            const bool in = t < r.len;
-            sum += in ? c : 0u;
-            r.e[t] = in ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
+            r.e[t] = t < r.len ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
         }
     } else {
         uint8_t* ep = reg + r.ext;
         for (uint32_t j = 0; j < r.len; ++j) {
             uint32_t c = ep[4 * j + 1];
-            c -= c >> 1;
-            ep[4 * j + 1] = static_cast<uint8_t>(c);
-            sum += c;
+            ep[4 * j + 1] = static_cast<uint8_t>(c - (c >> 1));
         }
     }
     r.esc -= r.esc >> 1;
-    r.tot = (sum + r.esc) & 0xFFFF;
 }
 
 // Encoder-side update of a sub-context (compress.c:293-314, patch :603-613):
-// find or insert v; returns the hit (old count, cum below, link).  `newlink`
-// is the link of an inserted entry.
-DEV uint32_t new_o2(uint8_t* reg, uint32_t& bump, uint32_t end, bool& ovf);
-
-// ALLOC: an inserted entry gets a fresh order-2 record as its link (order-1
-// contexts); otherwise its link is filled in later (order-2 contexts).
-template <uint32_t INL, uint32_t MINLOG, bool ALLOC>
+// find or insert v.  Returns the hit: old count (0 if new), cum below, total
+// before the update, and the entry's link.  ALLOC: an inserted entry gets a
+// fresh o2 record (order-1 contexts); otherwise its link is set later.
+template <uint32_t INL, uint32_t MINCAP, bool ALLOC>
 DEV Hit sub_update(uint8_t* reg, Rec<INL>& r, uint32_t v, uint32_t& bump,
                    uint32_t end, uint32_t& nodes, bool& ovf)
 {
     Hit h = rec_find(reg, r, v);
+    uint32_t tot = h.tot;
     if (h.found) {
         rec_bump(reg, r, h.k, h.cnt, kSubDelta);
     } else {
         uint32_t newlink = 0;
-        if (ALLOC) { newlink = new_o2(reg, bump, end, ovf); if (ovf) return h; }
-        if (!rec_insert<INL, MINLOG>(reg, r, h.k, v | (kSubDelta << 8) | (newlink << 16), bump, end)) {
+        if (ALLOC) {
+            if (bump + kO2Rec > end) { ovf = true; return h; }
+            newlink = bump / kO2Rec;
+            bump += kO2Rec;
+        }
+        if (!rec_insert<INL, MINCAP>(reg, r, h.k, v | (kSubDelta << 8) | (newlink << 16), bump, end)) {
             ovf = true;
             return h;
         }
         h.link = newlink;
         ++nodes;
         r.esc += kSubEscDelta;
-        r.tot += kSubEscDelta;
+        tot += kSubEscDelta;
     }
-    r.tot = (r.tot + kSubDelta) & 0xFFFF;
-    if (h.cnt > 0xFF - 2 * kSubDelta || r.tot > kTotalLimit) rec_rescale(reg, r);
+    tot = (tot + kSubDelta) & 0xFFFF;
+    if (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit) rec_rescale(reg, r);
     return h;
 }
 
 DEV void region_reset(uint8_t* reg, uint8_t* root)
 {
     root_clear(root);
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t x = 0; x < 256; ++x) *reinterpret_cast<uint4*>(reg + x * kO1Rec) = z;
+    for (uint32_t x = 0; x < 256; ++x) *reinterpret_cast<uint2*>(reg + x * kO1Rec) = make_uint2(0u, 0u);
 }
 
-DEV uint32_t new_o2(uint8_t* reg, uint32_t& bump, uint32_t end, bool& ovf)
+// ------------------------------------------------------- byte streams (HBM)
+// Each lane walks its own packet.  Byte-wide loads/stores would cost a 64-B
+// sector transfer per byte (a lane's line is evicted between steps under
+// 65536-way interleaving), so bytes move through 16-B register windows:
+// one aligned dwordx4 load / store per 16 bytes; packet edges fall back to
+// byte accesses so nothing outside [p, p+len) is read or written.
+
+DEV uint32_t win_get(const uint4& w, uint32_t i) { return (pick4(i >> 2, w) >> (8 * (i & 3))) & 0xFF; }
+
+DEV void win_set(uint4& w, uint32_t i, uint32_t b)
 {
-    if (bump + kO2Rec > end) { ovf = true; return 0; }
-    const uint32_t off = bump;
-    *reinterpret_cast<uint4*>(reg + off) = make_uint4(0u, 0u, 0u, 0u);
-    bump += kO2Rec;
-    return off / 32;
+    const uint32_t sh = 8 * (i & 3), d = i >> 2, m = ~(0xFFu << sh), x = b << sh;
+    w.x = d == 0 ? ((w.x & m) | x) : w.x;
+    w.y = d == 1 ? ((w.y & m) | x) : w.y;
+    w.z = d == 2 ? ((w.z & m) | x) : w.z;
+    w.w = d == 3 ? ((w.w & m) | x) : w.w;
+}
+
+DEV uint4 chunk_load(const uint8_t* lo, const uint8_t* hi, uintptr_t c)
+{
+    if (c >= reinterpret_cast<uintptr_t>(lo) && c + 16 <= reinterpret_cast<uintptr_t>(hi))
+        return *reinterpret_cast<const uint4*>(c);
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t t = 0; t < 16; ++t) {
+        const uintptr_t a = c + t;
+        if (a >= reinterpret_cast<uintptr_t>(lo) && a < reinterpret_cast<uintptr_t>(hi))
+            win_set(w, t, *reinterpret_cast<const uint8_t*>(a));
+    }
+    return w;
+}
+
+// sequential reader of [p, p+len); bytes past the end read as 0 (compress.c:366-367)
+struct InWin { const uint8_t* p; uint32_t len, pos; uint4 cur, nxt; };
+
+DEV void inwin_init(InWin& s, const uint8_t* p, uint32_t len)
+{
+    s.p = p; s.len = len; s.pos = 0;
+    const uintptr_t c = reinterpret_cast<uintptr_t>(p) & ~static_cast<uintptr_t>(15);
+    s.cur = chunk_load(p, p + len, c);
+    s.nxt = chunk_load(p, p + len, c + 16);
+}
+
+DEV uint32_t inwin_take(InWin& s)
+{
+    if (s.pos >= s.len) return 0;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(s.p) + s.pos;
+    const uint32_t b = win_get(s.cur, a & 15);
+    ++s.pos;
+    if ((a & 15) == 15) {                 // advance; prefetch the chunk after next
+        s.cur = s.nxt;
+        s.nxt = chunk_load(s.p, s.p + s.len, (a & ~static_cast<uintptr_t>(15)) + 32);
+    }
+    return b;
+}
+
+struct OutWin { uint8_t* p; uint32_t cap, n; uint4 w; };
+
+DEV void outwin_edge(uint8_t* p, uint32_t n, uintptr_t c, const uint4& w)
+{
+    for (uint32_t t = 0; t < 16; ++t) {
+        const uintptr_t a = c + t;
+        if (a >= reinterpret_cast<uintptr_t>(p) && a < reinterpret_cast<uintptr_t>(p) + n)
+            *reinterpret_cast<uint8_t*>(a) = static_cast<uint8_t>(win_get(w, t));
+    }
+}
+
+// caller guarantees n < cap
+DEV void outwin_put(OutWin& o, uint32_t byte)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(o.p) + o.n;
+    win_set(o.w, a & 15, byte);
+    ++o.n;
+    if ((a & 15) == 15) {
+        const uintptr_t c = a & ~static_cast<uintptr_t>(15);
+        if (c >= reinterpret_cast<uintptr_t>(o.p)) *reinterpret_cast<uint4*>(c) = o.w;
+        else outwin_edge(o.p, o.n, c, o.w);
+    }
+}
+
+DEV void outwin_finish(OutWin& o)
+{
+    if (o.n == 0) return;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(o.p) + o.n - 1;
+    if ((a & 15) != 15) outwin_edge(o.p, o.n, a & ~static_cast<uintptr_t>(15), o.w);
 }
 
 // ------------------------------------------------------------- range coder
 
 // compress.c:121-137; false = output full
 DEV bool enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total,
-                  uint8_t* op, uint32_t& n, uint32_t cap)
+                  OutWin& o)
 {
     range /= total;
     low += under * range;
@@ -427,25 +547,15 @@ DEV bool enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count
             if (range >= kBot) return true;
             range = (0u - low) & (kBot - 1);
         }
-        if (n >= cap) return false;
-        op[n++] = static_cast<uint8_t>(low >> 24);
+        if (o.n >= o.cap) return false;
+        outwin_put(o, low >> 24);
         range <<= 8;
         low <<= 8;
     }
 }
 
-struct DecIn { const uint8_t* p; uint32_t pos, len, nb; };
-
-DEV uint32_t din_take(DecIn& d)
-{
-    const uint32_t b = d.nb;
-    if (d.pos < d.len) ++d.pos;
-    d.nb = d.pos < d.len ? d.p[d.pos] : 0u;
-    return b;
-}
-
 // compress.c:354-371
-DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count, DecIn& in)
+DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count, InWin& in)
 {
     low += under * range;
     range *= count;
@@ -454,7 +564,7 @@ DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under
             if (range >= kBot) break;
             range = (0u - low) & (kBot - 1);
         }
-        code = (code << 8) | din_take(in);
+        code = (code << 8) | inwin_take(in);
         range <<= 8;
         low <<= 8;
     }
@@ -474,52 +584,53 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     const uint32_t len = b.in_len[pkt];
     const uint32_t cap = b.out_cap[pkt];
     if (len == 0) { b.out_len[pkt] = 0; return; }                   // compress.c:257
-    const uint8_t* ip = b.in + b.in_off[pkt];
-    uint8_t* op = b.out + b.out_off[pkt];
+    InWin in;
+    inwin_init(in, b.in + b.in_off[pkt], len);
+    OutWin o = { b.out + b.out_off[pkt], cap, 0u, make_uint4(0u, 0u, 0u, 0u) };
     const uint32_t end = ws.lane_region;
 
     region_reset(reg, root);
     uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1;
     uint32_t order = 0, b1 = 0, c2 = 0;
-    uint32_t low = 0, range = ~0u, n = 0;
+    bool c2fresh = false;
+    uint32_t low = 0, range = ~0u;
     bool ok = true, ovf = false;
-    uint32_t nv = ip[0];
 
     for (uint32_t i = 0; i < len; ++i) {
-        const uint32_t v = nv;
-        if (i + 1 < len) nv = ip[i + 1];
-        bool done = false, pend = false;
+        const uint32_t v = inwin_take(in);
+        bool done = false, pend = false, nfresh = false;
         uint32_t nxt = 0, kpend = 0;
         Rec<kO2Inl> r2;
         Rec<kO1Inl> r1;
-        if (order >= 2) rec_load(reg, c2 * 32, r2);
-        if (order >= 1) rec_load(reg, b1 * kO1Rec, r1);
+        if (order >= 2) { if (c2fresh) o2_fresh(c2, r2); else o2_load(reg, c2, r2); }
+        if (order >= 1) o1_load(reg, b1, r1);
 
         if (order >= 2) {                                            // order 2, compress.c:286-316
-            const uint32_t esc0 = r2.esc, tot0 = r2.tot;
-            const Hit h = sub_update<kO2Inl, kO2MinLog, false>(reg, r2, v, bump, end, nodes, ovf);
+            const uint32_t esc0 = r2.esc;
+            const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf);
             if (ovf) break;
             if (h.found) {
-                rec_store(reg, r2);
-                ok = enc_code(low, range, esc0 + h.under, h.cnt, tot0, op, n, cap);
+                o2_store(reg, r2);
+                ok = enc_code(low, range, esc0 + h.under, h.cnt, h.tot, o);
                 nxt = h.link;
                 done = true;
             } else {
                 pend = true;
                 kpend = h.k;
-                if (esc0 > 0 && esc0 < tot0) ok = enc_code(low, range, 0, esc0, tot0, op, n, cap);
+                if (esc0 > 0 && esc0 < h.tot) ok = enc_code(low, range, 0, esc0, h.tot, o);
             }
             if (!ok) break;
         }
         if (!done && order >= 1) {                                   // order 1
-            const uint32_t esc0 = r1.esc, tot0 = r1.tot;
-            const Hit h = sub_update<kO1Inl, kO1MinLog, true>(reg, r1, v, bump, end, nodes, ovf);
+            const uint32_t esc0 = r1.esc;
+            const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf);
             if (ovf) break;
-            rec_store(reg, r1);
+            o1_store(reg, r1);
             nxt = h.link;
-            if (pend) { rec_set_link(reg, r2, kpend, nxt); rec_store(reg, r2); }
-            if (h.found) { ok = enc_code(low, range, esc0 + h.under, h.cnt, tot0, op, n, cap); done = true; }
-            else if (esc0 > 0 && esc0 < tot0) ok = enc_code(low, range, 0, esc0, tot0, op, n, cap);
+            nfresh = !h.found;
+            if (pend) { rec_set_link(reg, r2, kpend, nxt); o2_store(reg, r2); }
+            if (h.found) { ok = enc_code(low, range, esc0 + h.under, h.cnt, h.tot, o); done = true; }
+            else if (esc0 > 0 && esc0 < h.tot) ok = enc_code(low, range, 0, esc0, h.tot, o);
             if (!ok) break;
         }
         if (!done) {                                                 // root, compress.c:318-329
@@ -528,12 +639,12 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
             const uint32_t tot0 = rtot;
             if (cnt == 0) ++nodes;
             root_add(root, v, cnt);
-            ok = enc_code(low, range, 1 + under, 1 + cnt, tot0, op, n, cap);
+            ok = enc_code(low, range, 1 + under, 1 + cnt, tot0, o);
             if (!ok) break;
             rtot = (rtot + kRootDelta) & 0xFFFF;
             if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
         }
-        if (order >= 1) c2 = nxt;                                    // compress.c:331-335
+        if (order >= 1) { c2 = nxt; c2fresh = nfresh; }              // compress.c:331-335
         if (order < 2) ++order;
         b1 = v;
         if (nodes >= kMaxNodes) {                                    // compress.c:148-157
@@ -544,12 +655,13 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     if (ovf) { flag_exact(ws, pkt); return; }
     if (ok) {                                                        // compress.c:139-146
         while (low) {
-            if (n >= cap) { ok = false; break; }
-            op[n++] = static_cast<uint8_t>(low >> 24);
+            if (o.n >= o.cap) { ok = false; break; }
+            outwin_put(o, low >> 24);
             low <<= 8;
         }
     }
-    b.out_len[pkt] = ok ? n : 0u;
+    if (ok) outwin_finish(o);
+    b.out_len[pkt] = ok ? o.n : 0u;
 }
 
 DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t pkt,
@@ -558,62 +670,68 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
     const uint32_t len = b.in_len[pkt];
     const uint32_t cap = b.out_cap[pkt];
     if (len == 0) { b.out_len[pkt] = 0; return; }                   // compress.c:513
-    uint8_t* op = b.out + b.out_off[pkt];
+    OutWin o = { b.out + b.out_off[pkt], cap, 0u, make_uint4(0u, 0u, 0u, 0u) };
     const uint32_t end = ws.lane_region;
-    DecIn in = { b.in + b.in_off[pkt], 0u, len, 0u };
-    in.nb = in.p[0];
+    InWin in;
+    inwin_init(in, b.in + b.in_off[pkt], len);
 
     region_reset(reg, root);
     uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1;
     uint32_t order = 0, b1 = 0, c2 = 0;
-    uint32_t low = 0, code = 0, range = ~0u, n = 0;
-    for (int k = 0; k < 4; ++k) code = (code << 8) | din_take(in);   // compress.c:344-350
+    bool c2fresh = false;
+    uint32_t low = 0, code = 0, range = ~0u;
+    for (int k = 0; k < 4; ++k) code = (code << 8) | inwin_take(in);   // compress.c:344-350
     bool fail = false, anomaly = false, ovf = false;
 
     for (;;) {
         int at = -1;                         // context that produced the symbol (2, 1, 0)
         uint32_t v = 0, nxt = 0;
+        bool nfresh = false;
         Rec<kO2Inl> r2;
         Rec<kO1Inl> r1;
-        if (order >= 2) rec_load(reg, c2 * 32, r2);
-        if (order >= 1) rec_load(reg, b1 * kO1Rec, r1);
+        if (order >= 2) { if (c2fresh) o2_fresh(c2, r2); else o2_load(reg, c2, r2); }
+        if (order >= 1) o1_load(reg, b1, r1);
 
-        if (order >= 2 && r2.esc > 0 && r2.esc < r2.tot) {          // compress.c:529-568
-            range /= r2.tot;
-            uint32_t cd = ((code - low) / range) & 0xFFFF;
-            if (cd < r2.esc) {
-                dec_code(low, code, range, 0, r2.esc, in);
-            } else {
-                cd -= r2.esc;
-                Hit h;
-                if (!rec_search(reg, r2, cd, h)) { fail = true; break; }
-                v = h.val;
-                rec_bump(reg, r2, h.k, h.cnt, kSubDelta);
-                dec_code(low, code, range, r2.esc + h.under, h.cnt, in);
-                r2.tot = (r2.tot + kSubDelta) & 0xFFFF;
-                if (h.cnt > 0xFF - 2 * kSubDelta || r2.tot > kTotalLimit) rec_rescale(reg, r2);
-                rec_store(reg, r2);
-                nxt = h.link;
-                at = 2;
+        if (order >= 2 && r2.esc > 0) {                              // compress.c:529-568
+            const uint32_t tot = rec_total(reg, r2);
+            if (r2.esc < tot) {
+                range /= tot;
+                uint32_t cd = ((code - low) / range) & 0xFFFF;
+                if (cd < r2.esc) {
+                    dec_code(low, code, range, 0, r2.esc, in);
+                } else {
+                    cd -= r2.esc;
+                    Hit h;
+                    if (!rec_search(reg, r2, cd, h)) { fail = true; break; }
+                    v = h.val;
+                    rec_bump(reg, r2, h.k, h.cnt, kSubDelta);
+                    dec_code(low, code, range, r2.esc + h.under, h.cnt, in);
+                    if (h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit) rec_rescale(reg, r2);
+                    o2_store(reg, r2);
+                    nxt = h.link;
+                    at = 2;
+                }
             }
         }
-        if (at < 0 && order >= 1 && r1.esc > 0 && r1.esc < r1.tot) {
-            range /= r1.tot;
-            uint32_t cd = ((code - low) / range) & 0xFFFF;
-            if (cd < r1.esc) {
-                dec_code(low, code, range, 0, r1.esc, in);
-            } else {
-                cd -= r1.esc;
-                Hit h;
-                if (!rec_search(reg, r1, cd, h)) { fail = true; break; }
-                v = h.val;
-                rec_bump(reg, r1, h.k, h.cnt, kSubDelta);
-                dec_code(low, code, range, r1.esc + h.under, h.cnt, in);
-                r1.tot = (r1.tot + kSubDelta) & 0xFFFF;
-                if (h.cnt > 0xFF - 2 * kSubDelta || r1.tot > kTotalLimit) rec_rescale(reg, r1);
-                rec_store(reg, r1);
-                nxt = h.link;
-                at = 1;
+        if (at < 0 && order >= 1 && r1.esc > 0) {
+            const uint32_t tot = rec_total(reg, r1);
+            if (r1.esc < tot) {
+                range /= tot;
+                uint32_t cd = ((code - low) / range) & 0xFFFF;
+                if (cd < r1.esc) {
+                    dec_code(low, code, range, 0, r1.esc, in);
+                } else {
+                    cd -= r1.esc;
+                    Hit h;
+                    if (!rec_search(reg, r1, cd, h)) { fail = true; break; }
+                    v = h.val;
+                    rec_bump(reg, r1, h.k, h.cnt, kSubDelta);
+                    dec_code(low, code, range, r1.esc + h.under, h.cnt, in);
+                    if (h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit) rec_rescale(reg, r1);
+                    o1_store(reg, r1);
+                    nxt = h.link;
+                    at = 1;
+                }
             }
         }
         if (at < 0) {                                                // root, compress.c:570-596
@@ -636,21 +754,22 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         bool pend = false;
         uint32_t kpend = 0;
         if (order >= 2 && at < 2) {
-            const Hit h = sub_update<kO2Inl, kO2MinLog, false>(reg, r2, v, bump, end, nodes, ovf);
+            const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf);
             if (ovf) break;
-            if (h.found) rec_store(reg, r2);
+            if (h.found) o2_store(reg, r2);
             else { pend = true; kpend = h.k; }
         }
         if (order >= 1 && at < 1) {
-            const Hit h = sub_update<kO1Inl, kO1MinLog, true>(reg, r1, v, bump, end, nodes, ovf);
+            const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf);
             if (ovf) break;
-            rec_store(reg, r1);
+            o1_store(reg, r1);
             nxt = h.link;
+            nfresh = !h.found;
         }
-        if (pend) { rec_set_link(reg, r2, kpend, nxt); rec_store(reg, r2); }
-        if (n >= cap) { fail = true; break; }                        // compress.c:617
-        op[n++] = static_cast<uint8_t>(v);
-        if (order >= 1) c2 = nxt;
+        if (pend) { rec_set_link(reg, r2, kpend, nxt); o2_store(reg, r2); }
+        if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
+        outwin_put(o, v);
+        if (order >= 1) { c2 = nxt; c2fresh = nfresh; }
         if (order < 2) ++order;
         b1 = v;
         if (nodes >= kMaxNodes) {
@@ -659,54 +778,63 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         }
     }
     if (ovf || anomaly) { flag_exact(ws, pkt); return; }
-    b.out_len[pkt] = fail ? 0u : n;
+    if (!fail) outwin_finish(o);
+    b.out_len[pkt] = fail ? 0u : o.n;
 }
 
 }  // namespace
 
 extern "C" uint32_t rc_hip_lane_region_bytes(uint32_t max_len)
 {
-    // order-1 table + order-2 records (<= one per byte) + extension blocks
-    // (<= 16 B per model node); at most 4094 nodes between resets.
+    // order-1 table + one 8-B order-2 record per byte + extension blocks
+    // (< 16 B per model node over their lifetime; <= 4094 nodes between resets)
     const uint64_t L = max_len < 4096 ? max_len : 4096;
     const uint64_t nodes = 2 * L + 256 < 4094 ? 2 * L + 256 : 4094;
-    uint64_t bytes = kArenaBase + 32 * L + 16 * nodes + 4096;
+    uint64_t bytes = kArenaBase + kO2Rec * L + 16 * nodes + 1024;
     bytes = (bytes + 255) & ~255ull;
     return static_cast<uint32_t>(bytes);
 }
 
 #ifndef RC_LANE_HOST_TEST
-extern "C" __global__ __launch_bounds__(256)
-void rc_compress_lane(rc_batch_dev b, rc_workspace_dev ws)
+// Lane mapping: a workgroup is 4 wavefronts; the first `act` lanes of each
+// wavefront own one packet each (act = 64 by default; 32/16 trade VALU
+// efficiency for more resident waves per SIMD to overlap HBM latency).
+template <bool DECOMP>
+DEV void lane_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* root = smem + threadIdx.x * kRootStride;
-    const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t act = ws.lane_active;
+    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l >= act) return;
+    const uint32_t local = wave * act + l;
+    uint8_t* root = smem + local * kRootStride;
+    const uint32_t per_block = 4 * act;
+    const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
-    for (uint32_t pkt = slot; pkt < b.n; pkt += gridDim.x * kBlock)
-        compress_one(b, ws, pkt, reg, root);
+    for (uint32_t pkt = slot; pkt < b.n; pkt += gridDim.x * per_block) {
+        if (DECOMP) decompress_one(b, ws, pkt, reg, root);
+        else compress_one(b, ws, pkt, reg, root);
+    }
 }
 
 extern "C" __global__ __launch_bounds__(256)
-void rc_decompress_lane(rc_batch_dev b, rc_workspace_dev ws)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* root = smem + threadIdx.x * kRootStride;
-    const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
-    uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
-    for (uint32_t pkt = slot; pkt < b.n; pkt += gridDim.x * kBlock)
-        decompress_one(b, ws, pkt, reg, root);
-}
+void rc_compress_lane(rc_batch_dev b, rc_workspace_dev ws) { lane_main<false>(b, ws); }
+
+extern "C" __global__ __launch_bounds__(256)
+void rc_decompress_lane(rc_batch_dev b, rc_workspace_dev ws) { lane_main<true>(b, ws); }
 
 extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
                                   void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    uint32_t blocks = (b->n + kBlock - 1) / kBlock;
-    const uint32_t maxb = ws->lane_slots / kBlock;
+    const uint32_t act = ws->lane_active;
+    if (act != 64 && act != 32 && act != 16) return static_cast<int>(hipErrorInvalidValue);
+    const uint32_t per_block = 4 * act;
+    uint32_t blocks = (b->n + per_block - 1) / per_block;
+    const uint32_t maxb = ws->lane_slots / per_block;
     if (blocks > maxb) blocks = maxb;
     if (blocks == 0) return static_cast<int>(hipErrorInvalidValue);
-    const size_t lds = static_cast<size_t>(kBlock) * kRootStride;
+    const size_t lds = static_cast<size_t>(per_block) * kRootStride;
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(kBlock), lds, st, *b, *ws);
     else

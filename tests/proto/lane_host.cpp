@@ -17,7 +17,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0};
     rc_batch_dev b = { in, &ioff, &len, out, &ooff, &cap, out_len, 1, max_len };
     rc_workspace_dev ws = {};
-    ws.flag_list = flags; ws.counters = counters; ws.lane_region = need; ws.lane_pool = region;
+    ws.flag_list = flags; ws.counters = counters; ws.lane_region = need; ws.lane_pool = region; ws.lane_active = 64;
     *out_len = 0xFFFFFFFFu;
     if (decompress) decompress_one(b, ws, 0, region, g_root);
     else compress_one(b, ws, 0, region, g_root);

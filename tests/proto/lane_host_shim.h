@@ -7,6 +7,8 @@
 #define __device__
 #define __forceinline__ inline
 struct uint4 { uint32_t x, y, z, w; };
+struct uint2 { uint32_t x, y; };
+inline uint2 make_uint2(uint32_t a, uint32_t b) { return uint2{a, b}; }
 inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
 inline uint32_t host_sad_u8(uint32_t a, uint32_t b, uint32_t acc)
 {

@@ -196,3 +196,26 @@ def test_random_fuzz_vs_oracle(coder):
     for g, r in zip(garbage, res):
         e = port.decompress(g, 2048)
         assert r[0] == e[0] and (e[0] == 0 or r[1] == e[1])
+
+
+@pytest.fixture(scope="module")
+def wave_coder():
+    """The one-packet-per-wavefront kernels (ENET_RC_KERNEL=wave), kept as an
+    alternative path; the default is one packet per lane."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import os
+    from enet_amd import RangeCoder
+    os.environ["ENET_RC_KERNEL"] = "wave"
+    try:
+        c = RangeCoder()
+    finally:
+        del os.environ["ENET_RC_KERNEL"]
+    yield c
+    c.close()
+
+
+def test_wave_kernel_fixtures(wave_coder):
+    test_compress_fixtures(wave_coder)
+    test_decompress_fixtures_incl_garbage(wave_coder)
+    test_c1_digest(wave_coder)

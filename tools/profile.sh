@@ -1,14 +1,20 @@
 #!/bin/bash
 # Kernel-trace + PMC profile of bench.py on the GPU box (run under gpurun).
 # usage: tools/profile.sh TAG [bench args...]
+# Separate passes per counter group (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
-    python3 $R/bench.py --no-cpu --no-pcie "$@" > $OUT/bench_kt.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-    --output-format csv -d $OUT/pmc1 -o run -- python3 $R/bench.py --no-cpu --no-pcie --steps 1 --warmup 0 "$@" > $OUT/bench_pmc1.log 2>&1
+B="python3 $R/bench.py --no-cpu --no-pcie"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- $B "$@" > $OUT/bench_kt.log 2>&1
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY" \
+           "SQ_WAVES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- $B --steps 1 --warmup 0 "$@" > $OUT/bench_pmc$i.log 2>&1 || echo "pmc group $i failed: $grp" >> $OUT/errors.txt
+done
 echo done
