@@ -595,15 +595,23 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     bool c2fresh = false;
     uint32_t low = 0, range = ~0u;
     bool ok = true, ovf = false;
+    // software pipeline: the records of step i+1 are loaded during step i
+    // (the next order-1 context is the current byte, known at the top of the
+    // step; the next order-2 context once the current contexts are resolved).
+    Rec<kO1Inl> r1;
+    Rec<kO2Inl> r2;
+    o2_fresh(0, r2);
+    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kO1Inl; ++t) r1.e[t] = 0;
 
     for (uint32_t i = 0; i < len; ++i) {
         const uint32_t v = inwin_take(in);
+        Rec<kO1Inl> n1;
+        o1_load(reg, v, n1);                                         // next step's order-1 record
+        Rec<kO2Inl> n2;
         bool done = false, pend = false, nfresh = false;
         uint32_t nxt = 0, kpend = 0;
-        Rec<kO2Inl> r2;
-        Rec<kO1Inl> r1;
-        if (order >= 2) { if (c2fresh) o2_fresh(c2, r2); else o2_load(reg, c2, r2); }
-        if (order >= 1) o1_load(reg, b1, r1);
 
         if (order >= 2) {                                            // order 2, compress.c:286-316
             const uint32_t esc0 = r2.esc;
@@ -611,8 +619,9 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
             if (ovf) break;
             if (h.found) {
                 o2_store(reg, r2);
-                ok = enc_code(low, range, esc0 + h.under, h.cnt, h.tot, o);
                 nxt = h.link;
+                if (nxt * kO2Rec == r2.off) n2 = r2; else o2_load(reg, nxt, n2);
+                ok = enc_code(low, range, esc0 + h.under, h.cnt, h.tot, o);
                 done = true;
             } else {
                 pend = true;
@@ -625,10 +634,14 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
             const uint32_t esc0 = r1.esc;
             const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf);
             if (ovf) break;
-            o1_store(reg, r1);
             nxt = h.link;
             nfresh = !h.found;
-            if (pend) { rec_set_link(reg, r2, kpend, nxt); o2_store(reg, r2); }
+            if (pend) rec_set_link(reg, r2, kpend, nxt);
+            if (nfresh) o2_fresh(nxt, n2);
+            else if (order >= 2 && nxt * kO2Rec == r2.off) n2 = r2;
+            else o2_load(reg, nxt, n2);
+            o1_store(reg, r1);
+            if (pend) o2_store(reg, r2);
             if (h.found) { ok = enc_code(low, range, esc0 + h.under, h.cnt, h.tot, o); done = true; }
             else if (esc0 > 0 && esc0 < h.tot) ok = enc_code(low, range, 0, esc0, h.tot, o);
             if (!ok) break;
@@ -644,7 +657,9 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
             rtot = (rtot + kRootDelta) & 0xFFFF;
             if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
         }
-        if (order >= 1) { c2 = nxt; c2fresh = nfresh; }              // compress.c:331-335
+        if (order >= 1) { c2 = nxt; c2fresh = nfresh; r2 = n2; }     // compress.c:331-335
+        // the prefetched order-1 record is stale when it is the one this step updated
+        if (!(order >= 1 && v == b1)) r1 = n1;
         if (order < 2) ++order;
         b1 = v;
         if (nodes >= kMaxNodes) {                                    // compress.c:148-157
@@ -677,20 +692,22 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
 
     region_reset(reg, root);
     uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1;
-    uint32_t order = 0, b1 = 0, c2 = 0;
-    bool c2fresh = false;
+    uint32_t order = 0, b1 = 0;
     uint32_t low = 0, code = 0, range = ~0u;
     for (int k = 0; k < 4; ++k) code = (code << 8) | inwin_take(in);   // compress.c:344-350
     bool fail = false, anomaly = false, ovf = false;
+    // the next step's records are loaded as soon as the symbol is decoded
+    Rec<kO1Inl> r1;
+    Rec<kO2Inl> r2;
+    o2_fresh(0, r2);
+    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kO1Inl; ++t) r1.e[t] = 0;
 
     for (;;) {
         int at = -1;                         // context that produced the symbol (2, 1, 0)
         uint32_t v = 0, nxt = 0;
         bool nfresh = false;
-        Rec<kO2Inl> r2;
-        Rec<kO1Inl> r1;
-        if (order >= 2) { if (c2fresh) o2_fresh(c2, r2); else o2_load(reg, c2, r2); }
-        if (order >= 1) o1_load(reg, b1, r1);
 
         if (order >= 2 && r2.esc > 0) {                              // compress.c:529-568
             const uint32_t tot = rec_total(reg, r2);
@@ -707,7 +724,6 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
                     rec_bump(reg, r2, h.k, h.cnt, kSubDelta);
                     dec_code(low, code, range, r2.esc + h.under, h.cnt, in);
                     if (h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit) rec_rescale(reg, r2);
-                    o2_store(reg, r2);
                     nxt = h.link;
                     at = 2;
                 }
@@ -728,7 +744,6 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
                     rec_bump(reg, r1, h.k, h.cnt, kSubDelta);
                     dec_code(low, code, range, r1.esc + h.under, h.cnt, in);
                     if (h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit) rec_rescale(reg, r1);
-                    o1_store(reg, r1);
                     nxt = h.link;
                     at = 1;
                 }
@@ -750,26 +765,35 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
             if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
             at = 0;
         }
+        Rec<kO1Inl> n1;
+        o1_load(reg, v, n1);                                         // next step's order-1 record
         // patch the contexts above, compress.c:598-615
         bool pend = false;
         uint32_t kpend = 0;
         if (order >= 2 && at < 2) {
             const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf);
             if (ovf) break;
-            if (h.found) o2_store(reg, r2);
-            else { pend = true; kpend = h.k; }
+            if (!h.found) { pend = true; kpend = h.k; }
         }
         if (order >= 1 && at < 1) {
             const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf);
             if (ovf) break;
-            o1_store(reg, r1);
             nxt = h.link;
             nfresh = !h.found;
         }
-        if (pend) { rec_set_link(reg, r2, kpend, nxt); o2_store(reg, r2); }
+        if (pend) rec_set_link(reg, r2, kpend, nxt);
+        Rec<kO2Inl> n2;
+        if (order >= 1) {
+            if (nfresh) o2_fresh(nxt, n2);
+            else if (order >= 2 && nxt * kO2Rec == r2.off) n2 = r2;
+            else o2_load(reg, nxt, n2);
+        }
+        if (order >= 2) o2_store(reg, r2);
+        if (order >= 1 && at <= 1) o1_store(reg, r1);
         if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
         outwin_put(o, v);
-        if (order >= 1) { c2 = nxt; c2fresh = nfresh; }
+        if (order >= 1) r2 = n2;
+        if (!(order >= 1 && v == b1)) r1 = n1;
         if (order < 2) ++order;
         b1 = v;
         if (nodes >= kMaxNodes) {
