@@ -17,13 +17,17 @@
 //       count at the end of each 16-symbol group) -> lookups are 1-2 LDS
 //       reads + byte-SAD sums, no tree walk.
 //   order 1: 256 records of 64 B, direct-mapped by the previous byte, in a
-//       per-lane HBM region; order 2: 32-B records bump-allocated in the same
-//       region and reached through links stored in the entries (compress.c's
-//       suffix links, `parent`).  A record = 16-B header {esc, tot, len, ext}
-//       + inline sorted entries {value:8 | count:8 | link:16}; contexts that
-//       outgrow the inline slots move their entries to an extension block.
-//   Every byte therefore costs one dependent HBM round trip (the order-1 and
-//   order-2 records are loaded together), not a BST walk.
+//       per-lane HBM region; order 2: 8-B records bump-allocated in the same
+//       region, reached through links stored in the entries (compress.c's
+//       suffix links, `parent`).  Entries are sorted {value | count | link};
+//       contexts that outgrow their inline slots use an extension block.
+//   Each byte costs one HBM round trip, and that load is issued a step ahead.
+//
+// Code shape: 64 lanes run 64 different packets, so every `if` on per-lane
+// data is divergent.  Common paths are written as straight-line predicated
+// register code; rare paths (extension blocks, growth, rescale, packet edges,
+// model reset) sit behind wave-uniform ballot guards so a wave that does not
+// need them pays one scalar branch.
 //
 // Packets this model cannot reproduce -- corrupt streams whose root code
 // points past symbol 255 (compress.c:427-438 then depends on tree shape) --
@@ -51,13 +55,13 @@ constexpr uint32_t kSubEscDelta = 5;         // compress.c:36
 constexpr uint32_t kMaxNodes = 4096 - 2;     // compress.c:150
 constexpr uint32_t kTotalLimit = kBot - 0x100;
 
-constexpr uint32_t kBlock = 256;             // lanes (packets) per workgroup
 constexpr uint32_t kRootStride = 304;        // LDS bytes per lane; 76 dwords (76/4 odd: b128 conflict-free)
 
 DEV uint32_t val_of(uint32_t e) { return e & 0xFF; }
 DEV uint32_t cnt_of(uint32_t e) { return (e >> 8) & 0xFF; }
 DEV uint32_t sad(uint32_t x, uint32_t acc) { return __builtin_amdgcn_sad_u8(x, 0u, acc); }
 DEV uint32_t pick4(uint32_t i, const uint4& q) { return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w; }
+DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
 // ------------------------------------------------------------ order 0 (LDS)
 
@@ -192,15 +196,14 @@ DEV void o1_load(const uint8_t* reg, uint32_t x, Rec<kO1Inl>& r)
     r.e[10] = q3.x; r.e[11] = q3.y; r.e[12] = q3.z; r.e[13] = q3.w;
 }
 
+// in ext mode the inline slots are dead, so they are written unconditionally
 DEV void o1_store(uint8_t* reg, const Rec<kO1Inl>& r)
 {
     uint4* p = reinterpret_cast<uint4*>(reg + r.off);
     p[0] = make_uint4(r.esc | (r.len << 16), r.ext, r.e[0], r.e[1]);
-    if (r.ext == 0) {
-        p[1] = make_uint4(r.e[2], r.e[3], r.e[4], r.e[5]);
-        p[2] = make_uint4(r.e[6], r.e[7], r.e[8], r.e[9]);
-        p[3] = make_uint4(r.e[10], r.e[11], r.e[12], r.e[13]);
-    }
+    p[1] = make_uint4(r.e[2], r.e[3], r.e[4], r.e[5]);
+    p[2] = make_uint4(r.e[6], r.e[7], r.e[8], r.e[9]);
+    p[3] = make_uint4(r.e[10], r.e[11], r.e[12], r.e[13]);
 }
 
 DEV void o2_load(const uint8_t* reg, uint32_t idx, Rec<kO2Inl>& r)
@@ -228,38 +231,40 @@ DEV Hit rec_find(const uint8_t* reg, const Rec<INL>& r, uint32_t v)
 {
     Hit h = { 0u, 0u, 0u, 0u, v, 0u, false };
     uint32_t sum = 0;
-    if (r.ext == 0) {
+    const uint32_t ilen = r.ext == 0 ? r.len : 0u;
 #pragma unroll
-        for (uint32_t t = 0; t < INL; ++t) {
-            const uint32_t e = r.e[t];
-            const bool in = t < r.len;
-            const uint32_t c = in ? cnt_of(e) : 0u;
-            const bool lt = in && val_of(e) < v;
-            const bool eq = in && val_of(e) == v;
-            sum += c;
-            h.under += lt ? c : 0u;
-            h.k += lt ? 1u : 0u;
-            h.found = h.found || eq;
-            h.cnt = eq ? c : h.cnt;
-            h.link = eq ? (e >> 16) : h.link;
-        }
-    } else {
-        const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-        for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
-            const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
+    for (uint32_t t = 0; t < INL; ++t) {
+        const uint32_t e = r.e[t];
+        const bool in = t < ilen;
+        const uint32_t c = in ? cnt_of(e) : 0u;
+        const bool lt = in && val_of(e) < v;
+        const bool eq = in && val_of(e) == v;
+        sum += c;
+        h.under += lt ? c : 0u;
+        h.k += lt ? 1u : 0u;
+        h.found = h.found || eq;
+        h.cnt = eq ? c : h.cnt;
+        h.link = eq ? (e >> 16) : h.link;
+    }
+    if (any_lane(r.ext != 0)) {
+        if (r.ext != 0) {
+            const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
+            for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
+                const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
 #pragma unroll
-            for (uint32_t t = 0; t < 4; ++t) {
-                const uint32_t e = pick4(t, q);
-                const bool in = c0 + t < r.len;
-                const uint32_t c = in ? cnt_of(e) : 0u;
-                const bool lt = in && val_of(e) < v;
-                const bool eq = in && val_of(e) == v;
-                sum += c;
-                h.under += lt ? c : 0u;
-                h.k += lt ? 1u : 0u;
-                h.found = h.found || eq;
-                h.cnt = eq ? c : h.cnt;
-                h.link = eq ? (e >> 16) : h.link;
+                for (uint32_t t = 0; t < 4; ++t) {
+                    const uint32_t e = pick4(t, q);
+                    const bool in = c0 + t < r.len;
+                    const uint32_t c = in ? cnt_of(e) : 0u;
+                    const bool lt = in && val_of(e) < v;
+                    const bool eq = in && val_of(e) == v;
+                    sum += c;
+                    h.under += lt ? c : 0u;
+                    h.k += lt ? 1u : 0u;
+                    h.found = h.found || eq;
+                    h.cnt = eq ? c : h.cnt;
+                    h.link = eq ? (e >> 16) : h.link;
+                }
             }
         }
     }
@@ -271,173 +276,185 @@ template <uint32_t INL>
 DEV uint32_t rec_total(const uint8_t* reg, const Rec<INL>& r)
 {
     uint32_t sum = 0;
-    if (r.ext == 0) {
+    const uint32_t ilen = r.ext == 0 ? r.len : 0u;
 #pragma unroll
-        for (uint32_t t = 0; t < INL; ++t) sum += t < r.len ? cnt_of(r.e[t]) : 0u;
-    } else {
-        const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-        for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
-            const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
+    for (uint32_t t = 0; t < INL; ++t) sum += t < ilen ? cnt_of(r.e[t]) : 0u;
+    if (any_lane(r.ext != 0)) {
+        if (r.ext != 0) {
+            const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
+            for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
+                const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
 #pragma unroll
-            for (uint32_t t = 0; t < 4; ++t) sum += c0 + t < r.len ? cnt_of(pick4(t, q)) : 0u;
+                for (uint32_t t = 0; t < 4; ++t) sum += c0 + t < r.len ? cnt_of(pick4(t, q)) : 0u;
+            }
         }
     }
     return (r.esc + sum) & 0xFFFF;
 }
 
-// Decoder search (compress.c:373-416, minimum 0): entry whose interval holds code.
+// Decoder search (compress.c:373-416, minimum 0) where `en`: entry whose
+// interval holds code.  Returns false (corrupt stream) when none does.
 template <uint32_t INL>
-DEV bool rec_search(const uint8_t* reg, const Rec<INL>& r, uint32_t code, Hit& h)
+DEV Hit rec_search(const uint8_t* reg, const Rec<INL>& r, uint32_t code, bool en)
 {
+    Hit h = { 0u, 0u, 0u, 0u, 0u, 0u, false };
     uint32_t cum = 0;
     bool found = false;
-    h.k = 0; h.under = 0; h.cnt = 0; h.link = 0; h.val = 0;
-    if (r.ext == 0) {
+    const uint32_t ilen = (en && r.ext == 0) ? r.len : 0u;
 #pragma unroll
-        for (uint32_t t = 0; t < INL; ++t) {
-            const uint32_t e = r.e[t];
-            const bool in = t < r.len;
-            const uint32_t c = in ? cnt_of(e) : 0u;
-            const bool hit = in && !found && code < cum + c;
-            h.k = hit ? t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
-            h.link = hit ? (e >> 16) : h.link; h.val = hit ? val_of(e) : h.val;
-            found = found || hit;
-            cum += c;
-        }
-    } else {
-        const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-        for (uint32_t c0 = 0; c0 < r.len && !found; c0 += 4) {
-            const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
+    for (uint32_t t = 0; t < INL; ++t) {
+        const uint32_t e = r.e[t];
+        const bool in = t < ilen;
+        const uint32_t c = in ? cnt_of(e) : 0u;
+        const bool hit = in && !found && code < cum + c;
+        h.k = hit ? t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
+        h.link = hit ? (e >> 16) : h.link; h.val = hit ? val_of(e) : h.val;
+        found = found || hit;
+        cum += c;
+    }
+    if (any_lane(en && r.ext != 0)) {
+        if (en && r.ext != 0) {
+            const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
+            for (uint32_t c0 = 0; c0 < r.len && !found; c0 += 4) {
+                const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
 #pragma unroll
-            for (uint32_t t = 0; t < 4; ++t) {
-                const uint32_t e = pick4(t, q);
-                const bool in = c0 + t < r.len;
-                const uint32_t c = in ? cnt_of(e) : 0u;
-                const bool hit = in && !found && code < cum + c;
-                h.k = hit ? c0 + t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
-                h.link = hit ? (e >> 16) : h.link; h.val = hit ? val_of(e) : h.val;
-                found = found || hit;
-                cum += c;
+                for (uint32_t t = 0; t < 4; ++t) {
+                    const uint32_t e = pick4(t, q);
+                    const bool in = c0 + t < r.len;
+                    const uint32_t c = in ? cnt_of(e) : 0u;
+                    const bool hit = in && !found && code < cum + c;
+                    h.k = hit ? c0 + t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
+                    h.link = hit ? (e >> 16) : h.link; h.val = hit ? val_of(e) : h.val;
+                    found = found || hit;
+                    cum += c;
+                }
             }
         }
     }
     h.found = found;
-    return found;
+    return h;
 }
 
-// count[k] = cnt + d
+// count[k] = cnt + d where `en`
 template <uint32_t INL>
-DEV void rec_bump(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t cnt, uint32_t d)
+DEV void rec_bump(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t cnt, uint32_t d, bool en)
 {
-    if (r.ext == 0) {
+    const bool inl = en && r.ext == 0;
 #pragma unroll
-        for (uint32_t t = 0; t < INL; ++t) r.e[t] += (t == k) ? (d << 8) : 0u;
-    } else {
-        reg[r.ext + 4 * k + 1] = static_cast<uint8_t>(cnt + d);
+    for (uint32_t t = 0; t < INL; ++t) r.e[t] += (inl && t == k) ? (d << 8) : 0u;
+    if (any_lane(en && r.ext != 0)) {
+        if (en && r.ext != 0) reg[r.ext + 4 * k + 1] = static_cast<uint8_t>(cnt + d);
     }
 }
 
-// Insert entry `ne` at position k; moves to / grows an extension block when full.
+// Insert entry `ne` at position k where `en`; moves to / grows an extension
+// block when the inline slots or the block are full.  false = region full.
 template <uint32_t INL, uint32_t MINCAP>
-DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t& bump, uint32_t end)
+DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t& bump, uint32_t end, bool en)
 {
-    if (r.ext == 0 && r.len < INL) {
+    const bool fast = en && r.ext == 0 && r.len < INL;
 #pragma unroll
-        for (int t = INL - 1; t >= 0; --t) {
-            const uint32_t prev = t > 0 ? r.e[t > 0 ? t - 1 : 0] : 0u;
-            r.e[t] = (static_cast<uint32_t>(t) > k) ? prev : (static_cast<uint32_t>(t) == k ? ne : r.e[t]);
-        }
-    } else {
-        const uint32_t cap = r.ext ? cap_for(r.len, MINCAP) : INL;
-        if (r.ext != 0 && r.len < cap) {
-            uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
-            for (uint32_t j = r.len; j > k; --j) ep[j] = ep[j - 1];
-            ep[k] = ne;
-        } else {
-            const uint32_t ncap = r.ext ? 2 * cap : MINCAP;
-            const uint32_t at = (bump + 15) & ~15u;
-            if (at + 4 * ncap > end) return false;
-            uint32_t* np = reinterpret_cast<uint32_t*>(reg + at);
-            if (r.ext == 0) {
-#pragma unroll
-                for (uint32_t t = 0; t < INL; ++t) np[t + (t >= k ? 1u : 0u)] = r.e[t];
+    for (int t = INL - 1; t >= 0; --t) {
+        const uint32_t prev = t > 0 ? r.e[t > 0 ? t - 1 : 0] : 0u;
+        const uint32_t shifted = (static_cast<uint32_t>(t) > k) ? prev
+                               : (static_cast<uint32_t>(t) == k ? ne : r.e[t]);
+        r.e[t] = fast ? shifted : r.e[t];
+    }
+    bool ok = true;
+    if (any_lane(en && !fast)) {
+        if (en && !fast) {
+            const uint32_t cap = r.ext ? cap_for(r.len, MINCAP) : INL;
+            if (r.ext != 0 && r.len < cap) {
+                uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
+                for (uint32_t j = r.len; j > k; --j) ep[j] = ep[j - 1];
+                ep[k] = ne;
             } else {
-                const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-                for (uint32_t j = 0; j < r.len; ++j) np[j + (j >= k ? 1u : 0u)] = ep[j];
+                const uint32_t ncap = r.ext ? 2 * cap : MINCAP;
+                const uint32_t at = (bump + 15) & ~15u;
+                if (at + 4 * ncap > end) {
+                    ok = false;
+                } else {
+                    uint32_t* np = reinterpret_cast<uint32_t*>(reg + at);
+                    if (r.ext == 0) {
+#pragma unroll
+                        for (uint32_t t = 0; t < INL; ++t) np[t + (t >= k ? 1u : 0u)] = r.e[t];
+                    } else {
+                        const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
+                        for (uint32_t j = 0; j < r.len; ++j) np[j + (j >= k ? 1u : 0u)] = ep[j];
+                    }
+                    np[k] = ne;
+                    r.ext = at;
+                    bump = at + 4 * ncap;
+                }
             }
-            np[k] = ne;
-            r.ext = at;
-            bump = at + 4 * ncap;
         }
     }
-    r.len += 1;
-    return true;
+    r.len += (en && ok) ? 1u : 0u;
+    return ok;
 }
 
-// Link of entry k (an o2 entry created before its suffix context was known).
+// Link of entry k where `en` (an o2 entry created before its suffix context was known).
 template <uint32_t INL>
-DEV void rec_set_link(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t link)
+DEV void rec_set_link(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t link, bool en)
 {
-    if (r.ext == 0) {
+    const bool inl = en && r.ext == 0;
 #pragma unroll
-        for (uint32_t t = 0; t < INL; ++t) r.e[t] = (t == k) ? ((r.e[t] & 0xFFFFu) | (link << 16)) : r.e[t];
-    } else {
-        *reinterpret_cast<uint16_t*>(reg + r.ext + 4 * k + 2) = static_cast<uint16_t>(link);
+    for (uint32_t t = 0; t < INL; ++t)
+        r.e[t] = (inl && t == k) ? ((r.e[t] & 0xFFFFu) | (link << 16)) : r.e[t];
+    if (any_lane(en && r.ext != 0)) {
+        if (en && r.ext != 0) *reinterpret_cast<uint16_t*>(reg + r.ext + 4 * k + 2) = static_cast<uint16_t>(link);
     }
 }
 
-// compress.c:90-112 on a record
+// compress.c:90-112 on a record, where `en`
 template <uint32_t INL>
-DEV void rec_rescale(uint8_t* reg, Rec<INL>& r)
+DEV void rec_rescale(uint8_t* reg, Rec<INL>& r, bool en)
 {
-    if (r.ext == 0) {
+    if (!any_lane(en)) return;
+    const bool inl = en && r.ext == 0;
 #pragma unroll
-        for (uint32_t t = 0; t < INL; ++t) {
-            const uint32_t e = r.e[t];
-            uint32_t c = cnt_of(e);
-            c -= c >> 1;
-            r.e[t] = t < r.len ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
-        }
-    } else {
+    for (uint32_t t = 0; t < INL; ++t) {
+        const uint32_t e = r.e[t];
+        uint32_t c = cnt_of(e);
+        c -= c >> 1;
+        r.e[t] = (inl && t < r.len) ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
+    }
+    if (en && r.ext != 0) {
         uint8_t* ep = reg + r.ext;
         for (uint32_t j = 0; j < r.len; ++j) {
-            uint32_t c = ep[4 * j + 1];
+            const uint32_t c = ep[4 * j + 1];
             ep[4 * j + 1] = static_cast<uint8_t>(c - (c >> 1));
         }
     }
-    r.esc -= r.esc >> 1;
+    r.esc -= en ? (r.esc >> 1) : 0u;
 }
 
-// Encoder-side update of a sub-context (compress.c:293-314, patch :603-613):
-// find or insert v.  Returns the hit: old count (0 if new), cum below, total
-// before the update, and the entry's link.  ALLOC: an inserted entry gets a
-// fresh o2 record (order-1 contexts); otherwise its link is set later.
+// Encoder-side update of a sub-context where `en` (compress.c:293-314, patch
+// :603-613): find or insert v.  Returns the hit: old count (0 if new), cum
+// below, total before the update, and the entry's link.  ALLOC: an inserted
+// entry gets a fresh o2 record (order-1 contexts); otherwise its link is set
+// later with rec_set_link (order-2 contexts).
 template <uint32_t INL, uint32_t MINCAP, bool ALLOC>
 DEV Hit sub_update(uint8_t* reg, Rec<INL>& r, uint32_t v, uint32_t& bump,
-                   uint32_t end, uint32_t& nodes, bool& ovf)
+                   uint32_t end, uint32_t& nodes, bool& ovf, bool en)
 {
     Hit h = rec_find(reg, r, v);
-    uint32_t tot = h.tot;
-    if (h.found) {
-        rec_bump(reg, r, h.k, h.cnt, kSubDelta);
-    } else {
-        uint32_t newlink = 0;
-        if (ALLOC) {
-            if (bump + kO2Rec > end) { ovf = true; return h; }
-            newlink = bump / kO2Rec;
-            bump += kO2Rec;
-        }
-        if (!rec_insert<INL, MINCAP>(reg, r, h.k, v | (kSubDelta << 8) | (newlink << 16), bump, end)) {
-            ovf = true;
-            return h;
-        }
-        h.link = newlink;
-        ++nodes;
-        r.esc += kSubEscDelta;
-        tot += kSubEscDelta;
+    const bool ins = en && !h.found;
+    rec_bump(reg, r, h.k, h.cnt, kSubDelta, en && h.found);
+    uint32_t newlink = 0;
+    if (ALLOC) {
+        newlink = bump / kO2Rec;
+        bump += ins ? kO2Rec : 0u;
+        if (ins && bump > end) ovf = true;
     }
-    tot = (tot + kSubDelta) & 0xFFFF;
-    if (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit) rec_rescale(reg, r);
+    const bool ok = rec_insert<INL, MINCAP>(reg, r, h.k, v | (kSubDelta << 8) | (newlink << 16),
+                                            bump, end, ins);
+    ovf = ovf || !ok;
+    h.link = ins ? newlink : h.link;
+    nodes += ins ? 1u : 0u;
+    r.esc += ins ? kSubEscDelta : 0u;
+    const uint32_t tot = (h.tot + (ins ? kSubEscDelta : 0u) + kSubDelta) & 0xFFFF;
+    rec_rescale(reg, r, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
     return h;
 }
 
@@ -465,15 +482,19 @@ DEV void win_set(uint4& w, uint32_t i, uint32_t b)
     w.w = d == 3 ? ((w.w & m) | x) : w.w;
 }
 
-DEV uint4 chunk_load(const uint8_t* lo, const uint8_t* hi, uintptr_t c)
+DEV uint4 chunk_load(const uint8_t* lo, const uint8_t* hi, uintptr_t c, bool en)
 {
-    if (c >= reinterpret_cast<uintptr_t>(lo) && c + 16 <= reinterpret_cast<uintptr_t>(hi))
-        return *reinterpret_cast<const uint4*>(c);
+    const bool full = c >= reinterpret_cast<uintptr_t>(lo) && c + 16 <= reinterpret_cast<uintptr_t>(hi);
     uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t t = 0; t < 16; ++t) {
-        const uintptr_t a = c + t;
-        if (a >= reinterpret_cast<uintptr_t>(lo) && a < reinterpret_cast<uintptr_t>(hi))
-            win_set(w, t, *reinterpret_cast<const uint8_t*>(a));
+    if (en && full) w = *reinterpret_cast<const uint4*>(c);
+    if (any_lane(en && !full)) {
+        if (en && !full) {
+            for (uint32_t t = 0; t < 16; ++t) {
+                const uintptr_t a = c + t;
+                if (a >= reinterpret_cast<uintptr_t>(lo) && a < reinterpret_cast<uintptr_t>(hi))
+                    win_set(w, t, *reinterpret_cast<const uint8_t*>(a));
+            }
+        }
     }
     return w;
 }
@@ -485,19 +506,25 @@ DEV void inwin_init(InWin& s, const uint8_t* p, uint32_t len)
 {
     s.p = p; s.len = len; s.pos = 0;
     const uintptr_t c = reinterpret_cast<uintptr_t>(p) & ~static_cast<uintptr_t>(15);
-    s.cur = chunk_load(p, p + len, c);
-    s.nxt = chunk_load(p, p + len, c + 16);
+    s.cur = chunk_load(p, p + len, c, true);
+    s.nxt = chunk_load(p, p + len, c + 16, true);
 }
 
-DEV uint32_t inwin_take(InWin& s)
+// next byte where `en` (0 past the end)
+DEV uint32_t inwin_take(InWin& s, bool en)
 {
-    if (s.pos >= s.len) return 0;
     const uintptr_t a = reinterpret_cast<uintptr_t>(s.p) + s.pos;
-    const uint32_t b = win_get(s.cur, a & 15);
-    ++s.pos;
-    if ((a & 15) == 15) {                 // advance; prefetch the chunk after next
-        s.cur = s.nxt;
-        s.nxt = chunk_load(s.p, s.p + s.len, (a & ~static_cast<uintptr_t>(15)) + 32);
+    const bool live = en && s.pos < s.len;
+    const uint32_t b = live ? win_get(s.cur, a & 15) : 0u;
+    s.pos += live ? 1u : 0u;
+    const bool adv = live && (a & 15) == 15;
+    if (any_lane(adv)) {                  // advance; prefetch the chunk after next
+        const uint4 n = chunk_load(s.p, s.p + s.len, (a & ~static_cast<uintptr_t>(15)) + 32, adv);
+        // component-wise: a select of whole vectors is lowered through scratch
+        s.cur.x = adv ? s.nxt.x : s.cur.x; s.cur.y = adv ? s.nxt.y : s.cur.y;
+        s.cur.z = adv ? s.nxt.z : s.cur.z; s.cur.w = adv ? s.nxt.w : s.cur.w;
+        s.nxt.x = adv ? n.x : s.nxt.x; s.nxt.y = adv ? n.y : s.nxt.y;
+        s.nxt.z = adv ? n.z : s.nxt.z; s.nxt.w = adv ? n.w : s.nxt.w;
     }
     return b;
 }
@@ -513,60 +540,84 @@ DEV void outwin_edge(uint8_t* p, uint32_t n, uintptr_t c, const uint4& w)
     }
 }
 
-// caller guarantees n < cap
-DEV void outwin_put(OutWin& o, uint32_t byte)
+// append a byte where `en` (caller guarantees n < cap)
+DEV void outwin_put(OutWin& o, uint32_t byte, bool en)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(o.p) + o.n;
-    win_set(o.w, a & 15, byte);
-    ++o.n;
-    if ((a & 15) == 15) {
+    uint4 w = o.w;
+    win_set(w, a & 15, byte);
+    o.w.x = en ? w.x : o.w.x; o.w.y = en ? w.y : o.w.y;
+    o.w.z = en ? w.z : o.w.z; o.w.w = en ? w.w : o.w.w;
+    o.n += en ? 1u : 0u;
+    const bool flush = en && (a & 15) == 15;
+    if (any_lane(flush)) {
         const uintptr_t c = a & ~static_cast<uintptr_t>(15);
-        if (c >= reinterpret_cast<uintptr_t>(o.p)) *reinterpret_cast<uint4*>(c) = o.w;
-        else outwin_edge(o.p, o.n, c, o.w);
+        const bool whole = c >= reinterpret_cast<uintptr_t>(o.p);
+        if (flush && whole) *reinterpret_cast<uint4*>(c) = o.w;
+        if (any_lane(flush && !whole)) {
+            if (flush && !whole) outwin_edge(o.p, o.n, c, o.w);
+        }
     }
 }
 
-DEV void outwin_finish(OutWin& o)
+DEV void outwin_finish(OutWin& o, bool en)
 {
-    if (o.n == 0) return;
     const uintptr_t a = reinterpret_cast<uintptr_t>(o.p) + o.n - 1;
-    if ((a & 15) != 15) outwin_edge(o.p, o.n, a & ~static_cast<uintptr_t>(15), o.w);
+    if (en && o.n > 0 && (a & 15) != 15) outwin_edge(o.p, o.n, a & ~static_cast<uintptr_t>(15), o.w);
 }
 
 // ------------------------------------------------------------- range coder
 
-// compress.c:121-137; false = output full
-DEV bool enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total,
-                  OutWin& o)
+// compress.c:121-137 where `en`; clears `ok` when the output is full (the
+// whole compress call then returns 0, compress.c:116-117)
+DEV void enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total,
+                  OutWin& o, bool en, bool& ok)
 {
-    range /= total;
-    low += under * range;
-    range *= count;
-    for (;;) {
-        if ((low ^ (low + range)) >= kTop) {
-            if (range >= kBot) return true;
-            range = (0u - low) & (kBot - 1);
-        }
-        if (o.n >= o.cap) return false;
-        outwin_put(o, low >> 24);
-        range <<= 8;
-        low <<= 8;
+    en = en && ok;
+    const uint32_t r = range / (en ? total : 1u);
+    low = en ? low + under * r : low;
+    range = en ? r * count : range;
+    bool more = en;
+    while (any_lane(more)) {
+        const bool carry = (low ^ (low + range)) >= kTop;
+        const bool stop = carry && range >= kBot;
+        more = more && !stop;
+        if (!any_lane(more)) break;
+        range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
+        const bool full = more && o.n >= o.cap;
+        ok = ok && !full;
+        more = more && !full;
+        outwin_put(o, low >> 24, more);
+        range = more ? range << 8 : range;
+        low = more ? low << 8 : low;
     }
 }
 
-// compress.c:354-371
-DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count, InWin& in)
+// compress.c:352 (truncated to u16 at :545/:575); divides range by total where `en`
+DEV uint32_t dec_read(uint32_t& range, uint32_t low, uint32_t code, uint32_t total, bool en)
 {
-    low += under * range;
-    range *= count;
-    for (;;) {
-        if ((low ^ (low + range)) >= kTop) {
-            if (range >= kBot) break;
-            range = (0u - low) & (kBot - 1);
-        }
-        code = (code << 8) | inwin_take(in);
-        range <<= 8;
-        low <<= 8;
+    const uint32_t r = range / (en ? total : 1u);
+    range = en ? r : range;
+    return ((code - low) / (en ? r : 1u)) & 0xFFFF;
+}
+
+// compress.c:354-371 where `en`
+DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count,
+                  InWin& in, bool en)
+{
+    low = en ? low + under * range : low;
+    range = en ? range * count : range;
+    bool more = en;
+    while (any_lane(more)) {
+        const bool carry = (low ^ (low + range)) >= kTop;
+        const bool stop = carry && range >= kBot;
+        more = more && !stop;
+        if (!any_lane(more)) break;
+        range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
+        const uint32_t b = inwin_take(in, more);
+        code = more ? ((code << 8) | b) : code;
+        range = more ? range << 8 : range;
+        low = more ? low << 8 : low;
     }
 }
 
@@ -574,6 +625,13 @@ DEV void flag_exact(const rc_workspace_dev& ws, uint32_t pkt)
 {
     const uint32_t slot = atomicAdd(&ws.counters[0], 1u);
     ws.flag_list[slot] = pkt;
+}
+
+DEV void rec_clear(Rec<kO1Inl>& r1)
+{
+    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kO1Inl; ++t) r1.e[t] = 0;
 }
 
 // ------------------------------------------------------------ one packet
@@ -591,8 +649,7 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
 
     region_reset(reg, root);
     uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1;
-    uint32_t order = 0, b1 = 0, c2 = 0;
-    bool c2fresh = false;
+    uint32_t order = 0, b1 = 0;
     uint32_t low = 0, range = ~0u;
     bool ok = true, ovf = false;
     // software pipeline: the records of step i+1 are loaded during step i
@@ -601,81 +658,82 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     Rec<kO1Inl> r1;
     Rec<kO2Inl> r2;
     o2_fresh(0, r2);
-    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < kO1Inl; ++t) r1.e[t] = 0;
+    rec_clear(r1);
 
     for (uint32_t i = 0; i < len; ++i) {
-        const uint32_t v = inwin_take(in);
+        const uint32_t v = inwin_take(in, true);
         Rec<kO1Inl> n1;
         o1_load(reg, v, n1);                                         // next step's order-1 record
         Rec<kO2Inl> n2;
-        bool done = false, pend = false, nfresh = false;
-        uint32_t nxt = 0, kpend = 0;
+        o2_fresh(0, n2);
+        const bool en2 = order >= 2;
 
-        if (order >= 2) {                                            // order 2, compress.c:286-316
-            const uint32_t esc0 = r2.esc;
-            const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf);
-            if (ovf) break;
-            if (h.found) {
-                o2_store(reg, r2);
-                nxt = h.link;
-                if (nxt * kO2Rec == r2.off) n2 = r2; else o2_load(reg, nxt, n2);
-                ok = enc_code(low, range, esc0 + h.under, h.cnt, h.tot, o);
-                done = true;
-            } else {
-                pend = true;
-                kpend = h.k;
-                if (esc0 > 0 && esc0 < h.tot) ok = enc_code(low, range, 0, esc0, h.tot, o);
-            }
-            if (!ok) break;
-        }
-        if (!done && order >= 1) {                                   // order 1
-            const uint32_t esc0 = r1.esc;
-            const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf);
-            if (ovf) break;
-            nxt = h.link;
-            nfresh = !h.found;
-            if (pend) rec_set_link(reg, r2, kpend, nxt);
+        // order 2, compress.c:286-316
+        const uint32_t esc2 = r2.esc;
+        const Hit h2 = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, en2);
+        const bool done2 = en2 && h2.found;
+        enc_code(low, range, done2 ? esc2 + h2.under : 0u, done2 ? h2.cnt : esc2, h2.tot, o,
+                 done2 || (en2 && esc2 > 0 && esc2 < h2.tot), ok);
+        const bool pend = en2 && !h2.found;
+        uint32_t nxt = h2.link;
+
+        // order 1
+        const bool en1 = !done2 && order >= 1;
+        const uint32_t esc1 = r1.esc;
+        const Hit h1 = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf, en1);
+        const bool done1 = en1 && h1.found;
+        nxt = en1 ? h1.link : nxt;
+        const bool nfresh = en1 && !h1.found;
+        rec_set_link(reg, r2, h2.k, nxt, pend);
+        enc_code(low, range, done1 ? esc1 + h1.under : 0u, done1 ? h1.cnt : esc1, h1.tot, o,
+                 done1 || (en1 && esc1 > 0 && esc1 < h1.tot), ok);
+
+        // next order-2 record: fresh, the one just updated, or a load
+        const bool same2 = en2 && nxt * kO2Rec == r2.off;
+        if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
+        if (en1) o1_store(reg, r1);
+        if (en2) o2_store(reg, r2);
+
+        // root, compress.c:318-329
+        const bool en0 = !done2 && !done1;
+        uint32_t under0, cnt0;
+        root_lookup(root, v, under0, cnt0);
+        if (en0) root_add(root, v, cnt0);
+        nodes += (en0 && cnt0 == 0) ? 1u : 0u;
+        enc_code(low, range, 1 + under0, 1 + cnt0, rtot, o, en0, ok);
+        rtot = en0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
+        const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit);
+        if (any_lane(rs0)) { if (rs0) rtot = root_rescale(root); }
+
+        if (any_lane(!ok || ovf)) { if (!ok || ovf) break; }
+
+        // advance, compress.c:331-336
+        if (order >= 1) {
             if (nfresh) o2_fresh(nxt, n2);
-            else if (order >= 2 && nxt * kO2Rec == r2.off) n2 = r2;
-            else o2_load(reg, nxt, n2);
-            o1_store(reg, r1);
-            if (pend) o2_store(reg, r2);
-            if (h.found) { ok = enc_code(low, range, esc0 + h.under, h.cnt, h.tot, o); done = true; }
-            else if (esc0 > 0 && esc0 < h.tot) ok = enc_code(low, range, 0, esc0, h.tot, o);
-            if (!ok) break;
+            else if (same2) n2 = r2;
+            r2 = n2;
         }
-        if (!done) {                                                 // root, compress.c:318-329
-            uint32_t under, cnt;
-            root_lookup(root, v, under, cnt);
-            const uint32_t tot0 = rtot;
-            if (cnt == 0) ++nodes;
-            root_add(root, v, cnt);
-            ok = enc_code(low, range, 1 + under, 1 + cnt, tot0, o);
-            if (!ok) break;
-            rtot = (rtot + kRootDelta) & 0xFFFF;
-            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
-        }
-        if (order >= 1) { c2 = nxt; c2fresh = nfresh; r2 = n2; }     // compress.c:331-335
         // the prefetched order-1 record is stale when it is the one this step updated
-        if (!(order >= 1 && v == b1)) r1 = n1;
-        if (order < 2) ++order;
+        if (!(en1 && v == b1)) r1 = n1;
+        order += order < 2 ? 1u : 0u;
         b1 = v;
-        if (nodes >= kMaxNodes) {                                    // compress.c:148-157
-            region_reset(reg, root);
-            rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0;
+        if (any_lane(nodes >= kMaxNodes)) {                          // compress.c:148-157
+            if (nodes >= kMaxNodes) {
+                region_reset(reg, root);
+                rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0;
+            }
         }
     }
     if (ovf) { flag_exact(ws, pkt); return; }
-    if (ok) {                                                        // compress.c:139-146
-        while (low) {
-            if (o.n >= o.cap) { ok = false; break; }
-            outwin_put(o, low >> 24);
-            low <<= 8;
-        }
+    // flush, compress.c:139-146
+    while (any_lane(ok && low != 0)) {
+        const bool more = ok && low != 0;
+        const bool full = more && o.n >= o.cap;
+        ok = ok && !full;
+        outwin_put(o, low >> 24, more && !full);
+        low = (more && !full) ? low << 8 : low;
     }
-    if (ok) outwin_finish(o);
+    outwin_finish(o, ok);
     b.out_len[pkt] = ok ? o.n : 0u;
 }
 
@@ -694,115 +752,107 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
     uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1;
     uint32_t order = 0, b1 = 0;
     uint32_t low = 0, code = 0, range = ~0u;
-    for (int k = 0; k < 4; ++k) code = (code << 8) | inwin_take(in);   // compress.c:344-350
+    for (int k = 0; k < 4; ++k) code = (code << 8) | inwin_take(in, true);   // compress.c:344-350
     bool fail = false, anomaly = false, ovf = false;
     // the next step's records are loaded as soon as the symbol is decoded
     Rec<kO1Inl> r1;
     Rec<kO2Inl> r2;
     o2_fresh(0, r2);
-    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < kO1Inl; ++t) r1.e[t] = 0;
+    rec_clear(r1);
 
     for (;;) {
-        int at = -1;                         // context that produced the symbol (2, 1, 0)
-        uint32_t v = 0, nxt = 0;
-        bool nfresh = false;
+        // order 2, compress.c:529-568 (contexts with escapes == 0 are skipped)
+        const uint32_t tot2 = rec_total(reg, r2);
+        const bool try2 = order >= 2 && r2.esc > 0 && r2.esc < tot2;
+        uint32_t cd = dec_read(range, low, code, tot2, try2);
+        const bool sym2 = try2 && cd >= r2.esc;
+        const Hit h2 = rec_search(reg, r2, cd - r2.esc, sym2);
+        const bool miss2 = sym2 && !h2.found;
+        const bool done2 = sym2 && !miss2;
+        rec_bump(reg, r2, h2.k, h2.cnt, kSubDelta, done2);
+        dec_code(low, code, range, done2 ? r2.esc + h2.under : 0u, done2 ? h2.cnt : r2.esc, in,
+                 try2 && !miss2);
+        rec_rescale(reg, r2, done2 && (h2.cnt > 0xFF - 2 * kSubDelta || tot2 + kSubDelta > kTotalLimit));
+        uint32_t v = done2 ? h2.val : 0u;
+        uint32_t nxt = h2.link;
 
-        if (order >= 2 && r2.esc > 0) {                              // compress.c:529-568
-            const uint32_t tot = rec_total(reg, r2);
-            if (r2.esc < tot) {
-                range /= tot;
-                uint32_t cd = ((code - low) / range) & 0xFFFF;
-                if (cd < r2.esc) {
-                    dec_code(low, code, range, 0, r2.esc, in);
-                } else {
-                    cd -= r2.esc;
-                    Hit h;
-                    if (!rec_search(reg, r2, cd, h)) { fail = true; break; }
-                    v = h.val;
-                    rec_bump(reg, r2, h.k, h.cnt, kSubDelta);
-                    dec_code(low, code, range, r2.esc + h.under, h.cnt, in);
-                    if (h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit) rec_rescale(reg, r2);
-                    nxt = h.link;
-                    at = 2;
-                }
-            }
-        }
-        if (at < 0 && order >= 1 && r1.esc > 0) {
-            const uint32_t tot = rec_total(reg, r1);
-            if (r1.esc < tot) {
-                range /= tot;
-                uint32_t cd = ((code - low) / range) & 0xFFFF;
-                if (cd < r1.esc) {
-                    dec_code(low, code, range, 0, r1.esc, in);
-                } else {
-                    cd -= r1.esc;
-                    Hit h;
-                    if (!rec_search(reg, r1, cd, h)) { fail = true; break; }
-                    v = h.val;
-                    rec_bump(reg, r1, h.k, h.cnt, kSubDelta);
-                    dec_code(low, code, range, r1.esc + h.under, h.cnt, in);
-                    if (h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit) rec_rescale(reg, r1);
-                    nxt = h.link;
-                    at = 1;
-                }
-            }
-        }
-        if (at < 0) {                                                // root, compress.c:570-596
-            range /= rtot;
-            uint32_t cd = ((code - low) / range) & 0xFFFF;
-            if (cd < 1) { dec_code(low, code, range, 0, 1, in); break; }   // end of stream
-            cd -= 1;
-            if (cd >= rtot - 1) { anomaly = true; break; }          // past symbol 255
-            v = root_search(root, cd);
-            uint32_t under, cnt;
-            root_lookup(root, v, under, cnt);
-            if (cnt == 0) ++nodes;
-            root_add(root, v, cnt);
-            dec_code(low, code, range, 1 + under, 1 + cnt, in);
-            rtot = (rtot + kRootDelta) & 0xFFFF;
-            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
-            at = 0;
-        }
+        // order 1
+        const uint32_t tot1 = rec_total(reg, r1);
+        const bool try1 = !done2 && !miss2 && order >= 1 && r1.esc > 0 && r1.esc < tot1;
+        cd = dec_read(range, low, code, tot1, try1);
+        const bool sym1 = try1 && cd >= r1.esc;
+        const Hit h1 = rec_search(reg, r1, cd - r1.esc, sym1);
+        const bool miss1 = sym1 && !h1.found;
+        const bool done1 = sym1 && !miss1;
+        rec_bump(reg, r1, h1.k, h1.cnt, kSubDelta, done1);
+        dec_code(low, code, range, done1 ? r1.esc + h1.under : 0u, done1 ? h1.cnt : r1.esc, in,
+                 try1 && !miss1);
+        rec_rescale(reg, r1, done1 && (h1.cnt > 0xFF - 2 * kSubDelta || tot1 + kSubDelta > kTotalLimit));
+        v = done1 ? h1.val : v;
+        nxt = done1 ? h1.link : nxt;
+
+        // root, compress.c:570-596; a root escape is the end of the stream
+        const bool try0 = !done2 && !done1 && !miss2 && !miss1;
+        cd = dec_read(range, low, code, rtot, try0);
+        const bool end0 = try0 && cd < 1;
+        const bool bad0 = try0 && !end0 && cd - 1 >= rtot - 1;      // past symbol 255
+        const bool sym0 = try0 && !end0 && !bad0;
+        uint32_t v0 = 0;
+        if (sym0) v0 = root_search(root, cd - 1);
+        uint32_t under0 = 0, cnt0 = 0;
+        root_lookup(root, v0, under0, cnt0);
+        if (sym0) root_add(root, v0, cnt0);
+        nodes += (sym0 && cnt0 == 0) ? 1u : 0u;
+        dec_code(low, code, range, end0 ? 0u : 1 + under0, end0 ? 1u : 1 + cnt0, in, end0 || sym0);
+        rtot = sym0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
+        const bool rs0 = sym0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit);
+        if (any_lane(rs0)) { if (rs0) rtot = root_rescale(root); }
+        v = sym0 ? v0 : v;
+
+        fail = miss2 || miss1;
+        anomaly = bad0;
+        const bool live = done2 || done1 || sym0;
+
         Rec<kO1Inl> n1;
         o1_load(reg, v, n1);                                         // next step's order-1 record
+
         // patch the contexts above, compress.c:598-615
-        bool pend = false;
-        uint32_t kpend = 0;
-        if (order >= 2 && at < 2) {
-            const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf);
-            if (ovf) break;
-            if (!h.found) { pend = true; kpend = h.k; }
-        }
-        if (order >= 1 && at < 1) {
-            const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf);
-            if (ovf) break;
-            nxt = h.link;
-            nfresh = !h.found;
-        }
-        if (pend) rec_set_link(reg, r2, kpend, nxt);
+        const bool p2 = live && order >= 2 && !done2;
+        const Hit g2 = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, p2);
+        const bool pend = p2 && !g2.found;
+        const bool p1 = live && order >= 1 && sym0;
+        const Hit g1 = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf, p1);
+        nxt = p1 ? g1.link : nxt;
+        const bool nfresh = p1 && !g1.found;
+        rec_set_link(reg, r2, g2.k, nxt, pend);
+
         Rec<kO2Inl> n2;
-        if (order >= 1) {
-            if (nfresh) o2_fresh(nxt, n2);
-            else if (order >= 2 && nxt * kO2Rec == r2.off) n2 = r2;
-            else o2_load(reg, nxt, n2);
+        o2_fresh(nxt, n2);
+        const bool same2 = order >= 2 && nxt * kO2Rec == r2.off;
+        if (live && order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
+        if (live && order >= 2) o2_store(reg, r2);
+        if (live && order >= 1 && !done2) o1_store(reg, r1);
+
+        const bool full = live && o.n >= o.cap;                      // compress.c:617
+        fail = fail || full;
+        outwin_put(o, v, live && !full);
+        if (any_lane(!live || full || ovf)) { if (!live || full || ovf) break; }
+
+        if (order >= 1 && !same2) {          // field-wise: a struct select would go through scratch
+            r2.off = n2.off; r2.esc = n2.esc; r2.len = n2.len; r2.ext = n2.ext; r2.e[0] = n2.e[0];
         }
-        if (order >= 2) o2_store(reg, r2);
-        if (order >= 1 && at <= 1) o1_store(reg, r1);
-        if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
-        outwin_put(o, v);
-        if (order >= 1) r2 = n2;
-        if (!(order >= 1 && v == b1)) r1 = n1;
-        if (order < 2) ++order;
+        if (!(order >= 1 && v == b1 && !done2)) r1 = n1;
+        order += order < 2 ? 1u : 0u;
         b1 = v;
-        if (nodes >= kMaxNodes) {
-            region_reset(reg, root);
-            rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0;
+        if (any_lane(nodes >= kMaxNodes)) {
+            if (nodes >= kMaxNodes) {
+                region_reset(reg, root);
+                rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0;
+            }
         }
     }
     if (ovf || anomaly) { flag_exact(ws, pkt); return; }
-    if (!fail) outwin_finish(o);
+    outwin_finish(o, !fail);
     b.out_len[pkt] = fail ? 0u : o.n;
 }
 
@@ -860,9 +910,9 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
     if (blocks == 0) return static_cast<int>(hipErrorInvalidValue);
     const size_t lds = static_cast<size_t>(per_block) * kRootStride;
     if (decompress)
-        hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(kBlock), lds, st, *b, *ws);
+        hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(256), lds, st, *b, *ws);
     else
-        hipLaunchKernelGGL(rc_compress_lane, dim3(blocks), dim3(kBlock), lds, st, *b, *ws);
+        hipLaunchKernelGGL(rc_compress_lane, dim3(blocks), dim3(256), lds, st, *b, *ws);
     return static_cast<int>(hipGetLastError());
 }
 #endif  // RC_LANE_HOST_TEST
