@@ -737,6 +737,13 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     b.out_len[pkt] = ok ? o.n : 0u;
 }
 
+DEV void rec2_copy(Rec<kO2Inl>& d, const Rec<kO2Inl>& r)
+{
+    d.off = r.off; d.esc = r.esc; d.len = r.len; d.ext = r.ext; d.e[0] = r.e[0];
+}
+
+// The decoder keeps data-dependent branches: unlike the encoder, each level's
+// work (two divisions, a search) is only needed by the lanes that reach it.
 DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t pkt,
                         uint8_t* reg, uint8_t* root)
 {
@@ -761,88 +768,92 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
     rec_clear(r1);
 
     for (;;) {
-        // order 2, compress.c:529-568 (contexts with escapes == 0 are skipped)
-        const uint32_t tot2 = rec_total(reg, r2);
-        const bool try2 = order >= 2 && r2.esc > 0 && r2.esc < tot2;
-        uint32_t cd = dec_read(range, low, code, tot2, try2);
-        const bool sym2 = try2 && cd >= r2.esc;
-        const Hit h2 = rec_search(reg, r2, cd - r2.esc, sym2);
-        const bool miss2 = sym2 && !h2.found;
-        const bool done2 = sym2 && !miss2;
-        rec_bump(reg, r2, h2.k, h2.cnt, kSubDelta, done2);
-        dec_code(low, code, range, done2 ? r2.esc + h2.under : 0u, done2 ? h2.cnt : r2.esc, in,
-                 try2 && !miss2);
-        rec_rescale(reg, r2, done2 && (h2.cnt > 0xFF - 2 * kSubDelta || tot2 + kSubDelta > kTotalLimit));
-        uint32_t v = done2 ? h2.val : 0u;
-        uint32_t nxt = h2.link;
+        int at = -1;                         // context that produced the symbol (2, 1, 0)
+        uint32_t v = 0, nxt = 0;
+        bool nfresh = false;
 
-        // order 1
-        const uint32_t tot1 = rec_total(reg, r1);
-        const bool try1 = !done2 && !miss2 && order >= 1 && r1.esc > 0 && r1.esc < tot1;
-        cd = dec_read(range, low, code, tot1, try1);
-        const bool sym1 = try1 && cd >= r1.esc;
-        const Hit h1 = rec_search(reg, r1, cd - r1.esc, sym1);
-        const bool miss1 = sym1 && !h1.found;
-        const bool done1 = sym1 && !miss1;
-        rec_bump(reg, r1, h1.k, h1.cnt, kSubDelta, done1);
-        dec_code(low, code, range, done1 ? r1.esc + h1.under : 0u, done1 ? h1.cnt : r1.esc, in,
-                 try1 && !miss1);
-        rec_rescale(reg, r1, done1 && (h1.cnt > 0xFF - 2 * kSubDelta || tot1 + kSubDelta > kTotalLimit));
-        v = done1 ? h1.val : v;
-        nxt = done1 ? h1.link : nxt;
-
-        // root, compress.c:570-596; a root escape is the end of the stream
-        const bool try0 = !done2 && !done1 && !miss2 && !miss1;
-        cd = dec_read(range, low, code, rtot, try0);
-        const bool end0 = try0 && cd < 1;
-        const bool bad0 = try0 && !end0 && cd - 1 >= rtot - 1;      // past symbol 255
-        const bool sym0 = try0 && !end0 && !bad0;
-        uint32_t v0 = 0;
-        if (sym0) v0 = root_search(root, cd - 1);
-        uint32_t under0 = 0, cnt0 = 0;
-        root_lookup(root, v0, under0, cnt0);
-        if (sym0) root_add(root, v0, cnt0);
-        nodes += (sym0 && cnt0 == 0) ? 1u : 0u;
-        dec_code(low, code, range, end0 ? 0u : 1 + under0, end0 ? 1u : 1 + cnt0, in, end0 || sym0);
-        rtot = sym0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
-        const bool rs0 = sym0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit);
-        if (any_lane(rs0)) { if (rs0) rtot = root_rescale(root); }
-        v = sym0 ? v0 : v;
-
-        fail = miss2 || miss1;
-        anomaly = bad0;
-        const bool live = done2 || done1 || sym0;
-
+        if (order >= 2 && r2.esc > 0) {                              // compress.c:529-568
+            const uint32_t tot = rec_total(reg, r2);
+            if (r2.esc < tot) {
+                range /= tot;
+                uint32_t cd = ((code - low) / range) & 0xFFFF;
+                if (cd < r2.esc) {
+                    dec_code(low, code, range, 0, r2.esc, in, true);
+                } else {
+                    const Hit h = rec_search(reg, r2, cd - r2.esc, true);
+                    if (!h.found) { fail = true; break; }
+                    v = h.val;
+                    rec_bump(reg, r2, h.k, h.cnt, kSubDelta, true);
+                    dec_code(low, code, range, r2.esc + h.under, h.cnt, in, true);
+                    rec_rescale(reg, r2, h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit);
+                    nxt = h.link;
+                    at = 2;
+                }
+            }
+        }
+        if (at < 0 && order >= 1 && r1.esc > 0) {
+            const uint32_t tot = rec_total(reg, r1);
+            if (r1.esc < tot) {
+                range /= tot;
+                uint32_t cd = ((code - low) / range) & 0xFFFF;
+                if (cd < r1.esc) {
+                    dec_code(low, code, range, 0, r1.esc, in, true);
+                } else {
+                    const Hit h = rec_search(reg, r1, cd - r1.esc, true);
+                    if (!h.found) { fail = true; break; }
+                    v = h.val;
+                    rec_bump(reg, r1, h.k, h.cnt, kSubDelta, true);
+                    dec_code(low, code, range, r1.esc + h.under, h.cnt, in, true);
+                    rec_rescale(reg, r1, h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit);
+                    nxt = h.link;
+                    at = 1;
+                }
+            }
+        }
+        if (at < 0) {                                                // root, compress.c:570-596
+            range /= rtot;
+            uint32_t cd = ((code - low) / range) & 0xFFFF;
+            if (cd < 1) { dec_code(low, code, range, 0, 1, in, true); break; }   // end of stream
+            cd -= 1;
+            if (cd >= rtot - 1) { anomaly = true; break; }          // past symbol 255
+            v = root_search(root, cd);
+            uint32_t under, cnt;
+            root_lookup(root, v, under, cnt);
+            if (cnt == 0) ++nodes;
+            root_add(root, v, cnt);
+            dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
+            rtot = (rtot + kRootDelta) & 0xFFFF;
+            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
+            at = 0;
+        }
         Rec<kO1Inl> n1;
         o1_load(reg, v, n1);                                         // next step's order-1 record
-
         // patch the contexts above, compress.c:598-615
-        const bool p2 = live && order >= 2 && !done2;
-        const Hit g2 = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, p2);
-        const bool pend = p2 && !g2.found;
-        const bool p1 = live && order >= 1 && sym0;
-        const Hit g1 = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf, p1);
-        nxt = p1 ? g1.link : nxt;
-        const bool nfresh = p1 && !g1.found;
-        rec_set_link(reg, r2, g2.k, nxt, pend);
-
+        bool pend = false;
+        uint32_t kpend = 0;
+        if (order >= 2 && at < 2) {
+            const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, true);
+            if (ovf) break;
+            if (!h.found) { pend = true; kpend = h.k; }
+        }
+        if (order >= 1 && at < 1) {
+            const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf, true);
+            if (ovf) break;
+            nxt = h.link;
+            nfresh = !h.found;
+        }
+        rec_set_link(reg, r2, kpend, nxt, pend);
         Rec<kO2Inl> n2;
         o2_fresh(nxt, n2);
         const bool same2 = order >= 2 && nxt * kO2Rec == r2.off;
-        if (live && order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
-        if (live && order >= 2) o2_store(reg, r2);
-        if (live && order >= 1 && !done2) o1_store(reg, r1);
-
-        const bool full = live && o.n >= o.cap;                      // compress.c:617
-        fail = fail || full;
-        outwin_put(o, v, live && !full);
-        if (any_lane(!live || full || ovf)) { if (!live || full || ovf) break; }
-
-        if (order >= 1 && !same2) {          // field-wise: a struct select would go through scratch
-            r2.off = n2.off; r2.esc = n2.esc; r2.len = n2.len; r2.ext = n2.ext; r2.e[0] = n2.e[0];
-        }
-        if (!(order >= 1 && v == b1 && !done2)) r1 = n1;
-        order += order < 2 ? 1u : 0u;
+        if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
+        if (order >= 2) o2_store(reg, r2);
+        if (order >= 1 && at <= 1) o1_store(reg, r1);
+        if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
+        outwin_put(o, v, true);
+        if (order >= 1 && !same2) rec2_copy(r2, n2);
+        if (!(order >= 1 && v == b1)) r1 = n1;
+        if (order < 2) ++order;
         b1 = v;
         if (any_lane(nodes >= kMaxNodes)) {
             if (nodes >= kMaxNodes) {
