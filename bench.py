@@ -145,10 +145,12 @@ def main():
     t_dom = t_dec if dom_is_dec else t_comp
     alg = alg_d if dom_is_dec else alg_c
     achieved = alg / t_dom / 1e9
+    kname = "rc_decompress_lane" if dom_is_dec else "rc_compress_lane"
+    traffic, tsrc = measured_traffic(kname, args.workload, n)
     roofline = {
-        "kernel": "rc_decompress_wave" if dom_is_dec else "rc_compress_wave",
+        "kernel": kname,
         "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": None,
+        "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "traffic_source": tsrc,
         "alg_bytes_per_launch": alg, "launch_ms": round(t_dom * 1e3, 4),
         "compress_ms": round(t_comp * 1e3, 4), "decompress_ms": round(t_dec * 1e3, 4),
     }
@@ -182,7 +184,7 @@ def main():
         result["pcie_inclusive"] = pcie_inclusive(coder, d, o, l, args)
 
     if world > 1 and not args.no_rccl:
-        rs = rccl_scatter_gather(dist, dev, din, cout, clen, coff, world, rank)
+        rs = rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank)
         if rank == 0:
             result["rccl_scatter_gather"] = rs
 
@@ -229,54 +231,72 @@ def pcie_inclusive(coder, d, o, l, args):
             "bit_exact": ok, "note": "host pinned staging memcpy + H2D + kernels + D2H + host memcpy, best of 3"}
 
 
-def rccl_scatter_gather(dist, dev, din, cout, clen, coff, world, rank):
-    """Times an RCCL scatter of one shard per rank from rank 0 and the gather
-    of the compressed shards back (grouped send/recv over xGMI)."""
+def rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank):
+    """End-to-end sharded pipeline from one root GPU: rank 0 scatters a batch
+    of world x (this shard's packets) over RCCL (grouped isend/irecv on the
+    direct xGMI links), every rank compresses its shard, and the compressed
+    packets are gathered back to rank 0 (enet_amd/shard.py).  Reported beside
+    the device-resident number; not part of the timed region of `value`."""
     import torch
-    shard = din.numel()
-    send = torch.empty(shard * world, dtype=torch.uint8, device=dev) if rank == 0 else None
-    recv = torch.empty(shard, dtype=torch.uint8, device=dev)
-    times = []
-    for it in range(4):
+    from enet_amd import shard
+    n = dlen.numel()
+    if rank == 0:
+        big = din.repeat(world)
+        blen = dlen.repeat(world)
+        boff = torch.zeros_like(blen, dtype=torch.int64)
+        boff[1:] = torch.cumsum(blen[:-1].to(torch.int64), 0)
+    else:
+        big = boff = blen = None
+    best = None
+    for it in range(3):
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ops = []
-        if rank == 0:
-            for r in range(1, world):
-                ops.append(dist.P2POp(dist.isend, send[r * shard:(r + 1) * shard], r))
-            recv.copy_(send[:shard])
-        else:
-            ops.append(dist.P2POp(dist.irecv, recv, 0))
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+        pay, poff, pln = shard.scatter_batch(dist, big, boff, blen, device=dev)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        # gather compressed payload sizes then payloads (padded to the max)
-        tot = clen.to(torch.int64).sum().view(1)
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.all_gather(sizes, tot)
-        mx = int(max(s.item() for s in sizes))
-        buf = torch.empty(mx, dtype=torch.uint8, device=dev)
-        buf[: int(tot.item())].copy_(cout[: int(tot.item())])
-        ops = []
-        if rank == 0:
-            gathered = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world - 1)]
-            for r in range(1, world):
-                ops.append(dist.P2POp(dist.irecv, gathered[r - 1], r))
-        else:
-            ops.append(dist.P2POp(dist.isend, buf, 0))
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+        cap = (2 * pln.to(torch.int64) + 64).to(torch.int32)
+        coff = torch.zeros(pln.numel(), dtype=torch.int64, device=dev)
+        coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+        cout = torch.empty(int(coff[-1] + cap[-1]), dtype=torch.uint8, device=dev)
+        clen = torch.zeros_like(pln)
+        coder.compress_batch(pay, poff, pln, cout, coff, cap, clen, max_len=max_len)
+        res, rl = shard.pack_results(cout, coff, clen)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        if it > 0:
-            times.append((t1 - t0, t2 - t1))
-    sc = min(t[0] for t in times)
-    ga = min(t[1] for t in times)
-    return {"scatter_ms": round(sc * 1e3, 3), "gather_ms": round(ga * 1e3, 3),
-            "scatter_GBps": round(shard * (world - 1) / sc / 1e9, 2),
-            "note": "rank0 -> ranks grouped isend/irecv (RCCL over xGMI), not in the timed region"}
+        parts = shard.gather_results(dist, res, rl)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        tt = torch.tensor([t1 - t0, t2 - t1, t3 - t2], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        if it > 0 and (best is None or tt.sum() < sum(best)):
+            best = [float(x) for x in tt.tolist()]
+    payload = float(dlen.to(torch.int64).sum().item()) * world
+    sc, co, ga = best
+    return {"scatter_ms": round(sc * 1e3, 3), "compress_ms": round(co * 1e3, 3), "gather_ms": round(ga * 1e3, 3),
+            "end_to_end_GiBps": round(payload / (sc + co + ga) / GIB, 4),
+            "scatter_GBps": round(payload * (world - 1) / world / sc / 1e9, 2),
+            "packets": n * world,
+            "note": "rank0 scatters world x shard over RCCL (xGMI), ranks compress, results gathered to rank0; "
+                    "separate from the timed region of value"}
+
+
+def measured_traffic(kernel, workload, packets):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/traffic_latest.json, written by tools/traffic.py from
+    separate --pmc passes of this same bench command), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("workload") != workload or t.get("packets") != packets:
+        return None, None
+    k = t.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k.get("hbm_bytes_per_launch"), "profiles/traffic_latest.json (" + t.get("source", "") + ")"
 
 
 def cpu_baseline(d, o, l, threads):

@@ -49,13 +49,16 @@ static int ws_reserve(rc_ctx *c, size_t n)
     if (n <= c->ws.n_cap) return 0;
     size_t cap = c->ws.n_cap ? c->ws.n_cap : 1024;
     while (cap < n) cap *= 2;
-    uint32_t *fl = NULL;
+    uint32_t *fl = NULL, *ord = NULL;
     if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) return -1;
+    if (hipMalloc((void **) &ord, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(fl); return -1; }
     if (c->ws.flag_list) {
-        hipStreamSynchronize(c->stream);
+        hipDeviceSynchronize();
         hipFree(c->ws.flag_list);
+        hipFree(c->ws.order);
     }
     c->ws.flag_list = fl;
+    c->ws.order = ord;
     c->ws.n_cap = (uint32_t) cap;
     return 0;
 }
@@ -106,6 +109,7 @@ void *enet_range_coder_create(void)
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) goto fail;
     if (hipMalloc((void **) &c->ws.counters, 16) != hipSuccess) goto fail;
+    if (hipMalloc((void **) &c->ws.bins, RC_LEN_BINS * sizeof(uint32_t)) != hipSuccess) goto fail;
     c->ws.exact_slots = EXACT_SLOTS;
     if (hipMalloc(&c->ws.exact_pool, (size_t) EXACT_SLOTS * RC_EXACT_POOL_BYTES) != hipSuccess) goto fail;
     if (ws_reserve(c, 1024) != 0) goto fail;
@@ -130,6 +134,8 @@ void enet_range_coder_destroy(void *context)
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->ws.flag_list) hipFree(c->ws.flag_list);
     if (c->ws.counters) hipFree(c->ws.counters);
+    if (c->ws.order) hipFree(c->ws.order);
+    if (c->ws.bins) hipFree(c->ws.bins);
     if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
     if (c->d_stage) hipFree(c->d_stage);

@@ -896,10 +896,50 @@ DEV void lane_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
-    for (uint32_t pkt = slot; pkt < b.n; pkt += gridDim.x * per_block) {
+    for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
+        const uint32_t pkt = ws.order ? ws.order[i] : i;
         if (DECOMP) decompress_one(b, ws, pkt, reg, root);
         else compress_one(b, ws, pkt, reg, root);
     }
+}
+
+// ---------------------------------------------------------- ragged batches
+// The 64 packets of a wavefront advance in lock-step, so a wavefront lasts
+// as long as its longest packet.  For batches of mixed lengths (config C4)
+// the packets are first binned by length (16-B bins, longest first) and the
+// lane kernels walk that order.  Order inside a bin is arbitrary; it only
+// affects scheduling, never results.
+__device__ __forceinline__ uint32_t len_bin(uint32_t len)
+{
+    const uint32_t b = len >> 4;
+    return RC_LEN_BINS - 1 - (b < RC_LEN_BINS - 1 ? b : RC_LEN_BINS - 1);
+}
+
+extern "C" __global__ void rc_len_hist(const uint32_t* len, uint32_t n, uint32_t* bins)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&bins[len_bin(len[i])], 1u);
+}
+
+extern "C" __global__ __launch_bounds__(RC_LEN_BINS) void rc_len_scan(uint32_t* bins)
+{
+    __shared__ uint32_t s[RC_LEN_BINS];
+    const uint32_t t = threadIdx.x;
+    s[t] = bins[t];
+    __syncthreads();
+    for (uint32_t d = 1; d < RC_LEN_BINS; d <<= 1) {
+        const uint32_t x = t >= d ? s[t - d] : 0u;
+        __syncthreads();
+        s[t] += x;
+        __syncthreads();
+    }
+    bins[t] = s[t] - bins[t];            // exclusive prefix = first slot of the bin
+}
+
+extern "C" __global__ void rc_len_scatter(const uint32_t* len, uint32_t n, uint32_t* bins, uint32_t* order)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) order[atomicAdd(&bins[len_bin(len[i])], 1u)] = i;
 }
 
 extern "C" __global__ __launch_bounds__(256)
@@ -920,10 +960,21 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
     if (blocks > maxb) blocks = maxb;
     if (blocks == 0) return static_cast<int>(hipErrorInvalidValue);
     const size_t lds = static_cast<size_t>(per_block) * kRootStride;
+    rc_workspace_dev w = *ws;
+    w.order = nullptr;
+    if (b->n >= 1024 && ws->order && ws->bins) {        // bin packets by length (ragged batches)
+        hipError_t e = hipMemsetAsync(ws->bins, 0, RC_LEN_BINS * sizeof(uint32_t), st);
+        if (e != hipSuccess) return static_cast<int>(e);
+        const uint32_t g = (b->n + 255) / 256;
+        hipLaunchKernelGGL(rc_len_hist, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins);
+        hipLaunchKernelGGL(rc_len_scan, dim3(1), dim3(RC_LEN_BINS), 0, st, ws->bins);
+        hipLaunchKernelGGL(rc_len_scatter, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins, ws->order);
+        w.order = ws->order;
+    }
     if (decompress)
-        hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(256), lds, st, *b, *ws);
+        hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(256), lds, st, *b, w);
     else
-        hipLaunchKernelGGL(rc_compress_lane, dim3(blocks), dim3(256), lds, st, *b, *ws);
+        hipLaunchKernelGGL(rc_compress_lane, dim3(blocks), dim3(256), lds, st, *b, w);
     return static_cast<int>(hipGetLastError());
 }
 #endif  // RC_LANE_HOST_TEST

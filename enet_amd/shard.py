@@ -1,0 +1,136 @@
+"""Sharding packet batches across GPUs.
+
+Packets are independent (compress.c keeps no state across calls,
+:252-265), so a batch shards into contiguous packet ranges with no exchange
+during coding.  The only collectives are the scatter of a batch from a root
+rank and the gather of the results, done with grouped point-to-point
+send/recv -- on MI355X that is RCCL over the direct xGMI link between each
+pair of GPUs (backend "nccl"); on CPU the same code runs over gloo, which is
+how it is tested.
+
+Layout on the wire, per destination rank: a small int64 header
+[n_packets, payload_bytes], then the packet lengths (int32) and the payload
+bytes (uint8); offsets are rebuilt locally as the exclusive cumsum of the
+lengths.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+
+def shard_ranges(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous packet ranges [start, end) for ``world`` ranks with about
+    equal payload bytes each (config C4 balances by sum of N)."""
+    ln = np.asarray(lengths, dtype=np.int64)
+    n = len(ln)
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    cum = np.concatenate([[0], np.cumsum(ln)])
+    total = cum[-1]
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(cum, total * r / world, side="left")))
+    cuts.append(n)
+    cuts = np.maximum.accumulate(np.minimum(np.asarray(cuts), n))
+    return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
+
+
+def _offsets(lengths):
+    import torch
+    off = torch.zeros_like(lengths, dtype=torch.int64)
+    if lengths.numel() > 1:
+        off[1:] = torch.cumsum(lengths[:-1].to(torch.int64), 0)
+    return off
+
+
+def scatter_batch(dist, data, offsets, lengths, root: int = 0, device=None):
+    """Scatter a packet batch held by ``root`` (``data``/``offsets``/``lengths``
+    tensors; ignored on other ranks) into per-rank shards.  Every rank returns
+    its shard as (data, offsets, lengths) on ``device``."""
+    import torch
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = device if device is not None else (data.device if data is not None else torch.device("cpu"))
+    hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+    if rank == root:
+        ln_cpu = lengths.to("cpu")
+        ranges = shard_ranges(ln_cpu.numpy(), world)
+        ops, keep = [], None
+        off_cpu = offsets.to("cpu")
+        for r, (a, b) in enumerate(ranges):
+            if a < b:
+                lo = int(off_cpu[a]); hi = int(off_cpu[b - 1] + ln_cpu[b - 1])
+            else:
+                lo = hi = 0
+            h = torch.tensor([b - a, hi - lo], dtype=torch.int64, device=dev)
+            ln_r = lengths[a:b].to(device=dev, dtype=torch.int32).contiguous()
+            pay = data[lo:hi].to(dev).contiguous()
+            if r == root:
+                keep = (pay, ln_r)
+                continue
+            dist.send(h, r)
+            if b > a:
+                ops.append(dist.P2POp(dist.isend, ln_r, r))
+                ops.append(dist.P2POp(dist.isend, pay, r))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        pay, ln_r = keep
+        return pay, _offsets(ln_r), ln_r
+    dist.recv(hdr, root)
+    n, nbytes = int(hdr[0]), int(hdr[1])
+    ln_r = torch.empty(n, dtype=torch.int32, device=dev)
+    pay = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    if n:
+        ops = [dist.P2POp(dist.irecv, ln_r, root), dist.P2POp(dist.irecv, pay, root)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return pay, _offsets(ln_r), ln_r
+
+
+def pack_results(out, out_off, out_len):
+    """Compacts per-packet results (out[out_off[i] : +out_len[i]]) into one
+    contiguous byte tensor; returns (bytes, lengths)."""
+    import torch
+    n = out_len.numel()
+    if n == 0:
+        return torch.empty(0, dtype=torch.uint8, device=out.device), out_len
+    ln = out_len.to(torch.int64)
+    dst = _offsets(ln)
+    total = int((dst[-1] + ln[-1]).item())
+    idx = torch.repeat_interleave(out_off.to(torch.int64) - dst, ln) + torch.arange(total, device=out.device)
+    return out[idx], out_len
+
+
+def gather_results(dist, payload, lengths, root: int = 0):
+    """Gather each rank's packed results (bytes + int32 lengths) to ``root``.
+    Returns on root a list of (payload, lengths) in rank order; None elsewhere."""
+    import torch
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = payload.device
+    hdr = torch.tensor([lengths.numel(), payload.numel()], dtype=torch.int64, device=dev)
+    if rank != root:
+        dist.send(hdr, root)
+        if lengths.numel():
+            ops = [dist.P2POp(dist.isend, lengths.to(torch.int32).contiguous(), root),
+                   dist.P2POp(dist.isend, payload.contiguous(), root)]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return None
+    parts = [None] * world
+    parts[root] = (payload, lengths)
+    for r in range(world):
+        if r == root:
+            continue
+        h = torch.zeros(2, dtype=torch.int64, device=dev)
+        dist.recv(h, r)
+        n, nb = int(h[0]), int(h[1])
+        ln = torch.empty(n, dtype=torch.int32, device=dev)
+        pay = torch.empty(nb, dtype=torch.uint8, device=dev)
+        if n:
+            ops = [dist.P2POp(dist.irecv, ln, r), dist.P2POp(dist.irecv, pay, r)]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        parts[r] = (pay, ln)
+    return parts
