@@ -40,7 +40,7 @@ typedef struct {
     uint32_t  kernel;       /* RC_KERNEL_* */
     uint32_t  lane_active;  /* lane kernels: packets per wavefront (64, 32 or 16) */
     uint32_t *order;        /* [n_cap] processing order (packets binned by length), lane kernels */
-    uint32_t *bins;         /* [RC_LEN_BINS] length-bin counters */
+    uint32_t *bins;         /* [RC_LEN_BINS + 1] length-bin counters + uniform flag */
 } rc_workspace_dev;
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */

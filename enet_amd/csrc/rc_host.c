@@ -109,7 +109,7 @@ void *enet_range_coder_create(void)
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) goto fail;
     if (hipMalloc((void **) &c->ws.counters, 16) != hipSuccess) goto fail;
-    if (hipMalloc((void **) &c->ws.bins, RC_LEN_BINS * sizeof(uint32_t)) != hipSuccess) goto fail;
+    if (hipMalloc((void **) &c->ws.bins, (RC_LEN_BINS + 1) * sizeof(uint32_t)) != hipSuccess) goto fail;
     c->ws.exact_slots = EXACT_SLOTS;
     if (hipMalloc(&c->ws.exact_pool, (size_t) EXACT_SLOTS * RC_EXACT_POOL_BYTES) != hipSuccess) goto fail;
     if (ws_reserve(c, 1024) != 0) goto fail;

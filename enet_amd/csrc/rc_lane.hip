@@ -896,8 +896,9 @@ DEV void lane_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
+    const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
-        const uint32_t pkt = ws.order ? ws.order[i] : i;
+        const uint32_t pkt = order ? order[i] : i;
         if (DECOMP) decompress_one(b, ws, pkt, reg, root);
         else compress_one(b, ws, pkt, reg, root);
     }
@@ -915,31 +916,88 @@ __device__ __forceinline__ uint32_t len_bin(uint32_t len)
     return RC_LEN_BINS - 1 - (b < RC_LEN_BINS - 1 ? b : RC_LEN_BINS - 1);
 }
 
-extern "C" __global__ void rc_len_hist(const uint32_t* len, uint32_t n, uint32_t* bins)
+constexpr uint32_t kBinChunk = 4096;     // packets per binning workgroup (16 per thread)
+
+// Wave-aggregated LDS histogram of one element per lane: lanes that share a
+// bin are served by one LDS atomic (uniform batches take a single pass).
+// Returns the element's rank among the workgroup's elements of its bin.
+__device__ __forceinline__ uint32_t bin_rank(uint32_t* hist, uint32_t bin, bool valid)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&bins[len_bin(len[i])], 1u);
+    uint64_t rem = __ballot(valid);
+    const uint64_t below = (1ull << (threadIdx.x & 63)) - 1;
+    uint32_t rank = 0;
+    while (rem) {
+        const int leader = __ffsll(static_cast<unsigned long long>(rem)) - 1;
+        const uint32_t lb = __shfl(bin, leader);
+        const bool mine = valid && bin == lb;
+        const uint64_t peers = __ballot(mine);
+        uint32_t base = 0;
+        if ((threadIdx.x & 63) == static_cast<uint32_t>(leader))
+            base = atomicAdd(&hist[lb], static_cast<uint32_t>(__popcll(peers)));
+        base = __shfl(base, leader);
+        if (mine) rank = base + static_cast<uint32_t>(__popcll(peers & below));
+        rem &= ~peers;
+    }
+    return rank;
 }
 
+extern "C" __global__ __launch_bounds__(256) void rc_len_hist(const uint32_t* len, uint32_t n, uint32_t* bins)
+{
+    __shared__ uint32_t h[RC_LEN_BINS];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kBinChunk;
+    for (uint32_t k = 0; k < kBinChunk / 256; ++k) {
+        const uint32_t i = base + k * 256 + threadIdx.x;
+        (void) bin_rank(h, i < n ? len_bin(len[i]) : 0u, i < n);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
+}
+
+// Exclusive prefix over the bins; bins[RC_LEN_BINS] = 1 when every packet
+// falls in one bin (uniform lengths: the lane kernels then keep batch order).
 extern "C" __global__ __launch_bounds__(RC_LEN_BINS) void rc_len_scan(uint32_t* bins)
 {
     __shared__ uint32_t s[RC_LEN_BINS];
     const uint32_t t = threadIdx.x;
-    s[t] = bins[t];
-    __syncthreads();
+    const uint32_t mine = bins[t];
+    s[t] = mine;
+    const int used = __syncthreads_count(mine != 0);
     for (uint32_t d = 1; d < RC_LEN_BINS; d <<= 1) {
         const uint32_t x = t >= d ? s[t - d] : 0u;
         __syncthreads();
         s[t] += x;
         __syncthreads();
     }
-    bins[t] = s[t] - bins[t];            // exclusive prefix = first slot of the bin
+    bins[t] = s[t] - mine;               // exclusive prefix = first slot of the bin
+    if (t == 0) bins[RC_LEN_BINS] = used <= 1 ? 1u : 0u;
 }
 
-extern "C" __global__ void rc_len_scatter(const uint32_t* len, uint32_t n, uint32_t* bins, uint32_t* order)
+extern "C" __global__ __launch_bounds__(256)
+void rc_len_scatter(const uint32_t* len, uint32_t n, uint32_t* bins, uint32_t* order)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) order[atomicAdd(&bins[len_bin(len[i])], 1u)] = i;
+    if (bins[RC_LEN_BINS]) return;       // uniform: identity order
+    __shared__ uint32_t h[RC_LEN_BINS];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * kBinChunk;
+    uint32_t rank[kBinChunk / 256], bin[kBinChunk / 256];
+#pragma unroll
+    for (uint32_t k = 0; k < kBinChunk / 256; ++k) {
+        const uint32_t i = base + k * 256 + threadIdx.x;
+        bin[k] = i < n ? len_bin(len[i]) : 0u;
+        rank[k] = bin_rank(h, bin[k], i < n);
+    }
+    __syncthreads();
+    const uint32_t c = h[threadIdx.x];
+    if (c) h[threadIdx.x] = atomicAdd(&bins[threadIdx.x], c);   // this workgroup's slots in the bin
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kBinChunk / 256; ++k) {
+        const uint32_t i = base + k * 256 + threadIdx.x;
+        if (i < n) order[h[bin[k]] + rank[k]] = i;
+    }
 }
 
 extern "C" __global__ __launch_bounds__(256)
@@ -963,9 +1021,9 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
     rc_workspace_dev w = *ws;
     w.order = nullptr;
     if (b->n >= 1024 && ws->order && ws->bins) {        // bin packets by length (ragged batches)
-        hipError_t e = hipMemsetAsync(ws->bins, 0, RC_LEN_BINS * sizeof(uint32_t), st);
+        hipError_t e = hipMemsetAsync(ws->bins, 0, (RC_LEN_BINS + 1) * sizeof(uint32_t), st);
         if (e != hipSuccess) return static_cast<int>(e);
-        const uint32_t g = (b->n + 255) / 256;
+        const uint32_t g = (b->n + kBinChunk - 1) / kBinChunk;
         hipLaunchKernelGGL(rc_len_hist, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins);
         hipLaunchKernelGGL(rc_len_scan, dim3(1), dim3(RC_LEN_BINS), 0, st, ws->bins);
         hipLaunchKernelGGL(rc_len_scatter, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins, ws->order);

@@ -73,8 +73,8 @@ int enet_host_compress_with_range_coder(ENetHost *host);
  * and its result goes to out[out_off[i] .. +out_cap[i]); out_len[i] receives
  * exactly what enet_range_coder_compress (single buffer, inLimit = in_len[i],
  * outLimit = out_cap[i]) or enet_range_coder_decompress would return.
- * max_len bounds in_len[] (it sizes the per-wave LDS arena; longer packets
- * are still handled, on the slower exact path); 0 means 4096.
+ * max_len bounds in_len[] (it sizes each lane's model region in HBM; longer
+ * packets are still handled, on the slower exact path); 0 means 4096.
  * Return value: 0 on success, otherwise a HIP error code. */
 
 /* All pointers are DEVICE pointers; work is enqueued on `stream` (a

@@ -1,0 +1,178 @@
+/* enet_loopback.c -- live ENet hosts over 127.0.0.1 with the range coder
+ * enabled (enet_host_compress_with_range_coder, enet.h:574), used to show the
+ * drop-in: the same source is linked once against the reference library
+ * (compress.c inside) and once against the reference library WITHOUT
+ * compress.c plus libenet_rc_amd.so (oracle/Makefile, targets loopback_ref /
+ * loopback_amd).  Peers of either build talk to each other, so the GPU coder's
+ * datagrams are decoded by compress.c and vice versa (tests/test_integration.py).
+ *
+ *   enet_loopback both   PORT COUNT   two hosts in this process
+ *   enet_loopback server PORT COUNT   echo COUNT packets back, then exit
+ *   enet_loopback client PORT COUNT   send COUNT packets, check the echoes
+ *
+ * Payloads are low-entropy "game state" records so that datagrams compress
+ * (protocol.c:1696 only sends the compressed form when it is smaller).
+ * Prints one JSON line; exit status 0 iff every echo matched. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <enet/enet.h>
+
+extern const char *enet_rc_version(void) __attribute__((weak));
+
+static uint64_t mix(uint64_t *s)
+{
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* packet k: 40..1300 bytes of 24-B entity records with small deltas */
+static size_t make_payload(uint32_t k, uint8_t *p)
+{
+    uint64_t s = 0x454E4554ull + k;
+    size_t n = 40 + (size_t) (mix(&s) % 1261);
+    uint16_t pos[3] = { (uint16_t) mix(&s), (uint16_t) mix(&s), (uint16_t) mix(&s) };
+    for (size_t i = 0; i < n; ++i) {
+        size_t f = i % 24;
+        if (f == 0) {
+            for (int a = 0; a < 3; ++a) pos[a] = (uint16_t) (pos[a] + (int) (mix(&s) % 7) - 3);
+            p[i] = (uint8_t) (i / 24 + k);
+        } else if (f == 1) p[i] = 1;
+        else if (f >= 2 && f < 8) p[i] = (uint8_t) (pos[(f - 2) / 2] >> (8 * (f & 1)));
+        else if (f == 8) p[i] = (uint8_t) (mix(&s) % 4);
+        else if (f == 11) p[i] = 100;
+        else p[i] = 0;
+    }
+    return n;
+}
+
+static double now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+static ENetHost *mk_host(const ENetAddress *a, int *rc)
+{
+    ENetHost *h = enet_host_create(a, 4, 2, 0, 0);
+    if (!h) { fprintf(stderr, "enet_host_create failed\n"); exit(2); }
+    *rc = enet_host_compress_with_range_coder(h);
+    if (*rc != 0) { fprintf(stderr, "enet_host_compress_with_range_coder = %d\n", *rc); exit(3); }
+    return h;
+}
+
+typedef struct {
+    ENetHost *host;
+    ENetPeer *peer;
+    int is_client, connected, done;
+    uint32_t count, sent, got, bad;
+    uint64_t raw_bytes;
+} Side;
+
+static void pump(Side *s)
+{
+    ENetEvent ev;
+    while (enet_host_service(s->host, &ev, 0) > 0) {
+        switch (ev.type) {
+        case ENET_EVENT_TYPE_CONNECT:
+            s->connected = 1;
+            s->peer = ev.peer;
+            break;
+        case ENET_EVENT_TYPE_RECEIVE: {
+            if (s->is_client) {
+                uint8_t want[1400];
+                size_t n = make_payload(s->got, want);
+                if (ev.packet->dataLength != n || memcmp(ev.packet->data, want, n) != 0) ++s->bad;
+                ++s->got;
+                if (s->got == s->count) s->done = 1;
+            } else {                       /* echo */
+                ENetPacket *e = enet_packet_create(ev.packet->data, ev.packet->dataLength,
+                                                   ENET_PACKET_FLAG_RELIABLE);
+                enet_peer_send(ev.peer, 0, e);
+                s->raw_bytes += ev.packet->dataLength;
+                if (++s->got == s->count) s->done = 1;
+            }
+            enet_packet_destroy(ev.packet);
+            break;
+        }
+        case ENET_EVENT_TYPE_DISCONNECT:
+            s->connected = 0;
+            break;
+        default:
+            break;
+        }
+    }
+    if (s->is_client && s->connected) {
+        /* keep a window of packets in flight */
+        while (s->sent < s->count && s->sent < s->got + 64) {
+            uint8_t buf[1400];
+            size_t n = make_payload(s->sent, buf);
+            enet_peer_send(s->peer, 0, enet_packet_create(buf, n, ENET_PACKET_FLAG_RELIABLE));
+            s->raw_bytes += n;
+            ++s->sent;
+        }
+        enet_host_flush(s->host);
+    }
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 4) { fprintf(stderr, "usage: %s both|server|client PORT COUNT\n", argv[0]); return 2; }
+    const char *role = argv[1];
+    const int both = !strcmp(role, "both"), server = both || !strcmp(role, "server"),
+              client = both || !strcmp(role, "client");
+    uint32_t count = (uint32_t) strtoul(argv[3], NULL, 10);
+    if (enet_initialize() != 0) return 2;
+    ENetAddress addr;
+    enet_address_set_host(&addr, "127.0.0.1");
+    addr.port = (enet_uint16) atoi(argv[2]);
+
+    Side sv, cl;
+    memset(&sv, 0, sizeof sv);
+    memset(&cl, 0, sizeof cl);
+    int rc = 0;
+    if (server) { sv.host = mk_host(&addr, &rc); sv.count = count; }
+    if (client) {
+        cl.host = mk_host(NULL, &rc);
+        cl.is_client = 1;
+        cl.count = count;
+        cl.peer = enet_host_connect(cl.host, &addr, 2, 0);
+        if (!cl.peer) return 4;
+    }
+    double t0 = now(), deadline = t0 + 60.0;
+    while (now() < deadline) {
+        if (server) pump(&sv);
+        if (client) pump(&cl);
+        if ((!server || sv.done) && (!client || cl.done)) break;
+        if (!both) {                     /* block briefly in the single-role modes */
+            ENetHost *h = server ? sv.host : cl.host;
+            enet_host_flush(h);
+            struct timespec ts = { 0, 200000 };
+            nanosleep(&ts, NULL);
+        }
+    }
+    /* let the last echoes / acks leave */
+    for (int i = 0; i < 50; ++i) {
+        if (server) { pump(&sv); enet_host_flush(sv.host); }
+        if (client) { pump(&cl); enet_host_flush(cl.host); }
+        struct timespec ts = { 0, 2000000 };
+        nanosleep(&ts, NULL);
+    }
+    Side *s = client ? &cl : &sv;
+    int ok = s->done && s->bad == 0;
+    printf("{\"role\": \"%s\", \"coder\": \"%s\", \"packets\": %u, \"received\": %u, \"mismatches\": %u, "
+           "\"payload_bytes\": %llu, \"wire_bytes_sent\": %u, \"seconds\": %.3f, \"ok\": %s}\n",
+           role, enet_rc_version ? enet_rc_version() : "reference compress.c", count, s->got, s->bad,
+           (unsigned long long) s->raw_bytes, s->host->totalSentData, now() - t0, ok ? "true" : "false");
+    fflush(stdout);
+    if (server) enet_host_destroy(sv.host);
+    if (client) enet_host_destroy(cl.host);
+    enet_deinitialize();
+    return ok ? 0 : 1;
+}
