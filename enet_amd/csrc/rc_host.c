@@ -39,6 +39,7 @@ typedef struct {
     uint8_t *h_stage;               /* pinned */
     size_t h_stage_cap;
     uint32_t last_exact;
+    uint32_t max_slots;             /* lanes with a model region (ENET_RC_SLOTS) */
 } rc_ctx;
 
 static void *ctx_alloc(size_t n) { return enet_malloc ? enet_malloc(n) : malloc(n); }
@@ -70,7 +71,7 @@ static int ws_reserve(rc_ctx *c, size_t n)
 static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 {
     uint32_t region = rc_hip_lane_region_bytes(max_len ? max_len : 4096);
-    size_t slots = n < MAX_LANE_SLOTS ? n : MAX_LANE_SLOTS;
+    size_t slots = n < c->max_slots ? n : c->max_slots;
     slots = (slots + 255) & ~(size_t) 255;
     if (slots <= c->ws.lane_slots && region <= c->ws.lane_region) return 0;
     if (slots < c->ws.lane_slots) slots = c->ws.lane_slots;
@@ -119,6 +120,9 @@ void *enet_range_coder_create(void)
         const char *a = getenv("ENET_RC_LANES");
         c->ws.lane_active = 64;
         if (a && (atoi(a) == 32 || atoi(a) == 16)) c->ws.lane_active = (uint32_t) atoi(a);
+        const char *sl = getenv("ENET_RC_SLOTS");
+        c->max_slots = MAX_LANE_SLOTS;
+        if (sl && atol(sl) >= 256 && atol(sl) <= (1l << 22)) c->max_slots = (uint32_t) atol(sl);
     }
     if (stage_reserve(c, 1u << 16) != 0) goto fail;
     return c;

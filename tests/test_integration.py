@@ -73,7 +73,7 @@ def test_gpu_coder_in_live_hosts():
     _need(LOOP_AMD)
     rc, res, err = _run(LOOP_AMD, "both", _port(), 300)
     assert rc == 0 and res["ok"], (res, err)
-    assert res["coder"].startswith("enet_amd")
+    assert res["coder"].startswith("enet_rc_amd")
     assert res["wire_bytes_sent"] < res["payload_bytes"] / 2
 
 
@@ -81,11 +81,11 @@ def test_gpu_coder_in_live_hosts():
 def test_gpu_server_reference_client():
     _need(LOOP_AMD, LOOP_REF)
     c, s = _pair(LOOP_AMD, LOOP_REF, 300)
-    assert c["ok"] and c["mismatches"] == 0 and s["coder"].startswith("enet_amd")
+    assert c["ok"] and c["mismatches"] == 0 and s["coder"].startswith("enet_rc_amd")
 
 
 @pytest.mark.gpu
 def test_reference_server_gpu_client():
     _need(LOOP_AMD, LOOP_REF)
     c, s = _pair(LOOP_REF, LOOP_AMD, 300)
-    assert c["ok"] and c["mismatches"] == 0 and c["coder"].startswith("enet_amd")
+    assert c["ok"] and c["mismatches"] == 0 and c["coder"].startswith("enet_rc_amd")
