@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-pcie", action="store_true")
+    p.add_argument("--no-crc", action="store_true", help="skip the CRC-32 kernel line")
     p.add_argument("--no-rccl", action="store_true")
     return p.parse_args()
 
@@ -180,6 +181,9 @@ def main():
         "roofline": roofline,
     }
 
+    if not args.no_crc:
+        result["crc32"] = crc32_bench(coder, din, doff, dlen, in_bytes, n, stream)
+
     if rank == 0 and world == 1 and not args.no_pcie:
         result["pcie_inclusive"] = pcie_inclusive(coder, d, o, l, args)
 
@@ -196,6 +200,28 @@ def main():
     coder.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def crc32_bench(coder, din, doff, dlen, in_bytes, n, stream):
+    """enet_crc32 of every packet of the same batch
+    (rc_crc32_batch), device-resident.  Algorithmic bytes per launch: the
+    payload + 12 B of offset/length read + 4 B written per packet."""
+    import torch
+    out = torch.empty(n, dtype=torch.int32, device=din.device)
+    for _ in range(3):
+        coder.crc32_batch(din, doff, dlen, out, stream=stream)
+    reps = 20
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        coder.crc32_batch(din, doff, dlen, out, stream=stream)
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    t = ev[0].elapsed_time(ev[1]) / reps / 1e3
+    alg = in_bytes + 16 * n
+    return {"kernel": "rc_crc32_batch", "ms": round(t * 1e3, 4), "GiBps": round(in_bytes / t / GIB, 3),
+            "roofline": {"bound": "hbm", "achieved": round(alg / t / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}}
 
 
 def pcie_inclusive(coder, d, o, l, args):

@@ -100,6 +100,38 @@ class RangeCoder:
         self._batch(self.lib.enet_rc_decompress_batch_device, inp, in_off, in_len, max_len, out, out_off,
                     out_cap, out_len, stream)
 
+    def crc32_batch(self, inp, in_off, in_len, crc_out=None, stream=None):
+        """enet_crc32 (packet.c:143-163) of every packet, on the GPU.  Returns an
+        int32 device tensor holding the reference's uint32 results (network
+        byte order, as written into ENet datagram headers)."""
+        import torch
+        for t in (inp, in_off, in_len):
+            if not (t.is_cuda and t.is_contiguous()):
+                raise ValueError("batch tensors must be contiguous device tensors")
+        assert inp.dtype == torch.uint8 and in_off.dtype == torch.int64 and in_len.dtype == torch.int32
+        n = in_len.numel()
+        if crc_out is None:
+            crc_out = torch.empty(n, dtype=torch.int32, device=inp.device)
+        assert crc_out.is_cuda and crc_out.dtype == torch.int32 and crc_out.numel() >= n
+        if stream is None:
+            stream = torch.cuda.current_stream(inp.device)
+        rc = self.lib.enet_rc_crc32_batch_device(self.ctx, inp.data_ptr(), in_off.data_ptr(), in_len.data_ptr(),
+                                                 n, crc_out.data_ptr(), C.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"enet_rc_crc32_batch_device failed: HIP error {rc}")
+        return crc_out
+
+    def crc32(self, data: bytes) -> int:
+        """One datagram through the host-pointer batch path (like enet_crc32 on one buffer)."""
+        src = C.create_string_buffer(bytes(data) + b"\0")
+        off = (C.c_uint64 * 1)(0)
+        ln = (C.c_uint32 * 1)(len(data))
+        out = (C.c_uint32 * 1)(0)
+        rc = self.lib.enet_rc_crc32_batch_host(self.ctx, C.addressof(src), off, ln, 1, out)
+        if rc != 0:
+            raise RuntimeError(f"enet_rc_crc32_batch_host failed: HIP error {rc}")
+        return int(out[0])
+
     def last_exact_count(self) -> int:
         return int(self.lib.enet_rc_last_exact_count(self.ctx))
 

@@ -50,6 +50,12 @@ def _load() -> C.CDLL:
         f = getattr(lib, name)
         f.restype = C.c_int
         f.argtypes = args
+    lib.enet_rc_crc32_batch_device.restype = C.c_int
+    lib.enet_rc_crc32_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
+    lib.enet_rc_crc32_batch_host.restype = C.c_int
+    lib.enet_rc_crc32_batch_host.argtypes = [vp, vp, vp, vp, sz, vp]
+    lib.enet_rc_crc32.restype = u32
+    lib.enet_rc_crc32.argtypes = [C.POINTER(ENetBuffer), sz]
     lib.enet_rc_last_exact_count.restype = u32
     lib.enet_rc_last_exact_count.argtypes = [vp]
     lib.enet_rc_version.restype = C.c_char_p

@@ -56,6 +56,14 @@ int rc_hip_decompress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *s
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
 uint32_t rc_hip_lane_region_bytes(uint32_t max_len);
 
+/* CRC-32 of each packet (rc_crc32.hip): crc_out[i] = enet_crc32 (packet.c:143-163)
+ * of in[in_off[i] .. +in_len[i]).  tables: rc_hip_crc32_table_words() words
+ * built by rc_hip_crc32_build_tables, in device memory. */
+int rc_hip_crc32(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, uint32_t n,
+                 uint32_t *crc_out, const uint32_t *tables, void *stream);
+uint32_t rc_hip_crc32_table_words(void);
+void rc_hip_crc32_build_tables(uint32_t *t);
+
 /* Kernel introspection for bench/profiling. */
 const char *rc_hip_fast_kernel_name(int decompress);
 uint32_t    rc_hip_lds_bytes(uint32_t max_len);

@@ -1,0 +1,181 @@
+// rc_crc32.hip -- batched ENet datagram checksums on MI355X (gfx950).
+//
+// Same result as enet_crc32 (packet.c:143-163) over one buffer per packet:
+// reflected CRC-32, polynomial 0xEDB88320, register preset 0xFFFFFFFF, final
+// complement, returned in network byte order (ENET_HOST_TO_NET_32).
+// protocol.c:1709-1718 (send) and :1075-1091 (receive) are the call sites.
+//
+// One wavefront per packet, HBM-bound:
+//   * The packet is cut into 1 KiB blocks aligned to its END (a raw CRC with a
+//     zero register ignores leading zero bytes, so the first block is padded
+//     at the front for free).  Each lane owns 16 bytes of a block: one aligned
+//     16-B load per lane, wave-uniform funnel shift for the packet's alignment.
+//   * A lane's raw CRC of its 16 bytes is a slice-by-16 lookup (16 independent
+//     LDS reads, tables T_k[b] = CRC of b followed by k zero bytes).
+//   * Lanes are combined in a 6-level xor tree: crc(A||B) = shift(crc(A), |B|)
+//     ^ crc(B), where shift(v, n) -- n zero bytes through the register -- is
+//     linear in v, i.e. four 256-entry lookups per level (n = 16 << level).
+//     Blocks chain with the n = 1024 tables.
+//   * The 0xFFFFFFFF preset is folded in by complementing the first four
+//     message bytes (identical for packets of >= 4 bytes); shorter packets add
+//     shift(0xFFFFFFFF, L) directly.
+// Tables (44 KiB) are built on the host once per context and staged into LDS
+// by each workgroup of a persistent grid.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rc_abi_internal.h"
+
+namespace {
+
+constexpr uint32_t kSlice = 16;                 // slice-by-16 tables
+constexpr uint32_t kLevels = 7;                 // shift tables for 16 << 0..6 bytes
+constexpr uint32_t kTableWords = (kSlice + 4 * kLevels) * 256;
+constexpr uint32_t kBlock = 1024;               // bytes per wave pass (64 lanes x 16 B)
+constexpr uint32_t kWavesPerGroup = 4;
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t k) { return (w >> (8 * k)) & 0xFFu; }
+
+// 0xFF in every byte whose index (0..3 within dword d of a 16-B chunk) is >= k
+__device__ __forceinline__ uint32_t bytes_from(int k, int d)
+{
+    const int kd = k - 4 * d;
+    if (kd <= 0) return 0xFFFFFFFFu;
+    if (kd >= 4) return 0u;
+    return 0xFFFFFFFFu << (8 * kd);
+}
+
+__device__ __forceinline__ uint32_t shift_by(const uint32_t* s, uint32_t v)
+{
+    return s[byte_of(v, 0)] ^ s[256 + byte_of(v, 1)] ^ s[512 + byte_of(v, 2)] ^ s[768 + byte_of(v, 3)];
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh)
+{
+    // bytes sh.. of the 8-byte little-endian pair (lo, hi), sh in 0..3
+    return sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(64 * kWavesPerGroup)
+void rc_crc32_batch(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                    const uint32_t* __restrict__ in_len, uint32_t n, uint32_t* __restrict__ crc_out,
+                    const uint32_t* __restrict__ tables)
+{
+    __shared__ uint32_t tab[kTableWords];
+    for (uint32_t i = threadIdx.x; i < kTableWords / 4; i += blockDim.x)
+        reinterpret_cast<uint4*>(tab)[i] = reinterpret_cast<const uint4*>(tables)[i];
+    __syncthreads();
+    const uint32_t* sh = tab + kSlice * 256;    // shift tables, level-major
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerGroup + (threadIdx.x >> 6));
+    const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+    const uint64_t base = reinterpret_cast<uint64_t>(in);
+    for (uint32_t p = wave; p < n; p += nwaves) {
+        // everything per packet is wave-uniform; addresses are absolute
+        const uint64_t start = base + in_off[p];
+        const uint32_t len = in_len[p];
+        const uint64_t end = start + len;
+        const uint32_t nb = (len + kBlock - 1) / kBlock;
+        const uint32_t mis = static_cast<uint32_t>(end & 15);
+        const uint32_t dq = mis >> 2, bs = mis & 3;
+        uint32_t run = 0;
+        for (uint32_t b = 0; b < nb; ++b) {
+            // this lane's 16 bytes: [c, c + 16) (may start before the packet in block 0)
+            const uint64_t c = end - static_cast<uint64_t>(kBlock) * (nb - b) + 16 * lane;
+            const uint64_t a = c - mis;                                 // aligned granule holding byte c
+            uint4 w0 = make_uint4(0, 0, 0, 0), w1;
+            if (a + 16 > start) w0 = *reinterpret_cast<const uint4*>(a);   // granule overlaps the packet
+            // next granule: the neighbour's; lane 63 loads its own (only when misaligned)
+            w1.x = __shfl_down(w0.x, 1); w1.y = __shfl_down(w0.y, 1);
+            w1.z = __shfl_down(w0.z, 1); w1.w = __shfl_down(w0.w, 1);
+            if (lane == 63 && mis) w1 = *reinterpret_cast<const uint4*>(a + 16);
+            // funnel-shift the 32 bytes (w0, w1) right by mis -> 16 bytes d[0..3]
+            const uint32_t q[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+            uint32_t d[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t lo = dq == 0 ? q[k] : dq == 1 ? q[k + 1] : dq == 2 ? q[k + 2] : q[k + 3];
+                const uint32_t hi = dq == 0 ? q[k + 1] : dq == 1 ? q[k + 2] : dq == 2 ? q[k + 3] : q[k + 4];
+                d[k] = funnel(lo, hi, bs);
+            }
+            // zero the bytes before the packet; complement its first four (register preset)
+            const int lead = static_cast<int>(static_cast<int64_t>(start - c));   // packet byte 0 in chunk
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t keep = bytes_from(lead, k);
+                d[k] &= keep;
+                if (len >= 4) d[k] ^= keep & ~bytes_from(lead + 4, k);
+            }
+            // raw CRC of the 16 bytes (slice-by-16)
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v ^= tab[(15 - (4 * k + j)) * 256 + byte_of(d[k], j)];
+            // xor tree over the 64 lanes (lane order = message order)
+#pragma unroll
+            for (uint32_t lv = 0; lv < 6; ++lv) {
+                const uint32_t m = 1u << lv;
+                const uint32_t s = shift_by(sh + lv * 1024, v);
+                const uint32_t os = __shfl_xor(s, m), ov = __shfl_xor(v, m);
+                v = (lane & m) ? (os ^ v) : (s ^ ov);
+            }
+            run = shift_by(sh + 6 * 1024, run) ^ v;
+        }
+        if (lane == 0) {
+            uint32_t crc = run;
+            if (len < 4) {                       // preset through len bytes, zero data
+                uint32_t r = 0xFFFFFFFFu;
+                for (uint32_t k = 0; k < len; ++k) r = (r >> 8) ^ tab[r & 0xFF];
+                crc ^= r;
+            }
+            crc_out[p] = __builtin_bswap32(~crc);
+        }
+    }
+}
+
+extern "C" uint32_t rc_hip_crc32_table_words(void) { return kTableWords; }
+
+// Host-side table build (called once per context by rc_host.c).
+extern "C" void rc_hip_crc32_build_tables(uint32_t* t)
+{
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t c = b;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+        t[b] = c;
+    }
+    for (uint32_t s = 1; s < kSlice; ++s)
+        for (uint32_t b = 0; b < 256; ++b) {
+            const uint32_t prev = t[(s - 1) * 256 + b];
+            t[s * 256 + b] = (prev >> 8) ^ t[prev & 0xFF];
+        }
+    // shift(x, n): n zero bytes through a raw register holding x
+    auto shift = [&](uint32_t x, uint32_t nbytes) {
+        for (uint32_t k = 0; k < nbytes; ++k) x = (x >> 8) ^ t[x & 0xFF];
+        return x;
+    };
+    uint32_t* sh = t + kSlice * 256;
+    for (uint32_t lv = 0; lv < kLevels; ++lv)
+        for (uint32_t j = 0; j < 4; ++j)
+            for (uint32_t b = 0; b < 256; ++b)
+                sh[lv * 1024 + j * 256 + b] = shift(b << (8 * j), 16u << lv);
+}
+
+extern "C" int rc_hip_crc32(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t n,
+                            uint32_t* crc_out, const uint32_t* tables, void* stream)
+{
+    if (n == 0) return 0;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    uint32_t groups = (n + kWavesPerGroup - 1) / kWavesPerGroup;
+    const uint32_t cap = static_cast<uint32_t>(cus) * 3;        // 44 KiB LDS -> 3 groups per CU
+    if (groups > cap) groups = cap;
+    hipLaunchKernelGGL(rc_crc32_batch, dim3(groups), dim3(64 * kWavesPerGroup), 0,
+                       static_cast<hipStream_t>(stream), in, in_off, in_len, n, crc_out, tables);
+    return static_cast<int>(hipGetLastError());
+}

@@ -17,6 +17,7 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 
 #include "enet_rc_amd.h"
 #include "rc_abi_internal.h"
@@ -40,6 +41,7 @@ typedef struct {
     size_t h_stage_cap;
     uint32_t last_exact;
     uint32_t max_slots;             /* lanes with a model region (ENET_RC_SLOTS) */
+    uint32_t *crc_tables;           /* device: slice-by-16 + shift tables (rc_crc32.hip) */
 } rc_ctx;
 
 static void *ctx_alloc(size_t n) { return enet_malloc ? enet_malloc(n) : malloc(n); }
@@ -115,6 +117,16 @@ void *enet_range_coder_create(void)
     if (hipMalloc(&c->ws.exact_pool, (size_t) EXACT_SLOTS * RC_EXACT_POOL_BYTES) != hipSuccess) goto fail;
     if (ws_reserve(c, 1024) != 0) goto fail;
     {
+        const uint32_t words = rc_hip_crc32_table_words();
+        uint32_t *t = (uint32_t *) malloc(words * sizeof(uint32_t));
+        if (!t) goto fail;
+        rc_hip_crc32_build_tables(t);
+        hipError_t e = hipMalloc((void **) &c->crc_tables, words * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemcpy(c->crc_tables, t, words * sizeof(uint32_t), hipMemcpyHostToDevice);
+        free(t);
+        if (e != hipSuccess) goto fail;
+    }
+    {
         const char *k = getenv("ENET_RC_KERNEL");
         c->ws.kernel = (k && strcmp(k, "wave") == 0) ? RC_KERNEL_WAVE : RC_KERNEL_LANE;
         const char *a = getenv("ENET_RC_LANES");
@@ -142,6 +154,7 @@ void enet_range_coder_destroy(void *context)
     if (c->ws.bins) hipFree(c->ws.bins);
     if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
+    if (c->crc_tables) hipFree(c->crc_tables);
     if (c->d_stage) hipFree(c->d_stage);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -250,6 +263,83 @@ int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64
                                   const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
     return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+}
+
+/* ------------------------------------------------------------------ CRC-32 */
+
+int enet_rc_crc32_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                               const uint32_t *in_len, size_t n, uint32_t *crc_out, void *stream)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c || n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    return rc_hip_crc32(in, in_off, in_len, (uint32_t) n, crc_out, c->crc_tables, stream);
+}
+
+int enet_rc_crc32_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                             const uint32_t *in_len, size_t n, uint32_t *crc_out)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c || n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    uint64_t in_bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t e = in_off[i] + in_len[i];
+        if (e > in_bytes) in_bytes = e;
+    }
+    size_t a_ioff = (in_bytes + 15) & ~(size_t) 15;
+    size_t a_ilen = a_ioff + n * 8;
+    size_t a_crc = (a_ilen + n * 4 + 15) & ~(size_t) 15;
+    size_t total = a_crc + n * 4;
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    if (stage_reserve(c, total) != 0) return (int) hipErrorOutOfMemory;
+    uint8_t *h = c->h_stage, *d = c->d_stage;
+    memcpy(h, in, in_bytes);
+    memcpy(h + a_ioff, in_off, n * 8);
+    memcpy(h + a_ilen, in_len, n * 4);
+    hipError_t err = hipMemcpyAsync(d, h, a_crc, hipMemcpyHostToDevice, c->stream);
+    if (err != hipSuccess) return (int) err;
+    int rc = rc_hip_crc32(d, (const uint64_t *) (d + a_ioff), (const uint32_t *) (d + a_ilen), (uint32_t) n,
+                          (uint32_t *) (d + a_crc), c->crc_tables, (void *) c->stream);
+    if (rc != 0) return rc;
+    err = hipMemcpyAsync(h + a_crc, d + a_crc, n * 4, hipMemcpyDeviceToHost, c->stream);
+    if (err != hipSuccess) return (int) err;
+    err = hipStreamSynchronize(c->stream);
+    if (err != hipSuccess) return (int) err;
+    memcpy(crc_out, h + a_crc, n * 4);
+    return 0;
+}
+
+/* ENetChecksumCallback (enet.h:338) with no context argument: a process-wide
+ * context, created on first use.  Gather lists are checksummed as one stream,
+ * like enet_crc32's loop over buffers (packet.c:148-160). */
+static pthread_once_t crc_once = PTHREAD_ONCE_INIT;
+static void *crc_ctx;
+static pthread_mutex_t crc_lock = PTHREAD_MUTEX_INITIALIZER;
+static void crc_ctx_init(void) { crc_ctx = enet_range_coder_create(); }
+
+enet_uint32 enet_rc_crc32(const ENetBuffer *buffers, size_t bufferCount)
+{
+    pthread_once(&crc_once, crc_ctx_init);
+    size_t total = 0;
+    for (size_t i = 0; i < bufferCount; ++i) total += buffers[i].dataLength;
+    if (!crc_ctx || total > 0xFFFFFFFFu) abort();          /* no silent CPU fallback */
+    uint8_t *flat = (uint8_t *) malloc(total ? total : 1);
+    if (!flat) abort();
+    size_t pos = 0;
+    for (size_t i = 0; i < bufferCount; ++i) {
+        if (buffers[i].dataLength) memcpy(flat + pos, buffers[i].data, buffers[i].dataLength);
+        pos += buffers[i].dataLength;
+    }
+    uint64_t off = 0;
+    uint32_t len = (uint32_t) total, crc = 0;
+    pthread_mutex_lock(&crc_lock);
+    int rc = enet_rc_crc32_batch_host(crc_ctx, flat, &off, &len, 1, &crc);
+    pthread_mutex_unlock(&crc_lock);
+    free(flat);
+    if (rc != 0) abort();
+    return crc;
 }
 
 /* --------------------------------------------------------- per-datagram ABI */

@@ -97,6 +97,21 @@ int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64
                                   const uint32_t *in_len, size_t n, uint8_t *out,
                                   const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
 
+/* ==================================================================== CRC-32
+ * crc_out[i] = enet_crc32 (packet.c:143-163) of the single buffer
+ * in[in_off[i] .. +in_len[i]): CRC-32/IEEE, returned in network byte order
+ * exactly like the reference (ENET_HOST_TO_NET_32 of the complement), i.e.
+ * the value protocol.c:1709-1718 writes into the datagram header and
+ * protocol.c:1075-1091 compares.  Device / host pointer variants as above. */
+int enet_rc_crc32_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                               const uint32_t *in_len, size_t n, uint32_t *crc_out, void *stream);
+int enet_rc_crc32_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                             const uint32_t *in_len, size_t n, uint32_t *crc_out);
+/* Same signature as enet_crc32 / ENetChecksumCallback (enet.h:338, enet.h:564):
+ * host->checksum = enet_rc_crc32.  Uses a process-wide GPU context; aborts if
+ * no GPU is usable (there is no CPU fallback). */
+enet_uint32 enet_rc_crc32(const ENetBuffer *buffers, size_t bufferCount);
+
 /* ============================================================ introspection */
 /* Number of packets of the last batch that took the exact (binary-tree) path. */
 uint32_t enet_rc_last_exact_count(void *context);

@@ -182,3 +182,27 @@ def cpu_roundtrip(data, off, ln, threads: int, kind: str = "reference"):
         raise RuntimeError(f"cpubench_roundtrip failed rc={rc}")
     return dict(t_compress=tc.value, t_decompress=td.value,
                 compressed_bytes=cb.value, mismatches=mm.value)
+
+
+def crc32_batch(data: np.ndarray, off: np.ndarray, ln: np.ndarray, kind: str = "port") -> np.ndarray:
+    """enet_crc32 (packet.c:143-163) of every packet: the port's or the
+    reference's own function (exported by libenet_ref.so)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(ln, dtype=np.uint32)
+    out = np.zeros(len(ln), dtype=np.uint32)
+    if kind == "port":
+        lib = _load(PORT_SO)
+        lib.or_crc32_batch.restype = None
+        lib.or_crc32_batch(_ptr(data), _ptr(off), _ptr(ln), C.c_size_t(len(ln)), _ptr(out))
+        return out
+    lib = _load(REF_SO)
+    lib.enet_crc32.restype = C.c_uint32
+    lib.enet_crc32.argtypes = [C.c_void_p, C.c_size_t]
+    base = data.ctypes.data
+    buf = (_Buf * 1)()
+    for i in range(len(ln)):
+        buf[0].data = base + int(off[i])
+        buf[0].dataLength = int(ln[i])
+        out[i] = lib.enet_crc32(buf, 1)
+    return out

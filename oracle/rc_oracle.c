@@ -492,3 +492,41 @@ uint64_t or_fnv1a64_packets(const uint8_t *buf, const uint64_t *off, const uint3
     }
     return h;
 }
+
+/* enet_crc32 (packet.c:143-163): reflected CRC-32, polynomial 0xEDB88320,
+ * preset 0xFFFFFFFF, one table lookup per byte across the buffer list, result
+ * complemented and put in network byte order (ENET_HOST_TO_NET_32). The table
+ * is generated here from the polynomial rather than spelled out. */
+static uint32_t crc_table[256];
+static int crc_table_ready;
+
+static void crc_init(void)
+{
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t c = b;
+        for (int k = 0; k < 8; ++k) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        crc_table[b] = c;
+    }
+    crc_table_ready = 1;
+}
+
+uint32_t or_crc32(const OrBuffer *bufs, size_t nbufs)
+{
+    if (!crc_table_ready) crc_init();
+    uint32_t crc = 0xFFFFFFFFu;
+    for (size_t i = 0; i < nbufs; ++i) {
+        const uint8_t *p = (const uint8_t *) bufs[i].data;
+        for (size_t k = 0; k < bufs[i].dataLength; ++k) crc = (crc >> 8) ^ crc_table[(crc ^ p[k]) & 0xFFu];
+    }
+    crc = ~crc;
+    return ((crc & 0xFFu) << 24) | ((crc & 0xFF00u) << 8) | ((crc >> 8) & 0xFF00u) | (crc >> 24);
+}
+
+void or_crc32_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, size_t n,
+                    uint32_t *crc_out)
+{
+    for (size_t i = 0; i < n; ++i) {
+        OrBuffer b = { (void *) (in + in_off[i]), in_len[i] };
+        crc_out[i] = or_crc32(&b, 1);
+    }
+}

@@ -42,6 +42,9 @@ void or_decompress_batch(const uint8_t *in, const uint64_t *in_off, const uint32
                          const uint32_t *out_cap, uint32_t *out_len);
 
 /* Batch digest, SURVEY.md §8c. */
+uint32_t or_crc32(const OrBuffer *bufs, size_t nbufs);      /* packet.c:143-163 */
+void or_crc32_batch(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len, size_t n,
+                    uint32_t *crc_out);
 uint64_t or_fnv1a64_packets(const uint8_t *buf, const uint64_t *off, const uint32_t *len, size_t n);
 
 #ifdef __cplusplus

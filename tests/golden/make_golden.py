@@ -17,6 +17,10 @@ Files:
   gather_cases.npz      multi-buffer compress (incl. empty buffers)        -> ret, bytes
   decompress_cases.npz  decompress of valid / truncated / bit-flipped / garbage streams
   digests.json          C1 / C2 / C3 batch digests (SURVEY.md §8c format)
+  crc_cases.npz         enet_crc32 (packet.c:143-163) of single buffers, from the
+                        reference library's exported enet_crc32
+
+`python tests/golden/make_golden.py crc` regenerates crc_cases.npz only.
 """
 from __future__ import annotations
 
@@ -30,7 +34,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 from enet_amd import synth  # noqa: E402
-from oracle.pyoracle import Coder, compress_batch, fnv_digest, have_reference  # noqa: E402
+from oracle.pyoracle import Coder, compress_batch, crc32_batch, fnv_digest, have_reference  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 
@@ -52,7 +56,31 @@ def _pack_cases(cases, fields):
     return arrs
 
 
+def make_crc():
+    """CRC-32 fixtures: every length 0..80, then assorted sizes to 4096 B, plus
+    the standard check string; expected values from the reference itself."""
+    inputs = [b"123456789", b"", b"\0" * 1200, b"\xff" * 4096]
+    for n in range(0, 81):
+        inputs.append(synth.random_bytes(n, 500 + n).tobytes())
+    for k, n in enumerate((127, 128, 129, 255, 256, 1000, 1023, 1024, 1025, 1199, 1200, 1392,
+                           2047, 2048, 2049, 3000, 4095, 4096)):
+        inputs.append(synth.random_bytes(n, 900 + k).tobytes())
+    blob = np.frombuffer(b"".join(inputs), dtype=np.uint8)
+    ln = np.array([len(x) for x in inputs], dtype=np.uint32)
+    off = np.concatenate([[0], np.cumsum(ln[:-1], dtype=np.uint64)]).astype(np.uint64)
+    crc = crc32_batch(blob, off, ln, kind="reference")
+    np.savez_compressed(os.path.join(OUT, "crc_cases.npz"), inputs=blob, in_len=ln,
+                        crc=crc.astype(np.int64))
+    print(f"crc {len(inputs)}  check('123456789') = {int(crc[0]):#010x}")
+
+
 def main():
+    if not have_reference():
+        sys.exit("oracle/_ref/libenet_ref.so missing: run `make -C oracle` first")
+    if sys.argv[1:] == ["crc"]:
+        make_crc()
+        return
+    make_crc()
     if not have_reference():
         sys.exit("oracle/_ref/libenet_ref.so missing: run `make -C oracle` first")
     ref = Coder("reference")

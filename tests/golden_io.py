@@ -45,3 +45,11 @@ def gather_cases():
 def digests():
     with open(os.path.join(GOLDEN, "digests.json")) as f:
         return json.load(f)
+
+
+def crc_cases():
+    """[(input bytes, expected enet_crc32 value)] from crc_cases.npz."""
+    z = np.load(os.path.join(GOLDEN, "crc_cases.npz"), allow_pickle=False)
+    ins, inl, crc = z["inputs"], z["in_len"], z["crc"]
+    io = np.concatenate([[0], np.cumsum(inl.astype(np.int64))])
+    return [(ins[io[i]:io[i + 1]].tobytes(), int(crc[i])) for i in range(len(inl))]
