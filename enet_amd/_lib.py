@@ -16,7 +16,8 @@ except ImportError:  # the C ABI itself does not need torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "lib", "libenet_rc_amd.so")
+# ENET_RC_LIB: diagnostic override (e.g. the -DRC_PROFILE build used by tools/lane_prof.py)
+LIB_PATH = os.environ.get("ENET_RC_LIB") or os.path.join(HERE, "lib", "libenet_rc_amd.so")
 HEADER = os.path.join(ROOT, "include", "enet_rc_amd.h")
 
 

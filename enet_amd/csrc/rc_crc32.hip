@@ -51,6 +51,15 @@ __device__ __forceinline__ uint32_t shift_by(const uint32_t* s, uint32_t v)
     return s[byte_of(v, 0)] ^ s[256 + byte_of(v, 1)] ^ s[512 + byte_of(v, 2)] ^ s[768 + byte_of(v, 3)];
 }
 
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+// 16-B load through a global-address-space pointer (an integer address would
+// otherwise become a flat load)
+__device__ __forceinline__ uint4 gload16(uint64_t a)
+{
+    const v4u32 v = *((const __attribute__((address_space(1))) v4u32*) a);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh)
 {
     // bytes sh.. of the 8-byte little-endian pair (lo, hi), sh in 0..3
@@ -88,11 +97,11 @@ void rc_crc32_batch(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             const uint64_t c = end - static_cast<uint64_t>(kBlock) * (nb - b) + 16 * lane;
             const uint64_t a = c - mis;                                 // aligned granule holding byte c
             uint4 w0 = make_uint4(0, 0, 0, 0), w1;
-            if (a + 16 > start) w0 = *reinterpret_cast<const uint4*>(a);   // granule overlaps the packet
+            if (a + 16 > start) w0 = gload16(a);   // granule overlaps the packet
             // next granule: the neighbour's; lane 63 loads its own (only when misaligned)
             w1.x = __shfl_down(w0.x, 1); w1.y = __shfl_down(w0.y, 1);
             w1.z = __shfl_down(w0.z, 1); w1.w = __shfl_down(w0.w, 1);
-            if (lane == 63 && mis) w1 = *reinterpret_cast<const uint4*>(a + 16);
+            if (lane == 63 && mis) w1 = gload16(a + 16);
             // funnel-shift the 32 bytes (w0, w1) right by mis -> 16 bytes d[0..3]
             const uint32_t q[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
             uint32_t d[4];

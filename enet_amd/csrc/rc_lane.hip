@@ -42,8 +42,31 @@
 #include <stdint.h>
 
 #include "rc_abi_internal.h"
+#include "rc_udiv.h"
 
 #define DEV __device__ __forceinline__
+
+// Diagnostic build only (-DRC_PROFILE, tools/lane_prof.py): per-phase cycle
+// stamps accumulated per wave and summed into g_prof.  The product build
+// compiles every PROF_* to nothing.
+#ifdef RC_PROFILE
+__device__ unsigned long long g_prof[64];
+__device__ __forceinline__ unsigned long long prof_now()
+{
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define PROF_DECL unsigned long long prof_t = prof_now(), prof_acc[12] = {0};
+#define PROF(k) { const unsigned long long t_ = prof_now(); prof_acc[k] += t_ - prof_t; prof_t = t_; }
+#define PROF_FLUSH(base) { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 12; ++k_) atomicAdd(&g_prof[(base) + k_], prof_acc[k_]); }
+#else
+#define PROF_DECL
+#define PROF(k)
+#define PROF_FLUSH(base)
+#endif
 
 namespace {
 
@@ -109,8 +132,9 @@ DEV void root_add(uint8_t* r, uint32_t v, uint32_t cnt)
     }
 }
 
-// first symbol whose interval [v + C(<v), v + 1 + C(<=v)) holds code; code < 256 + sum
-DEV uint32_t root_search(const uint8_t* r, uint32_t code)
+// first symbol whose interval [v + C(<v), v + 1 + C(<=v)) holds code
+// (code < 256 + sum); also returns that interval's start (under) and count[v]
+DEV uint32_t root_search(const uint8_t* r, uint32_t code, uint32_t& under, uint32_t& cnt)
 {
     const uint4 c0 = reinterpret_cast<const uint4*>(r + 256)[0];
     const uint4 c1 = reinterpret_cast<const uint4*>(r + 256)[1];
@@ -124,15 +148,21 @@ DEV uint32_t root_search(const uint8_t* r, uint32_t code)
         prev = below ? ct : prev;
     }
     const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
-    uint32_t run = 16 * g + prev, j = 15;
+    uint32_t run = 16 * g + prev, j = 15, at = run, c = 0;
     bool found = false;
 #pragma unroll
     for (uint32_t t = 0; t < 16; ++t) {
-        run += 1 + ((pick4(t >> 2, q) >> (8 * (t & 3))) & 0xFF);
-        const bool hit = !found && code < run;
+        const uint32_t ct = (pick4(t >> 2, q) >> (8 * (t & 3))) & 0xFF;
+        const uint32_t nrun = run + 1 + ct;
+        const bool hit = !found && code < nrun;
         j = hit ? t : j;
+        at = hit ? run : at;
+        c = hit ? ct : c;
         found = found || hit;
+        run = nrun;
     }
+    under = at;
+    cnt = c;
     return 16 * g + j;
 }
 
@@ -471,6 +501,23 @@ DEV void region_reset(uint8_t* reg, uint8_t* root)
 // one aligned dwordx4 load / store per 16 bytes; packet edges fall back to
 // byte accesses so nothing outside [p, p+len) is read or written.
 
+// Byte-stream addresses are integers (alignment arithmetic); accesses through
+// them must name the global address space, otherwise they become flat_*
+// operations, which complete out of order and force vmcnt(0) waits -- a full
+// drain of every outstanding load and store, including the prefetches.
+#ifndef RC_LANE_HOST_TEST
+#define GPTR(T, a) ((__attribute__((address_space(1))) T*) (a))
+#define GPTRC(T, a) ((const __attribute__((address_space(1))) T*) (a))
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+DEV uint4 gload16(uintptr_t a) { const v4u32 v = *GPTRC(v4u32, a); return make_uint4(v.x, v.y, v.z, v.w); }
+DEV void gstore16(uintptr_t a, const uint4& w) { v4u32 v = {w.x, w.y, w.z, w.w}; *GPTR(v4u32, a) = v; }
+#else
+#define GPTR(T, a) ((T*) (a))
+#define GPTRC(T, a) ((const T*) (a))
+DEV uint4 gload16(uintptr_t a) { return *GPTRC(uint4, a); }
+DEV void gstore16(uintptr_t a, const uint4& w) { *GPTR(uint4, a) = w; }
+#endif
+
 DEV uint32_t win_get(const uint4& w, uint32_t i) { return (pick4(i >> 2, w) >> (8 * (i & 3))) & 0xFF; }
 
 DEV void win_set(uint4& w, uint32_t i, uint32_t b)
@@ -486,21 +533,23 @@ DEV uint4 chunk_load(const uint8_t* lo, const uint8_t* hi, uintptr_t c, bool en)
 {
     const bool full = c >= reinterpret_cast<uintptr_t>(lo) && c + 16 <= reinterpret_cast<uintptr_t>(hi);
     uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    if (en && full) w = *reinterpret_cast<const uint4*>(c);
+    if (en && full) w = gload16(c);
     if (any_lane(en && !full)) {
         if (en && !full) {
             for (uint32_t t = 0; t < 16; ++t) {
                 const uintptr_t a = c + t;
                 if (a >= reinterpret_cast<uintptr_t>(lo) && a < reinterpret_cast<uintptr_t>(hi))
-                    win_set(w, t, *reinterpret_cast<const uint8_t*>(a));
+                    win_set(w, t, *GPTRC(uint8_t, a));
             }
         }
     }
     return w;
 }
 
-// sequential reader of [p, p+len); bytes past the end read as 0 (compress.c:366-367)
-struct InWin { const uint8_t* p; uint32_t len, pos; uint4 cur, nxt; };
+// sequential reader of [p, p+len); bytes past the end read as 0 (compress.c:366-367).
+// Three 16-B chunks in flight: the chunk loaded when the reader advances is
+// first read 16 bytes later, so no step waits on it.
+struct InWin { const uint8_t* p; uint32_t len, pos; uint4 cur, nxt, fut; };
 
 DEV void inwin_init(InWin& s, const uint8_t* p, uint32_t len)
 {
@@ -508,6 +557,10 @@ DEV void inwin_init(InWin& s, const uint8_t* p, uint32_t len)
     const uintptr_t c = reinterpret_cast<uintptr_t>(p) & ~static_cast<uintptr_t>(15);
     s.cur = chunk_load(p, p + len, c, true);
     s.nxt = chunk_load(p, p + len, c + 16, true);
+    s.fut = chunk_load(p, p + len, c + 32, true);
+    // settle these before the step loop: a load still pending at the loop
+    // header makes the compiler wait for vmcnt(0) at the top of every step
+    __builtin_amdgcn_s_waitcnt(0);   // (the builtin, which the waitcnt pass understands)
 }
 
 // next byte where `en` (0 past the end)
@@ -518,13 +571,21 @@ DEV uint32_t inwin_take(InWin& s, bool en)
     const uint32_t b = live ? win_get(s.cur, a & 15) : 0u;
     s.pos += live ? 1u : 0u;
     const bool adv = live && (a & 15) == 15;
-    if (any_lane(adv)) {                  // advance; prefetch the chunk after next
-        const uint4 n = chunk_load(s.p, s.p + s.len, (a & ~static_cast<uintptr_t>(15)) + 32, adv);
+    if (any_lane(adv)) {                  // advance; fetch the chunk three ahead
         // component-wise: a select of whole vectors is lowered through scratch
         s.cur.x = adv ? s.nxt.x : s.cur.x; s.cur.y = adv ? s.nxt.y : s.cur.y;
         s.cur.z = adv ? s.nxt.z : s.cur.z; s.cur.w = adv ? s.nxt.w : s.cur.w;
-        s.nxt.x = adv ? n.x : s.nxt.x; s.nxt.y = adv ? n.y : s.nxt.y;
-        s.nxt.z = adv ? n.z : s.nxt.z; s.nxt.w = adv ? n.w : s.nxt.w;
+        s.nxt.x = adv ? s.fut.x : s.nxt.x; s.nxt.y = adv ? s.fut.y : s.nxt.y;
+        s.nxt.z = adv ? s.fut.z : s.nxt.z; s.nxt.w = adv ? s.fut.w : s.nxt.w;
+        // the load lands in `fut` directly; the rest of the step does not
+        // read it, so only this (one-in-16) step waits for it
+        const uintptr_t c = (a & ~static_cast<uintptr_t>(15)) + 48;
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(s.p), hi = lo + s.len;
+        const bool full = c >= lo && c + 16 <= hi;
+        if (adv && full) s.fut = gload16(c);
+        if (any_lane(adv && !full)) {
+            if (adv && !full) s.fut = chunk_load(s.p, s.p + s.len, c, true);
+        }
     }
     return b;
 }
@@ -536,7 +597,7 @@ DEV void outwin_edge(uint8_t* p, uint32_t n, uintptr_t c, const uint4& w)
     for (uint32_t t = 0; t < 16; ++t) {
         const uintptr_t a = c + t;
         if (a >= reinterpret_cast<uintptr_t>(p) && a < reinterpret_cast<uintptr_t>(p) + n)
-            *reinterpret_cast<uint8_t*>(a) = static_cast<uint8_t>(win_get(w, t));
+            *GPTR(uint8_t, a) = static_cast<uint8_t>(win_get(w, t));
     }
 }
 
@@ -553,7 +614,7 @@ DEV void outwin_put(OutWin& o, uint32_t byte, bool en)
     if (any_lane(flush)) {
         const uintptr_t c = a & ~static_cast<uintptr_t>(15);
         const bool whole = c >= reinterpret_cast<uintptr_t>(o.p);
-        if (flush && whole) *reinterpret_cast<uint4*>(c) = o.w;
+        if (flush && whole) gstore16(c, o.w);
         if (any_lane(flush && !whole)) {
             if (flush && !whole) outwin_edge(o.p, o.n, c, o.w);
         }
@@ -568,13 +629,14 @@ DEV void outwin_finish(OutWin& o, bool en)
 
 // ------------------------------------------------------------- range coder
 
+
 // compress.c:121-137 where `en`; clears `ok` when the output is full (the
 // whole compress call then returns 0, compress.c:116-117)
 DEV void enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total,
                   OutWin& o, bool en, bool& ok)
 {
     en = en && ok;
-    const uint32_t r = range / (en ? total : 1u);
+    const uint32_t r = udiv(range, en ? total : 1u);
     low = en ? low + under * r : low;
     range = en ? r * count : range;
     bool more = en;
@@ -596,9 +658,9 @@ DEV void enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count
 // compress.c:352 (truncated to u16 at :545/:575); divides range by total where `en`
 DEV uint32_t dec_read(uint32_t& range, uint32_t low, uint32_t code, uint32_t total, bool en)
 {
-    const uint32_t r = range / (en ? total : 1u);
+    const uint32_t r = udiv(range, en ? total : 1u);
     range = en ? r : range;
-    return ((code - low) / (en ? r : 1u)) & 0xFFFF;
+    return udiv(code - low, en ? r : 1u) & 0xFFFF;
 }
 
 // compress.c:354-371 where `en`
@@ -660,20 +722,27 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     o2_fresh(0, r2);
     rec_clear(r1);
 
+    PROF_DECL
     for (uint32_t i = 0; i < len; ++i) {
+#ifdef RC_PROFILE_DRAIN
+        __builtin_amdgcn_s_waitcnt(0);       // diagnostic: charge outstanding memory to slot 9
+        PROF(9)
+#endif
         const uint32_t v = inwin_take(in, true);
         Rec<kO1Inl> n1;
         o1_load(reg, v, n1);                                         // next step's order-1 record
         Rec<kO2Inl> n2;
-        o2_fresh(0, n2);
         const bool en2 = order >= 2;
+        PROF(0)
 
         // order 2, compress.c:286-316
         const uint32_t esc2 = r2.esc;
         const Hit h2 = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, en2);
         const bool done2 = en2 && h2.found;
+        PROF(1)
         enc_code(low, range, done2 ? esc2 + h2.under : 0u, done2 ? h2.cnt : esc2, h2.tot, o,
                  done2 || (en2 && esc2 > 0 && esc2 < h2.tot), ok);
+        PROF(2)
         const bool pend = en2 && !h2.found;
         uint32_t nxt = h2.link;
 
@@ -685,14 +754,18 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         nxt = en1 ? h1.link : nxt;
         const bool nfresh = en1 && !h1.found;
         rec_set_link(reg, r2, h2.k, nxt, pend);
+        PROF(3)
         enc_code(low, range, done1 ? esc1 + h1.under : 0u, done1 ? h1.cnt : esc1, h1.tot, o,
                  done1 || (en1 && esc1 > 0 && esc1 < h1.tot), ok);
+        PROF(4)
 
         // next order-2 record: fresh, the one just updated, or a load
         const bool same2 = en2 && nxt * kO2Rec == r2.off;
+        o2_fresh(0, n2);
         if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
         if (en1) o1_store(reg, r1);
         if (en2) o2_store(reg, r2);
+        PROF(5)
 
         // root, compress.c:318-329
         const bool en0 = !done2 && !done1;
@@ -700,10 +773,12 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         root_lookup(root, v, under0, cnt0);
         if (en0) root_add(root, v, cnt0);
         nodes += (en0 && cnt0 == 0) ? 1u : 0u;
+        PROF(6)
         enc_code(low, range, 1 + under0, 1 + cnt0, rtot, o, en0, ok);
         rtot = en0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
         const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit);
         if (any_lane(rs0)) { if (rs0) rtot = root_rescale(root); }
+        PROF(7)
 
         if (any_lane(!ok || ovf)) { if (!ok || ovf) break; }
 
@@ -723,7 +798,9 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
                 rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0;
             }
         }
+        PROF(8)
     }
+    PROF_FLUSH(0)
     if (ovf) { flag_exact(ws, pkt); return; }
     // flush, compress.c:139-146
     while (any_lane(ok && low != 0)) {
@@ -767,7 +844,13 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
     o2_fresh(0, r2);
     rec_clear(r1);
 
+    PROF_DECL
     for (;;) {
+        PROF(11)
+#ifdef RC_PROFILE_DRAIN
+        __builtin_amdgcn_s_waitcnt(0);       // diagnostic: charge outstanding memory to slot 8
+        PROF(8)
+#endif
         int at = -1;                         // context that produced the symbol (2, 1, 0)
         uint32_t v = 0, nxt = 0;
         bool nfresh = false;
@@ -775,8 +858,8 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         if (order >= 2 && r2.esc > 0) {                              // compress.c:529-568
             const uint32_t tot = rec_total(reg, r2);
             if (r2.esc < tot) {
-                range /= tot;
-                uint32_t cd = ((code - low) / range) & 0xFFFF;
+                range = udiv(range, tot);
+                uint32_t cd = udiv(code - low, range) & 0xFFFF;
                 if (cd < r2.esc) {
                     dec_code(low, code, range, 0, r2.esc, in, true);
                 } else {
@@ -791,11 +874,12 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
                 }
             }
         }
+        PROF(0)
         if (at < 0 && order >= 1 && r1.esc > 0) {
             const uint32_t tot = rec_total(reg, r1);
             if (r1.esc < tot) {
-                range /= tot;
-                uint32_t cd = ((code - low) / range) & 0xFFFF;
+                range = udiv(range, tot);
+                uint32_t cd = udiv(code - low, range) & 0xFFFF;
                 if (cd < r1.esc) {
                     dec_code(low, code, range, 0, r1.esc, in, true);
                 } else {
@@ -810,15 +894,15 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
                 }
             }
         }
+        PROF(1)
         if (at < 0) {                                                // root, compress.c:570-596
-            range /= rtot;
-            uint32_t cd = ((code - low) / range) & 0xFFFF;
+            range = udiv(range, rtot);
+            uint32_t cd = udiv(code - low, range) & 0xFFFF;
             if (cd < 1) { dec_code(low, code, range, 0, 1, in, true); break; }   // end of stream
             cd -= 1;
             if (cd >= rtot - 1) { anomaly = true; break; }          // past symbol 255
-            v = root_search(root, cd);
             uint32_t under, cnt;
-            root_lookup(root, v, under, cnt);
+            v = root_search(root, cd, under, cnt);
             if (cnt == 0) ++nodes;
             root_add(root, v, cnt);
             dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
@@ -826,16 +910,19 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
             if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
             at = 0;
         }
+        PROF(2)
         Rec<kO1Inl> n1;
         o1_load(reg, v, n1);                                         // next step's order-1 record
         // patch the contexts above, compress.c:598-615
         bool pend = false;
         uint32_t kpend = 0;
+        PROF(3)
         if (order >= 2 && at < 2) {
             const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, true);
             if (ovf) break;
             if (!h.found) { pend = true; kpend = h.k; }
         }
+        PROF(4)
         if (order >= 1 && at < 1) {
             const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf, true);
             if (ovf) break;
@@ -843,14 +930,17 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
             nfresh = !h.found;
         }
         rec_set_link(reg, r2, kpend, nxt, pend);
+        PROF(5)
         Rec<kO2Inl> n2;
         o2_fresh(nxt, n2);
         const bool same2 = order >= 2 && nxt * kO2Rec == r2.off;
         if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
         if (order >= 2) o2_store(reg, r2);
         if (order >= 1 && at <= 1) o1_store(reg, r1);
+        PROF(6)
         if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
         outwin_put(o, v, true);
+        PROF(7)
         if (order >= 1 && !same2) rec2_copy(r2, n2);
         if (!(order >= 1 && v == b1)) r1 = n1;
         if (order < 2) ++order;
@@ -862,12 +952,27 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
             }
         }
     }
+    PROF_FLUSH(16)
     if (ovf || anomaly) { flag_exact(ws, pkt); return; }
     outwin_finish(o, !fail);
     b.out_len[pkt] = fail ? 0u : o.n;
 }
 
 }  // namespace
+
+#ifdef RC_PROFILE
+// diagnostic build: copy out (and optionally clear) the phase counters
+extern "C" int rc_lane_prof_read(unsigned long long* out, int reset)
+{
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 64);
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[64] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+    }
+    return static_cast<int>(e);
+}
+#endif
 
 extern "C" uint32_t rc_hip_lane_region_bytes(uint32_t max_len)
 {
