@@ -254,6 +254,20 @@ DEV void o2_store(uint8_t* reg, const Rec<kO2Inl>& r)
     *reinterpret_cast<uint2*>(reg + r.off) = make_uint2(r.esc | (r.len << 16), r.ext ? r.ext : r.e[0]);
 }
 
+// Extension blocks are read and written 16 entries (four 16-B chunks) at a
+// time: the four loads are in flight together, so a context of n entries costs
+// ceil(n / 16) memory round trips instead of one per chunk or per entry.
+constexpr uint32_t kGrp = 16;
+
+DEV void grp_load(const uint32_t* ep, uint32_t g0, uint32_t n, uint4 (&q)[4])
+{
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        q[j] = g0 + 4 * j < n ? *reinterpret_cast<const uint4*>(ep + g0 + 4 * j) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+DEV uint32_t grp_get(const uint4 (&q)[4], uint32_t i) { return pick4(i & 3, q[i >> 2]); }
+
 // Encoder-side lookup of v (compress.c:159-199, minimum 0): k = first entry >= v,
 // under = counts below, found/cnt/link, tot = esc + all counts (before update).
 template <uint32_t INL>
@@ -279,12 +293,13 @@ DEV Hit rec_find(const uint8_t* reg, const Rec<INL>& r, uint32_t v)
     if (any_lane(r.ext != 0)) {
         if (r.ext != 0) {
             const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-            for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
-                const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
+            for (uint32_t g0 = 0; g0 < r.len; g0 += kGrp) {
+                uint4 q[4];
+                grp_load(ep, g0, r.len, q);
 #pragma unroll
-                for (uint32_t t = 0; t < 4; ++t) {
-                    const uint32_t e = pick4(t, q);
-                    const bool in = c0 + t < r.len;
+                for (uint32_t t = 0; t < kGrp; ++t) {
+                    const uint32_t e = grp_get(q, t);
+                    const bool in = g0 + t < r.len;
                     const uint32_t c = in ? cnt_of(e) : 0u;
                     const bool lt = in && val_of(e) < v;
                     const bool eq = in && val_of(e) == v;
@@ -312,10 +327,11 @@ DEV uint32_t rec_total(const uint8_t* reg, const Rec<INL>& r)
     if (any_lane(r.ext != 0)) {
         if (r.ext != 0) {
             const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-            for (uint32_t c0 = 0; c0 < r.len; c0 += 4) {
-                const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
+            for (uint32_t g0 = 0; g0 < r.len; g0 += kGrp) {
+                uint4 q[4];
+                grp_load(ep, g0, r.len, q);
 #pragma unroll
-                for (uint32_t t = 0; t < 4; ++t) sum += c0 + t < r.len ? cnt_of(pick4(t, q)) : 0u;
+                for (uint32_t t = 0; t < kGrp; ++t) sum += g0 + t < r.len ? cnt_of(grp_get(q, t)) : 0u;
             }
         }
     }
@@ -345,15 +361,16 @@ DEV Hit rec_search(const uint8_t* reg, const Rec<INL>& r, uint32_t code, bool en
     if (any_lane(en && r.ext != 0)) {
         if (en && r.ext != 0) {
             const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-            for (uint32_t c0 = 0; c0 < r.len && !found; c0 += 4) {
-                const uint4 q = *reinterpret_cast<const uint4*>(ep + c0);
+            for (uint32_t g0 = 0; g0 < r.len && !found; g0 += kGrp) {
+                uint4 q[4];
+                grp_load(ep, g0, r.len, q);
 #pragma unroll
-                for (uint32_t t = 0; t < 4; ++t) {
-                    const uint32_t e = pick4(t, q);
-                    const bool in = c0 + t < r.len;
+                for (uint32_t t = 0; t < kGrp; ++t) {
+                    const uint32_t e = grp_get(q, t);
+                    const bool in = g0 + t < r.len;
                     const uint32_t c = in ? cnt_of(e) : 0u;
                     const bool hit = in && !found && code < cum + c;
-                    h.k = hit ? c0 + t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
+                    h.k = hit ? g0 + t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
                     h.link = hit ? (e >> 16) : h.link; h.val = hit ? val_of(e) : h.val;
                     found = found || hit;
                     cum += c;
@@ -377,6 +394,35 @@ DEV void rec_bump(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t cnt, uint32_t 
     }
 }
 
+DEV void grp_put(uint4 (&o)[4], uint32_t i, uint32_t x)
+{
+    uint4& c = o[i >> 2];
+    switch (i & 3) { case 0: c.x = x; break; case 1: c.y = x; break; case 2: c.z = x; break; default: c.w = x; }
+}
+
+// dst[j], j in [0, n]: src[j] below k, ne at k, src[j-1] above k (src holds n
+// entries; the block holding dst has room for n + 1, rounded up to 4).  In
+// place (dst == src) the groups below k are not touched.  A group's stores
+// never reach the next group's entries, so they can precede its loads.
+DEV void ext_shift_insert(uint32_t* dst, const uint32_t* src, uint32_t n, uint32_t k, uint32_t ne, bool inplace)
+{
+    uint32_t carry = 0;
+    for (uint32_t g0 = inplace ? (k & ~(kGrp - 1)) : 0u; g0 <= n; g0 += kGrp) {
+        uint4 q[4], o[4];
+        grp_load(src, g0, n, q);
+#pragma unroll
+        for (uint32_t t = 0; t < kGrp; ++t) {
+            const uint32_t j = g0 + t;
+            const uint32_t prev = t == 0 ? carry : grp_get(q, t - 1);
+            grp_put(o, t, j < k ? grp_get(q, t) : (j == k ? ne : prev));
+        }
+        carry = grp_get(q, kGrp - 1);
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c)
+            if (g0 + 4 * c <= n) *reinterpret_cast<uint4*>(dst + g0 + 4 * c) = o[c];
+    }
+}
+
 // Insert entry `ne` at position k where `en`; moves to / grows an extension
 // block when the inline slots or the block are full.  false = region full.
 template <uint32_t INL, uint32_t MINCAP>
@@ -396,8 +442,7 @@ DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t
             const uint32_t cap = r.ext ? cap_for(r.len, MINCAP) : INL;
             if (r.ext != 0 && r.len < cap) {
                 uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
-                for (uint32_t j = r.len; j > k; --j) ep[j] = ep[j - 1];
-                ep[k] = ne;
+                ext_shift_insert(ep, ep, r.len, k, ne, true);
             } else {
                 const uint32_t ncap = r.ext ? 2 * cap : MINCAP;
                 const uint32_t at = (bump + 15) & ~15u;
@@ -408,11 +453,11 @@ DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t
                     if (r.ext == 0) {
 #pragma unroll
                         for (uint32_t t = 0; t < INL; ++t) np[t + (t >= k ? 1u : 0u)] = r.e[t];
+                        np[k] = ne;
                     } else {
                         const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-                        for (uint32_t j = 0; j < r.len; ++j) np[j + (j >= k ? 1u : 0u)] = ep[j];
+                        ext_shift_insert(np, ep, r.len, k, ne, false);
                     }
-                    np[k] = ne;
                     r.ext = at;
                     bump = at + 4 * ncap;
                 }
@@ -450,10 +495,19 @@ DEV void rec_rescale(uint8_t* reg, Rec<INL>& r, bool en)
         r.e[t] = (inl && t < r.len) ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
     }
     if (en && r.ext != 0) {
-        uint8_t* ep = reg + r.ext;
-        for (uint32_t j = 0; j < r.len; ++j) {
-            const uint32_t c = ep[4 * j + 1];
-            ep[4 * j + 1] = static_cast<uint8_t>(c - (c >> 1));
+        uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
+        for (uint32_t g0 = 0; g0 < r.len; g0 += kGrp) {
+            uint4 q[4];
+            grp_load(ep, g0, r.len, q);
+#pragma unroll
+            for (uint32_t t = 0; t < kGrp; ++t) {
+                const uint32_t e = grp_get(q, t);
+                const uint32_t c = cnt_of(e);
+                grp_put(q, t, (e & 0xFFFF00FFu) | ((c - (c >> 1)) << 8));
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+                if (g0 + 4 * c < r.len) *reinterpret_cast<uint4*>(ep + g0 + 4 * c) = q[c];
         }
     }
     r.esc -= en ? (r.esc >> 1) : 0u;
