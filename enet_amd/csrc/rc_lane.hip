@@ -188,25 +188,28 @@ DEV uint32_t root_rescale(uint8_t* r)
 }
 
 // ---------------------------------------------------- order 1/2 records (HBM)
-// o1 record, 64 B, direct-mapped by the context byte:
-//     w0 = esc | len << 16, w1 = ext offset (0 = entries inline), 14 inline entries
-// o2 record, 8 B, bump-allocated so that the records touched by consecutive
-//     steps share HBM sectors:
-//     w0 = esc | len << 16, w1 = the only entry while len <= 1, else ext offset
-// entry = value | count << 8 | link << 16, link = o2 record index (offset / 8):
+// Both record kinds start with the same two words:
+//     w0 = esc | len << 16,  w1 = ext / 16 | total << 16
+// (ext = extension block offset, 0 while the entries are inline; total =
+// esc + sum(counts) mod 2^16, maintained like compress.c's (:309-312, rescale
+// :107-112), so no lookup has to sum the counts).
+// o1 record, 64 B, direct-mapped by the context byte: header + 14 inline entries.
+// o2 record, 16 B, bump-allocated so that the records touched by consecutive
+//     steps share HBM sectors: header + 2 inline entries.
+// entry = value | count << 8 | link << 16, link = o2 record index (offset / 16):
 //     in an o1 entry the context (prev, value); in an o2 entry the suffix
 //     context (compress.c's `parent`, :294-295, :615).
-// total is not stored: total = esc + sum(counts) holds after every update of
-// compress.c (:309-312) and every rescale (:107-112).  A freshly allocated o2
-// record is never zero-filled or loaded: its first visit is the very next
-// step, which knows it is empty.
+// A freshly allocated o2 record is never zero-filled or loaded: its first
+// visit is the very next step, which knows it is empty.
 
 constexpr uint32_t kO1Rec = 64, kO1Inl = 14, kO1MinCap = 32;
-constexpr uint32_t kO2Rec = 8, kO2Inl = 1, kO2MinCap = 4;
+constexpr uint32_t kO2Rec = 16, kO2Inl = 2, kO2MinCap = 4;
 constexpr uint32_t kArenaBase = 256 * kO1Rec;
 
 template <uint32_t INL>
-struct Rec { uint32_t off, esc, len, ext; uint32_t e[INL]; };
+struct Rec { uint32_t off, esc, len, ext, tot; uint32_t e[INL]; };
+
+DEV uint32_t hdr_w1(uint32_t ext, uint32_t tot) { return (ext >> 4) | (tot << 16); }
 
 struct Hit { uint32_t k, under, cnt, link, val, tot; bool found; };
 
@@ -219,7 +222,8 @@ DEV void o1_load(const uint8_t* reg, uint32_t x, Rec<kO1Inl>& r)
 {
     const uint4* p = reinterpret_cast<const uint4*>(reg + x * kO1Rec);
     const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    r.off = x * kO1Rec; r.esc = q0.x & 0xFFFF; r.len = q0.x >> 16; r.ext = q0.y;
+    r.off = x * kO1Rec; r.esc = q0.x & 0xFFFF; r.len = q0.x >> 16;
+    r.ext = (q0.y & 0xFFFF) << 4; r.tot = q0.y >> 16;
     r.e[0] = q0.z; r.e[1] = q0.w;
     r.e[2] = q1.x; r.e[3] = q1.y; r.e[4] = q1.z; r.e[5] = q1.w;
     r.e[6] = q2.x; r.e[7] = q2.y; r.e[8] = q2.z; r.e[9] = q2.w;
@@ -230,7 +234,7 @@ DEV void o1_load(const uint8_t* reg, uint32_t x, Rec<kO1Inl>& r)
 DEV void o1_store(uint8_t* reg, const Rec<kO1Inl>& r)
 {
     uint4* p = reinterpret_cast<uint4*>(reg + r.off);
-    p[0] = make_uint4(r.esc | (r.len << 16), r.ext, r.e[0], r.e[1]);
+    p[0] = make_uint4(r.esc | (r.len << 16), hdr_w1(r.ext, r.tot), r.e[0], r.e[1]);
     p[1] = make_uint4(r.e[2], r.e[3], r.e[4], r.e[5]);
     p[2] = make_uint4(r.e[6], r.e[7], r.e[8], r.e[9]);
     p[3] = make_uint4(r.e[10], r.e[11], r.e[12], r.e[13]);
@@ -238,20 +242,20 @@ DEV void o1_store(uint8_t* reg, const Rec<kO1Inl>& r)
 
 DEV void o2_load(const uint8_t* reg, uint32_t idx, Rec<kO2Inl>& r)
 {
-    const uint2 q = *reinterpret_cast<const uint2*>(reg + idx * kO2Rec);
+    const uint4 q = *reinterpret_cast<const uint4*>(reg + idx * kO2Rec);
     r.off = idx * kO2Rec; r.esc = q.x & 0xFFFF; r.len = q.x >> 16;
-    r.ext = r.len >= 2 ? q.y : 0u;
-    r.e[0] = r.len >= 2 ? 0u : q.y;
+    r.ext = (q.y & 0xFFFF) << 4; r.tot = q.y >> 16;
+    r.e[0] = q.z; r.e[1] = q.w;
 }
 
 DEV void o2_fresh(uint32_t idx, Rec<kO2Inl>& r)
 {
-    r.off = idx * kO2Rec; r.esc = 0; r.len = 0; r.ext = 0; r.e[0] = 0;
+    r.off = idx * kO2Rec; r.esc = 0; r.len = 0; r.ext = 0; r.tot = 0; r.e[0] = 0; r.e[1] = 0;
 }
 
 DEV void o2_store(uint8_t* reg, const Rec<kO2Inl>& r)
 {
-    *reinterpret_cast<uint2*>(reg + r.off) = make_uint2(r.esc | (r.len << 16), r.ext ? r.ext : r.e[0]);
+    *reinterpret_cast<uint4*>(reg + r.off) = make_uint4(r.esc | (r.len << 16), hdr_w1(r.ext, r.tot), r.e[0], r.e[1]);
 }
 
 // Extension blocks are read and written 16 entries (four 16-B chunks) at a
@@ -313,30 +317,13 @@ DEV Hit rec_find(const uint8_t* reg, const Rec<INL>& r, uint32_t v)
             }
         }
     }
-    h.tot = (r.esc + sum) & 0xFFFF;
+    (void) sum;
+    h.tot = r.tot;
     return h;
 }
 
 template <uint32_t INL>
-DEV uint32_t rec_total(const uint8_t* reg, const Rec<INL>& r)
-{
-    uint32_t sum = 0;
-    const uint32_t ilen = r.ext == 0 ? r.len : 0u;
-#pragma unroll
-    for (uint32_t t = 0; t < INL; ++t) sum += t < ilen ? cnt_of(r.e[t]) : 0u;
-    if (any_lane(r.ext != 0)) {
-        if (r.ext != 0) {
-            const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-            for (uint32_t g0 = 0; g0 < r.len; g0 += kGrp) {
-                uint4 q[4];
-                grp_load(ep, g0, r.len, q);
-#pragma unroll
-                for (uint32_t t = 0; t < kGrp; ++t) sum += g0 + t < r.len ? cnt_of(grp_get(q, t)) : 0u;
-            }
-        }
-    }
-    return (r.esc + sum) & 0xFFFF;
-}
+DEV uint32_t rec_total(const uint8_t*, const Rec<INL>& r) { return r.tot; }
 
 // Decoder search (compress.c:373-416, minimum 0) where `en`: entry whose
 // interval holds code.  Returns false (corrupt stream) when none does.
@@ -487,12 +474,15 @@ DEV void rec_rescale(uint8_t* reg, Rec<INL>& r, bool en)
 {
     if (!any_lane(en)) return;
     const bool inl = en && r.ext == 0;
+    uint32_t sum = 0;
 #pragma unroll
     for (uint32_t t = 0; t < INL; ++t) {
         const uint32_t e = r.e[t];
         uint32_t c = cnt_of(e);
         c -= c >> 1;
-        r.e[t] = (inl && t < r.len) ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
+        const bool live = inl && t < r.len;
+        r.e[t] = live ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
+        sum += live ? c : 0u;
     }
     if (en && r.ext != 0) {
         uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
@@ -502,8 +492,9 @@ DEV void rec_rescale(uint8_t* reg, Rec<INL>& r, bool en)
 #pragma unroll
             for (uint32_t t = 0; t < kGrp; ++t) {
                 const uint32_t e = grp_get(q, t);
-                const uint32_t c = cnt_of(e);
-                grp_put(q, t, (e & 0xFFFF00FFu) | ((c - (c >> 1)) << 8));
+                const uint32_t c = cnt_of(e) - (cnt_of(e) >> 1);
+                grp_put(q, t, (e & 0xFFFF00FFu) | (c << 8));
+                sum += g0 + t < r.len ? c : 0u;
             }
 #pragma unroll
             for (uint32_t c = 0; c < 4; ++c)
@@ -511,6 +502,7 @@ DEV void rec_rescale(uint8_t* reg, Rec<INL>& r, bool en)
         }
     }
     r.esc -= en ? (r.esc >> 1) : 0u;
+    r.tot = en ? ((r.esc + sum) & 0xFFFF) : r.tot;                  // compress.c:107-112
 }
 
 // Encoder-side update of a sub-context where `en` (compress.c:293-314, patch
@@ -538,6 +530,7 @@ DEV Hit sub_update(uint8_t* reg, Rec<INL>& r, uint32_t v, uint32_t& bump,
     nodes += ins ? 1u : 0u;
     r.esc += ins ? kSubEscDelta : 0u;
     const uint32_t tot = (h.tot + (ins ? kSubEscDelta : 0u) + kSubDelta) & 0xFFFF;
+    r.tot = en ? tot : r.tot;
     rec_rescale(reg, r, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
     return h;
 }
@@ -745,7 +738,7 @@ DEV void flag_exact(const rc_workspace_dev& ws, uint32_t pkt)
 
 DEV void rec_clear(Rec<kO1Inl>& r1)
 {
-    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0;
+    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0; r1.tot = 0;
 #pragma unroll
     for (uint32_t t = 0; t < kO1Inl; ++t) r1.e[t] = 0;
 }
@@ -870,7 +863,7 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
 
 DEV void rec2_copy(Rec<kO2Inl>& d, const Rec<kO2Inl>& r)
 {
-    d.off = r.off; d.esc = r.esc; d.len = r.len; d.ext = r.ext; d.e[0] = r.e[0];
+    d.off = r.off; d.esc = r.esc; d.len = r.len; d.ext = r.ext; d.tot = r.tot; d.e[0] = r.e[0]; d.e[1] = r.e[1];
 }
 
 // The decoder keeps data-dependent branches: unlike the encoder, each level's
@@ -922,6 +915,7 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
                     v = h.val;
                     rec_bump(reg, r2, h.k, h.cnt, kSubDelta, true);
                     dec_code(low, code, range, r2.esc + h.under, h.cnt, in, true);
+                    r2.tot = (tot + kSubDelta) & 0xFFFF;
                     rec_rescale(reg, r2, h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit);
                     nxt = h.link;
                     at = 2;
@@ -942,6 +936,7 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
                     v = h.val;
                     rec_bump(reg, r1, h.k, h.cnt, kSubDelta, true);
                     dec_code(low, code, range, r1.esc + h.under, h.cnt, in, true);
+                    r1.tot = (tot + kSubDelta) & 0xFFFF;
                     rec_rescale(reg, r1, h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit);
                     nxt = h.link;
                     at = 1;
