@@ -16,7 +16,8 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
            "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
            "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_INST_CYCLES_SALU SQ_INST_CYCLES_VMEM_RD" \
            "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B" \
-           "TCC_EA0_WRREQ TCC_EA0_WRREQ_64B"; do
+           "TCC_EA0_WRREQ TCC_EA0_WRREQ_64B" \
+           "SQ_WAVES SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_IFETCH"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- $B --steps 1 --warmup 0 "$@" > $OUT/bench_pmc$i.log 2>&1 || echo "pmc group $i failed: $grp" >> $OUT/errors.txt
 done
