@@ -82,6 +82,8 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
     c->ws.lane_pool = NULL; c->ws.lane_slots = 0; c->ws.lane_region = 0;
     if (hipMalloc(&c->ws.lane_pool, slots * (size_t) region) != hipSuccess) return -1;
+    /* lane regions start at epoch 0: no order-1 record is live (rc_lane.hip) */
+    if (hipMemset(c->ws.lane_pool, 0, slots * (size_t) region) != hipSuccess) return -1;
     c->ws.lane_slots = (uint32_t) slots;
     c->ws.lane_region = region;
     return 0;

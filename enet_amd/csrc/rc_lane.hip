@@ -11,27 +11,27 @@
 // advance in lock-step in one wave, so the same arithmetic is one VALU
 // instruction for 64 packets.
 //
-// Model layout (only {count[v], escapes, total} per context and the node
-// count are observable):
+// Model (only {count[v], escapes, total} per context and the node count are
+// observable):
 //   order 0 (root): per lane in LDS, counts[256] (u8) + C[16] (u16 cumulative
 //       count at the end of each 16-symbol group) -> lookups are 1-2 LDS
 //       reads + byte-SAD sums, no tree walk.
-//   order 1: 256 records of 64 B, direct-mapped by the previous byte, in a
-//       per-lane HBM region; order 2: 8-B records bump-allocated in the same
-//       region, reached through links stored in the entries (compress.c's
-//       suffix links, `parent`).  Entries are sorted {value | count | link};
-//       contexts that outgrow their inline slots use an extension block.
+//   orders 1 and 2: records in a per-lane HBM region holding each context's
+//       symbols as sorted byte arrays (values, counts) that are searched and
+//       updated four symbols per instruction (byte permutes, v_dot4, v_sad);
+//       large contexts switch to a dense 256-symbol table.  See "order 1/2
+//       contexts" below for the layout.
 //   Each byte costs one HBM round trip, and that load is issued a step ahead.
 //
 // Code shape: 64 lanes run 64 different packets, so every `if` on per-lane
 // data is divergent.  Common paths are written as straight-line predicated
-// register code; rare paths (extension blocks, growth, rescale, packet edges,
-// model reset) sit behind wave-uniform ballot guards so a wave that does not
-// need them pays one scalar branch.
+// register code; rare paths (dense contexts, rescale, packet edges, model
+// reset) sit behind wave-uniform ballot guards so a wave that does not need
+// them pays one scalar branch.
 //
 // Packets this model cannot reproduce -- corrupt streams whose root code
 // points past symbol 255 (compress.c:427-438 then depends on tree shape) --
-// and packets whose region overflows are appended to the exact-path list
+// and packets that exhaust their region are appended to the exact-path list
 // (rc_kernels.hip), which re-runs compress.c's binary-tree model.
 
 #ifndef RC_LANE_HOST_TEST
@@ -187,358 +187,490 @@ DEV uint32_t root_rescale(uint8_t* r)
     return (sum + 1 + 256) & 0xFFFF;
 }
 
-// ---------------------------------------------------- order 1/2 records (HBM)
-// Both record kinds start with the same two words:
-//     w0 = esc | len << 16,  w1 = ext / 16 | total << 16
-// (ext = extension block offset, 0 while the entries are inline; total =
-// esc + sum(counts) mod 2^16, maintained like compress.c's (:309-312, rescale
-// :107-112), so no lookup has to sum the counts).
-// o1 record, 64 B, direct-mapped by the context byte: header + 14 inline entries.
-// o2 record, 16 B, bump-allocated so that the records touched by consecutive
-//     steps share HBM sectors: header + 2 inline entries.
-// entry = value | count << 8 | link << 16, link = o2 record index (offset / 16):
-//     in an o1 entry the context (prev, value); in an o2 entry the suffix
-//     context (compress.c's `parent`, :294-295, :615).
-// A freshly allocated o2 record is never zero-filled or loaded: its first
-// visit is the very next step, which knows it is empty.
+// ------------------------------------------------ order 1/2 contexts (HBM)
+// Per lane region (rc_hip_lane_region_bytes):
+//   [0, 64)        lane header: epoch counter (u32)
+//   [64, +16 KiB)  order-1 table: 256 records of 64 B, direct-mapped by the
+//                  context byte
+//   arena          bump-allocated: order-2 records (32 B) and dense blocks
+//
+// A record holds a context's symbols as parallel byte arrays, sorted by value:
+//   w0 = tag | len << 16 | dense << 24   (o1: tag = epoch, the record is
+//                                          empty unless it matches; o2: 0)
+//   w1 = esc | total << 16               (total = esc + sum(counts) mod 2^16,
+//                                          maintained as compress.c:309-314)
+//   w2 = dense block offset (when dense)
+//   o1 (64 B): w4..w6 vals[12], w7..w9 counts[12], w10..w15 links[12] (u16:
+//       the o2 record of context (prev, val), compress.c's `parent` chain)
+//   o2 (32 B): w4..w5 vals[8], w6..w7 counts[8]
+// Unused slots hold value 0xFF and count 0, so the byte-parallel (SWAR)
+// scans need no length mask: a present symbol's count is never 0 (rescale
+// keeps c - c/2 >= 1).  A context that outgrows its inline slots becomes
+// dense: C[16] (u16 cumulative group sums) + counts[256] (+ links[256] for
+// o1), found through w2 -- lookups are O(1) like the root's.
+//
+// Every packet and every model reset (compress.c:148-157) starts a new epoch:
+// o1 records from older epochs read as empty, the arena restarts, and o2
+// records are only reachable through current o1 links -- nothing is cleared.
+// o2 entries carry no links: the next o2 context (prev, v) is found through
+// o1[prev], which the step has loaded anyway.
 
-constexpr uint32_t kO1Rec = 64, kO1Inl = 14, kO1MinCap = 32;
-constexpr uint32_t kO2Rec = 16, kO2Inl = 2, kO2MinCap = 4;
-constexpr uint32_t kArenaBase = 256 * kO1Rec;
+constexpr uint32_t kO1Base = 64, kO1Rec = 64, kO1NV = 3, kO2Rec = 32, kO2NV = 2;
+constexpr uint32_t kArenaBase = kO1Base + 256 * kO1Rec;
+constexpr uint32_t kDenseO1 = 32 + 256 + 512, kDenseO2 = 32 + 256;
+constexpr uint32_t kDenseBudget = 0xFFFFFFFFu;   // dense blocks are bounded by the region size
 
-template <uint32_t INL>
-struct Rec { uint32_t off, esc, len, ext, tot; uint32_t e[INL]; };
+DEV uint32_t dot4(uint32_t a, uint32_t b, uint32_t acc) { return __builtin_amdgcn_udot4(a, b, acc, false); }
+DEV uint32_t bperm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+DEV uint32_t align8(uint32_t hi, uint32_t lo, uint32_t n) { return __builtin_amdgcn_alignbyte(hi, lo, n); }
 
-DEV uint32_t hdr_w1(uint32_t ext, uint32_t tot) { return (ext >> 4) | (tot << 16); }
-
-struct Hit { uint32_t k, under, cnt, link, val, tot; bool found; };
-
-DEV uint32_t cap_for(uint32_t len, uint32_t mincap)
+// 0x01 in each byte of w that is >= the value behind ny (= 0x01000100 - v * 0x00010001)
+DEV uint32_t swar_ge(uint32_t w, uint32_t ny)
 {
-    return len <= mincap ? mincap : (1u << (32 - __builtin_clz(len - 1)));
+    const uint32_t te = bperm(0u, w, 0x0C020C00u) + ny;   // bytes 0, 2 in 16-bit halves, + 256 - v
+    const uint32_t to = bperm(0u, w, 0x0C030C01u) + ny;   // bytes 1, 3
+    return bperm(to, te, 0x07030501u);                     // the carry bytes: 1 iff byte >= v
 }
 
-DEV void o1_load(const uint8_t* reg, uint32_t x, Rec<kO1Inl>& r)
+// bytes [0, k) of dword d (k relative to the array start) as a mask
+DEV uint32_t below_mask(int k, int d)
 {
-    const uint4* p = reinterpret_cast<const uint4*>(reg + x * kO1Rec);
+    const int kk = k - 4 * d;
+    return kk <= 0 ? 0u : (kk >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kk)) - 1u));
+}
+
+DEV uint32_t byte_mask(int k, int d)
+{
+    const int kk = k - 4 * d;
+    return (kk >= 0 && kk < 4) ? (0xFFu << (8 * kk)) : 0u;
+}
+
+template <uint32_t NV>
+struct Ctx {
+    uint32_t off, tag, len, dense, esc, tot, ext;
+    uint32_t val[NV], cnt[NV];
+    uint32_t lnk[2 * NV];            // o1 only (u16 pairs); unused for o2
+};
+using Ctx1 = Ctx<kO1NV>;
+using Ctx2 = Ctx<kO2NV>;
+
+template <uint32_t NV>
+DEV void ctx_empty(Ctx<NV>& c, uint32_t off, uint32_t tag)
+{
+    c.off = off; c.tag = tag; c.len = 0; c.dense = 0; c.esc = 0; c.tot = 0; c.ext = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < NV; ++d) { c.val[d] = 0xFFFFFFFFu; c.cnt[d] = 0u; }
+#pragma unroll
+    for (uint32_t d = 0; d < 2 * NV; ++d) c.lnk[d] = 0u;
+}
+
+DEV void o1_load(const uint8_t* reg, uint32_t x, uint32_t epoch, Ctx1& c)
+{
+    const uint4* p = reinterpret_cast<const uint4*>(reg + kO1Base + x * kO1Rec);
     const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    r.off = x * kO1Rec; r.esc = q0.x & 0xFFFF; r.len = q0.x >> 16;
-    r.ext = (q0.y & 0xFFFF) << 4; r.tot = q0.y >> 16;
-    r.e[0] = q0.z; r.e[1] = q0.w;
-    r.e[2] = q1.x; r.e[3] = q1.y; r.e[4] = q1.z; r.e[5] = q1.w;
-    r.e[6] = q2.x; r.e[7] = q2.y; r.e[8] = q2.z; r.e[9] = q2.w;
-    r.e[10] = q3.x; r.e[11] = q3.y; r.e[12] = q3.z; r.e[13] = q3.w;
+    const bool live = (q0.x & 0xFFFF) == epoch;
+    c.off = kO1Base + x * kO1Rec; c.tag = epoch;
+    c.len = live ? (q0.x >> 16) & 0xFF : 0u;
+    c.dense = live ? q0.x >> 24 : 0u;
+    c.esc = live ? q0.y & 0xFFFF : 0u;
+    c.tot = live ? q0.y >> 16 : 0u;
+    c.ext = q0.z;
+    c.val[0] = live ? q1.x : 0xFFFFFFFFu; c.val[1] = live ? q1.y : 0xFFFFFFFFu; c.val[2] = live ? q1.z : 0xFFFFFFFFu;
+    c.cnt[0] = live ? q1.w : 0u; c.cnt[1] = live ? q2.x : 0u; c.cnt[2] = live ? q2.y : 0u;
+    c.lnk[0] = q2.z; c.lnk[1] = q2.w; c.lnk[2] = q3.x; c.lnk[3] = q3.y; c.lnk[4] = q3.z; c.lnk[5] = q3.w;
 }
 
-// in ext mode the inline slots are dead, so they are written unconditionally
-DEV void o1_store(uint8_t* reg, const Rec<kO1Inl>& r)
+DEV void o1_store(uint8_t* reg, const Ctx1& c)
 {
-    uint4* p = reinterpret_cast<uint4*>(reg + r.off);
-    p[0] = make_uint4(r.esc | (r.len << 16), hdr_w1(r.ext, r.tot), r.e[0], r.e[1]);
-    p[1] = make_uint4(r.e[2], r.e[3], r.e[4], r.e[5]);
-    p[2] = make_uint4(r.e[6], r.e[7], r.e[8], r.e[9]);
-    p[3] = make_uint4(r.e[10], r.e[11], r.e[12], r.e[13]);
+    uint4* p = reinterpret_cast<uint4*>(reg + c.off);
+    p[0] = make_uint4(c.tag | (c.len << 16) | (c.dense << 24), c.esc | (c.tot << 16), c.ext, 0u);
+    p[1] = make_uint4(c.val[0], c.val[1], c.val[2], c.cnt[0]);
+    p[2] = make_uint4(c.cnt[1], c.cnt[2], c.lnk[0], c.lnk[1]);
+    p[3] = make_uint4(c.lnk[2], c.lnk[3], c.lnk[4], c.lnk[5]);
 }
 
-DEV void o2_load(const uint8_t* reg, uint32_t idx, Rec<kO2Inl>& r)
+DEV void o2_load(const uint8_t* reg, uint32_t idx, Ctx2& c)
 {
-    const uint4 q = *reinterpret_cast<const uint4*>(reg + idx * kO2Rec);
-    r.off = idx * kO2Rec; r.esc = q.x & 0xFFFF; r.len = q.x >> 16;
-    r.ext = (q.y & 0xFFFF) << 4; r.tot = q.y >> 16;
-    r.e[0] = q.z; r.e[1] = q.w;
+    const uint4* p = reinterpret_cast<const uint4*>(reg + idx * kO2Rec);
+    const uint4 q0 = p[0], q1 = p[1];
+    c.off = idx * kO2Rec; c.tag = 0;
+    c.len = (q0.x >> 16) & 0xFF; c.dense = q0.x >> 24;
+    c.esc = q0.y & 0xFFFF; c.tot = q0.y >> 16; c.ext = q0.z;
+    c.val[0] = q1.x; c.val[1] = q1.y; c.cnt[0] = q1.z; c.cnt[1] = q1.w;
+    c.lnk[0] = c.lnk[1] = c.lnk[2] = c.lnk[3] = 0u;
 }
 
-DEV void o2_fresh(uint32_t idx, Rec<kO2Inl>& r)
+DEV void o2_store(uint8_t* reg, const Ctx2& c)
 {
-    r.off = idx * kO2Rec; r.esc = 0; r.len = 0; r.ext = 0; r.tot = 0; r.e[0] = 0; r.e[1] = 0;
+    uint4* p = reinterpret_cast<uint4*>(reg + c.off);
+    p[0] = make_uint4((c.len << 16) | (c.dense << 24), c.esc | (c.tot << 16), c.ext, 0u);
+    p[1] = make_uint4(c.val[0], c.val[1], c.cnt[0], c.cnt[1]);
 }
 
-DEV void o2_store(uint8_t* reg, const Rec<kO2Inl>& r)
+// link of slot k (o1 inline)
+template <uint32_t NV>
+DEV uint32_t lnk_get(const Ctx<NV>& c, uint32_t k)
 {
-    *reinterpret_cast<uint4*>(reg + r.off) = make_uint4(r.esc | (r.len << 16), hdr_w1(r.ext, r.tot), r.e[0], r.e[1]);
-}
-
-// Extension blocks are read and written 16 entries (four 16-B chunks) at a
-// time: the four loads are in flight together, so a context of n entries costs
-// ceil(n / 16) memory round trips instead of one per chunk or per entry.
-constexpr uint32_t kGrp = 16;
-
-DEV void grp_load(const uint32_t* ep, uint32_t g0, uint32_t n, uint4 (&q)[4])
-{
+    // masked OR, not a select chain: the compiler turns selects between
+    // fields into a dynamically indexed load, which forces the record into
+    // scratch memory
+    const uint32_t d = k >> 1;
+    uint32_t w = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        q[j] = g0 + 4 * j < n ? *reinterpret_cast<const uint4*>(ep + g0 + 4 * j) : make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = 0; i < 2 * NV; ++i) w |= c.lnk[i] & (0u - static_cast<uint32_t>(d == i));
+    return (w >> (16 * (k & 1))) & 0xFFFF;
 }
 
-DEV uint32_t grp_get(const uint4 (&q)[4], uint32_t i) { return pick4(i & 3, q[i >> 2]); }
+// ---------------------------------------------------------------- dense
+// block: C[16] (u16, C[g] = counts of groups 0..g) | counts[256] | links[256] (o1)
 
-// Encoder-side lookup of v (compress.c:159-199, minimum 0): k = first entry >= v,
-// under = counts below, found/cnt/link, tot = esc + all counts (before update).
-template <uint32_t INL>
-DEV Hit rec_find(const uint8_t* reg, const Rec<INL>& r, uint32_t v)
+struct Dense { uint4 c0, c1, grp; uint32_t link; };
+
+DEV uint32_t dense_c(const Dense& z, uint32_t g)       // C[g]
 {
-    Hit h = { 0u, 0u, 0u, 0u, v, 0u, false };
+    const uint32_t i = (g >> 1) & 3;
+    const uint32_t w = g < 8 ? pick4(i, z.c0) : pick4(i, z.c1);   // (not a select of references)
+    return (g & 1) ? (w >> 16) : (w & 0xFFFF);
+}
+
+// counts below v (minimum 0) and count[v] in a dense context; loads C, v's group and link
+DEV void dense_find(const uint8_t* blk, uint32_t v, bool links, Dense& z, uint32_t& under, uint32_t& cnt)
+{
+    const uint32_t g = v >> 4, j = v & 15;
+    const uint4* p = reinterpret_cast<const uint4*>(blk);
+    z.c0 = p[0]; z.c1 = p[1]; z.grp = p[2 + g];
+    z.link = links ? reinterpret_cast<const uint16_t*>(blk + 288)[v] : 0u;
+    uint32_t within = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+        const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
+        const uint32_t mask = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+        within = sad(pick4(d, z.grp) & mask, within);
+    }
+    under = (g ? dense_c(z, g - 1) : 0u) + within;
+    cnt = (pick4(j >> 2, z.grp) >> (8 * (j & 3))) & 0xFF;
+}
+
+// count[v] += d and C[g..15] += d, given z from dense_find / dense_search for v
+DEV void dense_add(uint8_t* blk, uint32_t v, uint32_t d, Dense& z)
+{
+    const uint32_t g = v >> 4, j = v & 15, bd = d << (8 * (j & 3)), q = j >> 2;
+    z.grp.x += q == 0 ? bd : 0u; z.grp.y += q == 1 ? bd : 0u;
+    z.grp.z += q == 2 ? bd : 0u; z.grp.w += q == 3 ? bd : 0u;
+    // C[t] += d for t >= g: word i holds C[2i] | C[2i + 1] << 16
+#define RC_CADD(w, t) w += ((t) >= g ? d : 0u) | ((t) + 1 >= g ? (d << 16) : 0u)
+    RC_CADD(z.c0.x, 0u); RC_CADD(z.c0.y, 2u); RC_CADD(z.c0.z, 4u); RC_CADD(z.c0.w, 6u);
+    RC_CADD(z.c1.x, 8u); RC_CADD(z.c1.y, 10u); RC_CADD(z.c1.z, 12u); RC_CADD(z.c1.w, 14u);
+#undef RC_CADD
+    uint4* p = reinterpret_cast<uint4*>(blk);
+    p[0] = z.c0; p[1] = z.c1; p[2 + g] = z.grp;
+}
+
+// decoder: symbol whose interval [C(<v), C(<=v)) holds code (minimum 0)
+DEV bool dense_search(const uint8_t* blk, uint32_t code, bool links, Dense& z, uint32_t& v, uint32_t& under,
+                      uint32_t& cnt)
+{
+    const uint4* p = reinterpret_cast<const uint4*>(blk);
+    z.c0 = p[0]; z.c1 = p[1];
+    uint32_t g = 0, prev = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 16; ++t) {
+        const uint32_t ct = dense_c(z, t);
+        const bool below = ct <= code;
+        g += below ? 1u : 0u;
+        prev = below ? ct : prev;
+    }
+    const bool inside = g < 16;
+    g = inside ? g : 15u;
+    z.grp = p[2 + g];
+    uint32_t base = prev, j = 0;
+    uint32_t s = sad(z.grp.x, sad(z.grp.y, 0u));
+    bool hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 8u : 0u;
+    const uint32_t d0 = hi ? z.grp.z : z.grp.x, d1 = hi ? z.grp.w : z.grp.y;
+    s = sad(d0, 0u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 4u : 0u;
+    uint32_t w = hi ? d1 : d0;
+    s = sad(w & 0xFFFFu, 0u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 2u : 0u;
+    w = hi ? (w >> 16) : w;
+    s = w & 0xFFu;
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 1u : 0u;
+    w = hi ? (w >> 8) : w;
+    v = 16 * g + j;
+    under = base;
+    cnt = w & 0xFFu;
+    z.link = links ? reinterpret_cast<const uint16_t*>(blk + 288)[v] : 0u;
+    return inside && cnt != 0 && code < base + cnt;
+}
+
+// compress.c:90-112 on a dense context; returns sum of the halved counts
+DEV uint32_t dense_rescale(uint8_t* blk)
+{
+    uint4* p = reinterpret_cast<uint4*>(blk);
+    uint32_t sum = 0, cw[8];
+#pragma unroll
+    for (uint32_t g = 0; g < 16; ++g) {
+        uint4 q = p[2 + g];
+        q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
+        q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
+        q.z -= (q.z >> 1) & 0x7F7F7F7Fu;
+        q.w -= (q.w >> 1) & 0x7F7F7F7Fu;
+        p[2 + g] = q;
+        sum = sad(q.w, sad(q.z, sad(q.y, sad(q.x, sum))));
+        if (g & 1) cw[g >> 1] |= sum << 16; else cw[g >> 1] = sum;
+    }
+    p[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    p[1] = make_uint4(cw[4], cw[5], cw[6], cw[7]);
+    return sum;
+}
+
+// move an inline context to a fresh dense block (where `en`); false = arena full
+template <uint32_t NV>
+DEV bool densify(uint8_t* reg, Ctx<NV>& c, uint32_t& bump, uint32_t end, bool links, bool en)
+{
+    const uint32_t size = links ? kDenseO1 : kDenseO2;
+    const uint32_t at = (bump + 15) & ~15u;
+    const bool ok = at + size <= end;
+    if (!(en && ok)) return !en;
+    bump = at + size;
+    uint8_t* blk = reg + at;
+    uint4* p = reinterpret_cast<uint4*>(blk);
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = 2; i < 18; ++i) p[i] = z;
+    uint32_t cw[8];
+#pragma unroll
+    for (uint32_t g = 0; g < 16; ++g) {                 // C[g] = counts of values < 16 (g + 1)
+        const uint32_t ny = 0x01000100u - (16 * (g + 1)) * 0x00010001u;
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < NV; ++d) s = dot4(c.cnt[d], swar_ge(c.val[d], ny) ^ 0x01010101u, s);
+        if (g & 1) cw[g >> 1] |= s << 16; else cw[g >> 1] = s;
+    }
+    p[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    p[1] = make_uint4(cw[4], cw[5], cw[6], cw[7]);
+#pragma unroll
+    for (uint32_t d = 0; d < NV; ++d) {
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            if (4 * d + t < c.len) {
+                const uint32_t vv = (c.val[d] >> (8 * t)) & 0xFF;
+                blk[32 + vv] = static_cast<uint8_t>((c.cnt[d] >> (8 * t)) & 0xFF);
+                if (links) reinterpret_cast<uint16_t*>(blk + 288)[vv] =
+                    static_cast<uint16_t>((c.lnk[2 * d + (t >> 1)] >> (16 * (t & 1))) & 0xFFFF);
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t d = 0; d < NV; ++d) { c.val[d] = 0xFFFFFFFFu; c.cnt[d] = 0u; }
+    c.dense = 1;
+    c.ext = at;
+    return true;
+}
+
+// ------------------------------------------------ lookup and update (SWAR)
+
+template <uint32_t NV>
+struct Look {
+    uint32_t k, under, cnt, link;
+    bool found;
+    uint32_t eq[NV];
+    Dense z;
+};
+
+// compress.c:159-199 lookup of v (minimum 0): insertion slot k, counts below
+// v, count[v]; plus the link (o1) when present
+template <uint32_t NV>
+DEV Look<NV> ctx_find(const uint8_t* reg, const Ctx<NV>& c, uint32_t v, bool links)
+{
+    Look<NV> h;
+    h.k = 0; h.under = 0; h.cnt = 0; h.link = 0;
+    const uint32_t ny = 0x01000100u - v * 0x00010001u;
+    const uint32_t ny1 = ny - 0x00010001u;
+#pragma unroll
+    for (uint32_t d = 0; d < NV; ++d) {
+        const uint32_t ge = swar_ge(c.val[d], ny);
+        const uint32_t lt = ge ^ 0x01010101u;
+        // equal = >= v and not >= v + 1, among the live slots (v = 255 matches padding)
+        h.eq[d] = (ge ^ swar_ge(c.val[d], ny1)) & below_mask(static_cast<int>(c.len), d) & 0x01010101u;
+        h.k = sad(lt, h.k);
+        h.under = dot4(c.cnt[d], lt, h.under);
+        h.cnt = dot4(c.cnt[d], h.eq[d], h.cnt);
+    }
+    if (links) h.link = lnk_get<NV>(c, h.k);
+    if (any_lane(c.dense != 0)) {
+        if (c.dense != 0) {
+            uint32_t u, n;
+            dense_find(reg + c.ext, v, links, h.z, u, n);
+            h.under = u; h.cnt = n; h.link = h.z.link;
+        }
+    }
+    h.found = h.cnt != 0;
+    return h;
+}
+
+// insert (v, count 2[, link]) at slot k of an inline context with a free slot
+template <uint32_t NV>
+DEV void inline_insert(Ctx<NV>& c, uint32_t k, uint32_t v, uint32_t link, bool links, bool en)
+{
+    const int kk = static_cast<int>(k);
+    uint32_t pv = 0xFFFFFFFFu, pc = 0u;
+#pragma unroll
+    for (uint32_t d = 0; d < NV; ++d) {
+        const uint32_t bm = below_mask(kk, d), im = byte_mask(kk, d);
+        const uint32_t sv = align8(c.val[d], pv, 3), sc = align8(c.cnt[d], pc, 3);
+        pv = c.val[d]; pc = c.cnt[d];
+        const uint32_t nv = (c.val[d] & bm) | (sv & ~bm & ~im) | ((v * 0x01010101u) & im);
+        const uint32_t nc = (c.cnt[d] & bm) | (sc & ~bm & ~im) | ((kSubDelta * 0x01010101u) & im);
+        c.val[d] = en ? nv : c.val[d];
+        c.cnt[d] = en ? nc : c.cnt[d];
+    }
+    if (links) {
+        uint32_t pl = 0u;
+#pragma unroll
+        for (uint32_t d = 0; d < 2 * NV; ++d) {
+            const int kk2 = kk - 2 * static_cast<int>(d);
+            const uint32_t bm = kk2 <= 0 ? 0u : (kk2 >= 2 ? 0xFFFFFFFFu : 0xFFFFu);
+            const uint32_t im = kk2 == 0 ? 0xFFFFu : (kk2 == 1 ? 0xFFFF0000u : 0u);
+            const uint32_t sl = align8(c.lnk[d], pl, 2);
+            pl = c.lnk[d];
+            const uint32_t nl = (c.lnk[d] & bm) | (sl & ~bm & ~im) | ((link * 0x00010001u) & im);
+            c.lnk[d] = en ? nl : c.lnk[d];
+        }
+    }
+}
+
+// compress.c:90-112 where `en`
+template <uint32_t NV>
+DEV void ctx_rescale(uint8_t* reg, Ctx<NV>& c, bool en)
+{
+    if (!any_lane(en)) return;
     uint32_t sum = 0;
-    const uint32_t ilen = r.ext == 0 ? r.len : 0u;
 #pragma unroll
-    for (uint32_t t = 0; t < INL; ++t) {
-        const uint32_t e = r.e[t];
-        const bool in = t < ilen;
-        const uint32_t c = in ? cnt_of(e) : 0u;
-        const bool lt = in && val_of(e) < v;
-        const bool eq = in && val_of(e) == v;
-        sum += c;
-        h.under += lt ? c : 0u;
-        h.k += lt ? 1u : 0u;
-        h.found = h.found || eq;
-        h.cnt = eq ? c : h.cnt;
-        h.link = eq ? (e >> 16) : h.link;
+    for (uint32_t d = 0; d < NV; ++d) {
+        const uint32_t h = c.cnt[d] - ((c.cnt[d] >> 1) & 0x7F7F7F7Fu);
+        c.cnt[d] = en ? h : c.cnt[d];
+        sum = sad(h, sum);
     }
-    if (any_lane(r.ext != 0)) {
-        if (r.ext != 0) {
-            const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-            for (uint32_t g0 = 0; g0 < r.len; g0 += kGrp) {
-                uint4 q[4];
-                grp_load(ep, g0, r.len, q);
+    if (any_lane(en && c.dense != 0)) {
+        if (en && c.dense != 0) sum = dense_rescale(reg + c.ext);
+    }
+    c.esc -= en ? (c.esc >> 1) : 0u;
+    c.tot = en ? ((c.esc + sum) & 0xFFFF) : c.tot;
+}
+
+// compress.c:293-314 (and the decoder's patch, :598-615) where `en`: bump
+// v or insert it.  ALLOC (order-1 contexts): a new symbol gets a fresh o2
+// record, whose index becomes its link.  Returns the lookup (old count).
+template <uint32_t NV, bool ALLOC>
+DEV Look<NV> ctx_update(uint8_t* reg, Ctx<NV>& c, uint32_t v, uint32_t& bump, uint32_t end,
+                        uint32_t& nodes, uint32_t& dense_left, bool& ovf, bool en)
+{
+    Look<NV> h = ctx_find<NV>(reg, c, v, ALLOC);
+    const bool ins = en && !h.found;
+    uint32_t newlink = h.link;
+    if (ALLOC) {
+        const uint32_t at = bump;
+        newlink = ins ? at / kO2Rec : h.link;
+        bump += ins ? kO2Rec : 0u;
+        ovf = ovf || (ins && bump > end);
+    }
+    const bool inl = c.dense == 0;
+    // inline bump
 #pragma unroll
-                for (uint32_t t = 0; t < kGrp; ++t) {
-                    const uint32_t e = grp_get(q, t);
-                    const bool in = g0 + t < r.len;
-                    const uint32_t c = in ? cnt_of(e) : 0u;
-                    const bool lt = in && val_of(e) < v;
-                    const bool eq = in && val_of(e) == v;
-                    sum += c;
-                    h.under += lt ? c : 0u;
-                    h.k += lt ? 1u : 0u;
-                    h.found = h.found || eq;
-                    h.cnt = eq ? c : h.cnt;
-                    h.link = eq ? (e >> 16) : h.link;
-                }
+    for (uint32_t d = 0; d < NV; ++d) c.cnt[d] += (en && h.found && inl) ? (h.eq[d] << 1) : 0u;
+    // inline insert with room
+    const uint32_t cap = 4u * NV;
+    inline_insert<NV>(c, h.k, v, newlink, ALLOC, ins && inl && c.len < cap);
+    // full inline context -> dense; dense bump / insert
+    const bool grow = ins && inl && c.len >= cap;
+    if (any_lane(grow || (en && !inl))) {
+        if (grow) {
+            const bool ok = dense_left > 0 && densify<NV>(reg, c, bump, end, ALLOC, true);
+            dense_left -= ok ? 1u : 0u;
+            ovf = ovf || !ok;
+            if (ok) {
+                uint32_t u, n;
+                dense_find(reg + c.ext, v, ALLOC, h.z, u, n);
             }
         }
+        if (en && c.dense != 0 && !ovf) {
+            dense_add(reg + c.ext, v, kSubDelta, h.z);
+            if (ALLOC && ins) reinterpret_cast<uint16_t*>(reg + c.ext + 288)[v] = static_cast<uint16_t>(newlink);
+        }
     }
-    (void) sum;
-    h.tot = r.tot;
+    h.link = newlink;
+    c.len += ins ? 1u : 0u;
+    nodes += ins ? 1u : 0u;
+    c.esc += ins ? kSubEscDelta : 0u;
+    const uint32_t tot = (c.tot + (ins ? kSubEscDelta : 0u) + kSubDelta) & 0xFFFF;
+    c.tot = en ? tot : c.tot;
+    ctx_rescale<NV>(reg, c, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
     return h;
 }
 
-template <uint32_t INL>
-DEV uint32_t rec_total(const uint8_t*, const Rec<INL>& r) { return r.tot; }
-
-// Decoder search (compress.c:373-416, minimum 0) where `en`: entry whose
-// interval holds code.  Returns false (corrupt stream) when none does.
-template <uint32_t INL>
-DEV Hit rec_search(const uint8_t* reg, const Rec<INL>& r, uint32_t code, bool en)
+// Decoder: the symbol whose interval [under, under + count) holds code
+// (minimum 0), by halving on byte sums of the sorted counts
+template <uint32_t NV>
+DEV bool ctx_search(const uint8_t* reg, const Ctx<NV>& c, uint32_t code, bool links, Look<NV>& h, uint32_t& v)
 {
-    Hit h = { 0u, 0u, 0u, 0u, 0u, 0u, false };
-    uint32_t cum = 0;
-    bool found = false;
-    const uint32_t ilen = (en && r.ext == 0) ? r.len : 0u;
-#pragma unroll
-    for (uint32_t t = 0; t < INL; ++t) {
-        const uint32_t e = r.e[t];
-        const bool in = t < ilen;
-        const uint32_t c = in ? cnt_of(e) : 0u;
-        const bool hit = in && !found && code < cum + c;
-        h.k = hit ? t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
-        h.link = hit ? (e >> 16) : h.link; h.val = hit ? val_of(e) : h.val;
-        found = found || hit;
-        cum += c;
+    const uint32_t c0 = c.cnt[0], c1 = c.cnt[1], c2 = NV > 2 ? c.cnt[NV > 2 ? 2 : 0] : 0u, c3 = 0u;
+    const uint32_t v0 = c.val[0], v1 = c.val[1], v2 = NV > 2 ? c.val[NV > 2 ? 2 : 0] : 0xFFFFFFFFu;
+    uint32_t base = 0, j = 0, wa, wb, va, vb;
+    if (NV > 2) {
+        const uint32_t s = sad(c0, sad(c1, 0u));
+        const bool hi = code >= s;
+        base = hi ? s : 0u; j = hi ? 8u : 0u;
+        wa = hi ? c2 : c0; wb = hi ? c3 : c1;
+        va = hi ? v2 : v0; vb = hi ? 0xFFFFFFFFu : v1;
+    } else {
+        wa = c0; wb = c1; va = v0; vb = v1;
     }
-    if (any_lane(en && r.ext != 0)) {
-        if (en && r.ext != 0) {
-            const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-            for (uint32_t g0 = 0; g0 < r.len && !found; g0 += kGrp) {
-                uint4 q[4];
-                grp_load(ep, g0, r.len, q);
+    uint32_t s = sad(wa, 0u);
+    bool hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 4u : 0u;
+    uint32_t w = hi ? wb : wa, vw = hi ? vb : va;
+    s = sad(w & 0xFFFFu, 0u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 2u : 0u;
+    w = hi ? (w >> 16) : w; vw = hi ? (vw >> 16) : vw;
+    s = w & 0xFFu;
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 1u : 0u;
+    w = hi ? (w >> 8) : w; vw = hi ? (vw >> 8) : vw;
+    h.k = j; h.under = base; h.cnt = w & 0xFFu; v = vw & 0xFFu;
+    bool ok = h.cnt != 0 && code < base + h.cnt;
+    h.link = links ? lnk_get<NV>(c, j) : 0u;
 #pragma unroll
-                for (uint32_t t = 0; t < kGrp; ++t) {
-                    const uint32_t e = grp_get(q, t);
-                    const bool in = g0 + t < r.len;
-                    const uint32_t c = in ? cnt_of(e) : 0u;
-                    const bool hit = in && !found && code < cum + c;
-                    h.k = hit ? g0 + t : h.k; h.under = hit ? cum : h.under; h.cnt = hit ? c : h.cnt;
-                    h.link = hit ? (e >> 16) : h.link; h.val = hit ? val_of(e) : h.val;
-                    found = found || hit;
-                    cum += c;
-                }
-            }
+    for (uint32_t d = 0; d < NV; ++d) h.eq[d] = byte_mask(static_cast<int>(j), d) & 0x01010101u;
+    if (any_lane(c.dense != 0)) {
+        if (c.dense != 0) {
+            uint32_t u, n, vv;
+            ok = dense_search(reg + c.ext, code, links, h.z, vv, u, n);
+            h.under = u; h.cnt = n; v = vv; h.link = h.z.link;
         }
     }
-    h.found = found;
-    return h;
-}
-
-// count[k] = cnt + d where `en`
-template <uint32_t INL>
-DEV void rec_bump(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t cnt, uint32_t d, bool en)
-{
-    const bool inl = en && r.ext == 0;
-#pragma unroll
-    for (uint32_t t = 0; t < INL; ++t) r.e[t] += (inl && t == k) ? (d << 8) : 0u;
-    if (any_lane(en && r.ext != 0)) {
-        if (en && r.ext != 0) reg[r.ext + 4 * k + 1] = static_cast<uint8_t>(cnt + d);
-    }
-}
-
-DEV void grp_put(uint4 (&o)[4], uint32_t i, uint32_t x)
-{
-    uint4& c = o[i >> 2];
-    switch (i & 3) { case 0: c.x = x; break; case 1: c.y = x; break; case 2: c.z = x; break; default: c.w = x; }
-}
-
-// dst[j], j in [0, n]: src[j] below k, ne at k, src[j-1] above k (src holds n
-// entries; the block holding dst has room for n + 1, rounded up to 4).  In
-// place (dst == src) the groups below k are not touched.  A group's stores
-// never reach the next group's entries, so they can precede its loads.
-DEV void ext_shift_insert(uint32_t* dst, const uint32_t* src, uint32_t n, uint32_t k, uint32_t ne, bool inplace)
-{
-    uint32_t carry = 0;
-    for (uint32_t g0 = inplace ? (k & ~(kGrp - 1)) : 0u; g0 <= n; g0 += kGrp) {
-        uint4 q[4], o[4];
-        grp_load(src, g0, n, q);
-#pragma unroll
-        for (uint32_t t = 0; t < kGrp; ++t) {
-            const uint32_t j = g0 + t;
-            const uint32_t prev = t == 0 ? carry : grp_get(q, t - 1);
-            grp_put(o, t, j < k ? grp_get(q, t) : (j == k ? ne : prev));
-        }
-        carry = grp_get(q, kGrp - 1);
-#pragma unroll
-        for (uint32_t c = 0; c < 4; ++c)
-            if (g0 + 4 * c <= n) *reinterpret_cast<uint4*>(dst + g0 + 4 * c) = o[c];
-    }
-}
-
-// Insert entry `ne` at position k where `en`; moves to / grows an extension
-// block when the inline slots or the block are full.  false = region full.
-template <uint32_t INL, uint32_t MINCAP>
-DEV bool rec_insert(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t ne, uint32_t& bump, uint32_t end, bool en)
-{
-    const bool fast = en && r.ext == 0 && r.len < INL;
-#pragma unroll
-    for (int t = INL - 1; t >= 0; --t) {
-        const uint32_t prev = t > 0 ? r.e[t > 0 ? t - 1 : 0] : 0u;
-        const uint32_t shifted = (static_cast<uint32_t>(t) > k) ? prev
-                               : (static_cast<uint32_t>(t) == k ? ne : r.e[t]);
-        r.e[t] = fast ? shifted : r.e[t];
-    }
-    bool ok = true;
-    if (any_lane(en && !fast)) {
-        if (en && !fast) {
-            const uint32_t cap = r.ext ? cap_for(r.len, MINCAP) : INL;
-            if (r.ext != 0 && r.len < cap) {
-                uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
-                ext_shift_insert(ep, ep, r.len, k, ne, true);
-            } else {
-                const uint32_t ncap = r.ext ? 2 * cap : MINCAP;
-                const uint32_t at = (bump + 15) & ~15u;
-                if (at + 4 * ncap > end) {
-                    ok = false;
-                } else {
-                    uint32_t* np = reinterpret_cast<uint32_t*>(reg + at);
-                    if (r.ext == 0) {
-#pragma unroll
-                        for (uint32_t t = 0; t < INL; ++t) np[t + (t >= k ? 1u : 0u)] = r.e[t];
-                        np[k] = ne;
-                    } else {
-                        const uint32_t* ep = reinterpret_cast<const uint32_t*>(reg + r.ext);
-                        ext_shift_insert(np, ep, r.len, k, ne, false);
-                    }
-                    r.ext = at;
-                    bump = at + 4 * ncap;
-                }
-            }
-        }
-    }
-    r.len += (en && ok) ? 1u : 0u;
+    h.found = ok;
     return ok;
 }
 
-// Link of entry k where `en` (an o2 entry created before its suffix context was known).
-template <uint32_t INL>
-DEV void rec_set_link(uint8_t* reg, Rec<INL>& r, uint32_t k, uint32_t link, bool en)
+// decoder hit at a sub-context: count[v] += 2, total += 2, rescale (compress.c:559-568)
+template <uint32_t NV>
+DEV void ctx_hit(uint8_t* reg, Ctx<NV>& c, Look<NV>& h, uint32_t v)
 {
-    const bool inl = en && r.ext == 0;
+    if (c.dense == 0) {
 #pragma unroll
-    for (uint32_t t = 0; t < INL; ++t)
-        r.e[t] = (inl && t == k) ? ((r.e[t] & 0xFFFFu) | (link << 16)) : r.e[t];
-    if (any_lane(en && r.ext != 0)) {
-        if (en && r.ext != 0) *reinterpret_cast<uint16_t*>(reg + r.ext + 4 * k + 2) = static_cast<uint16_t>(link);
+        for (uint32_t d = 0; d < NV; ++d) c.cnt[d] += h.eq[d] << 1;
     }
-}
-
-// compress.c:90-112 on a record, where `en`
-template <uint32_t INL>
-DEV void rec_rescale(uint8_t* reg, Rec<INL>& r, bool en)
-{
-    if (!any_lane(en)) return;
-    const bool inl = en && r.ext == 0;
-    uint32_t sum = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < INL; ++t) {
-        const uint32_t e = r.e[t];
-        uint32_t c = cnt_of(e);
-        c -= c >> 1;
-        const bool live = inl && t < r.len;
-        r.e[t] = live ? ((e & 0xFFFF00FFu) | (c << 8)) : e;
-        sum += live ? c : 0u;
+    if (any_lane(c.dense != 0)) {
+        if (c.dense != 0) dense_add(reg + c.ext, v, kSubDelta, h.z);
     }
-    if (en && r.ext != 0) {
-        uint32_t* ep = reinterpret_cast<uint32_t*>(reg + r.ext);
-        for (uint32_t g0 = 0; g0 < r.len; g0 += kGrp) {
-            uint4 q[4];
-            grp_load(ep, g0, r.len, q);
-#pragma unroll
-            for (uint32_t t = 0; t < kGrp; ++t) {
-                const uint32_t e = grp_get(q, t);
-                const uint32_t c = cnt_of(e) - (cnt_of(e) >> 1);
-                grp_put(q, t, (e & 0xFFFF00FFu) | (c << 8));
-                sum += g0 + t < r.len ? c : 0u;
-            }
-#pragma unroll
-            for (uint32_t c = 0; c < 4; ++c)
-                if (g0 + 4 * c < r.len) *reinterpret_cast<uint4*>(ep + g0 + 4 * c) = q[c];
-        }
-    }
-    r.esc -= en ? (r.esc >> 1) : 0u;
-    r.tot = en ? ((r.esc + sum) & 0xFFFF) : r.tot;                  // compress.c:107-112
-}
-
-// Encoder-side update of a sub-context where `en` (compress.c:293-314, patch
-// :603-613): find or insert v.  Returns the hit: old count (0 if new), cum
-// below, total before the update, and the entry's link.  ALLOC: an inserted
-// entry gets a fresh o2 record (order-1 contexts); otherwise its link is set
-// later with rec_set_link (order-2 contexts).
-template <uint32_t INL, uint32_t MINCAP, bool ALLOC>
-DEV Hit sub_update(uint8_t* reg, Rec<INL>& r, uint32_t v, uint32_t& bump,
-                   uint32_t end, uint32_t& nodes, bool& ovf, bool en)
-{
-    Hit h = rec_find(reg, r, v);
-    const bool ins = en && !h.found;
-    rec_bump(reg, r, h.k, h.cnt, kSubDelta, en && h.found);
-    uint32_t newlink = 0;
-    if (ALLOC) {
-        newlink = bump / kO2Rec;
-        bump += ins ? kO2Rec : 0u;
-        if (ins && bump > end) ovf = true;
-    }
-    const bool ok = rec_insert<INL, MINCAP>(reg, r, h.k, v | (kSubDelta << 8) | (newlink << 16),
-                                            bump, end, ins);
-    ovf = ovf || !ok;
-    h.link = ins ? newlink : h.link;
-    nodes += ins ? 1u : 0u;
-    r.esc += ins ? kSubEscDelta : 0u;
-    const uint32_t tot = (h.tot + (ins ? kSubEscDelta : 0u) + kSubDelta) & 0xFFFF;
-    r.tot = en ? tot : r.tot;
-    rec_rescale(reg, r, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
-    return h;
-}
-
-DEV void region_reset(uint8_t* reg, uint8_t* root)
-{
-    root_clear(root);
-    for (uint32_t x = 0; x < 256; ++x) *reinterpret_cast<uint2*>(reg + x * kO1Rec) = make_uint2(0u, 0u);
+    const uint32_t tot = (c.tot + kSubDelta) & 0xFFFF;
+    c.tot = tot;
+    ctx_rescale<NV>(reg, c, h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit);
 }
 
 // ------------------------------------------------------- byte streams (HBM)
@@ -736,14 +868,22 @@ DEV void flag_exact(const rc_workspace_dev& ws, uint32_t pkt)
     ws.flag_list[slot] = pkt;
 }
 
-DEV void rec_clear(Rec<kO1Inl>& r1)
-{
-    r1.off = 0; r1.esc = 0; r1.len = 0; r1.ext = 0; r1.tot = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < kO1Inl; ++t) r1.e[t] = 0;
-}
-
 // ------------------------------------------------------------ one packet
+
+// next epoch of the lane's region (a packet start or a model reset); on wrap
+// the o1 tags are cleared so that no stale record can match again
+DEV uint32_t next_epoch(uint8_t* reg, uint32_t e)
+{
+    e += 1;
+    if (any_lane((e & 0xFFFF) == 0)) {
+        if ((e & 0xFFFF) == 0) {
+            for (uint32_t x = 0; x < 256; ++x) *reinterpret_cast<uint32_t*>(reg + kO1Base + x * kO1Rec) = 0u;
+            e += 1;
+        }
+    }
+    *reinterpret_cast<uint32_t*>(reg) = e;
+    return e;
+}
 
 DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t pkt,
                       uint8_t* reg, uint8_t* root)
@@ -756,59 +896,57 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     OutWin o = { b.out + b.out_off[pkt], cap, 0u, make_uint4(0u, 0u, 0u, 0u) };
     const uint32_t end = ws.lane_region;
 
-    region_reset(reg, root);
-    uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1;
+    uint32_t epoch = next_epoch(reg, *reinterpret_cast<const uint32_t*>(reg));
+    root_clear(root);
+    uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1, dense_left = kDenseBudget;
     uint32_t order = 0, b1 = 0;
     uint32_t low = 0, range = ~0u;
     bool ok = true, ovf = false;
     // software pipeline: the records of step i+1 are loaded during step i
     // (the next order-1 context is the current byte, known at the top of the
-    // step; the next order-2 context once the current contexts are resolved).
-    Rec<kO1Inl> r1;
-    Rec<kO2Inl> r2;
-    o2_fresh(0, r2);
-    rec_clear(r1);
+    // step; the next order-2 record once the order-1 lookup is done).
+    Ctx1 r1;
+    Ctx2 r2;
+    ctx_empty(r1, kO1Base, epoch & 0xFFFF);
+    ctx_empty(r2, 0u, 0u);
 
     PROF_DECL
     for (uint32_t i = 0; i < len; ++i) {
 #ifdef RC_PROFILE_DRAIN
-        __builtin_amdgcn_s_waitcnt(0);       // diagnostic: charge outstanding memory to slot 9
+        __builtin_amdgcn_s_waitcnt(0);
         PROF(9)
 #endif
         const uint32_t v = inwin_take(in, true);
-        Rec<kO1Inl> n1;
-        o1_load(reg, v, n1);                                         // next step's order-1 record
-        Rec<kO2Inl> n2;
+        Ctx1 n1;
+        o1_load(reg, v, epoch & 0xFFFF, n1);                       // next step's order-1 record
+        Ctx2 n2;
         const bool en2 = order >= 2;
         PROF(0)
 
         // order 2, compress.c:286-316
-        const uint32_t esc2 = r2.esc;
-        const Hit h2 = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, en2);
+        const uint32_t esc2 = r2.esc, tot2 = r2.tot;
+        const Look<kO2NV> h2 = ctx_update<kO2NV, false>(reg, r2, v, bump, end, nodes, dense_left, ovf, en2);
         const bool done2 = en2 && h2.found;
         PROF(1)
-        enc_code(low, range, done2 ? esc2 + h2.under : 0u, done2 ? h2.cnt : esc2, h2.tot, o,
-                 done2 || (en2 && esc2 > 0 && esc2 < h2.tot), ok);
+        enc_code(low, range, done2 ? esc2 + h2.under : 0u, done2 ? h2.cnt : esc2, tot2, o,
+                 done2 || (en2 && esc2 > 0 && esc2 < tot2), ok);
         PROF(2)
-        const bool pend = en2 && !h2.found;
-        uint32_t nxt = h2.link;
 
-        // order 1
+        // order 1 (its lookup also yields the next order-2 record: the link of v)
         const bool en1 = !done2 && order >= 1;
-        const uint32_t esc1 = r1.esc;
-        const Hit h1 = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf, en1);
+        const uint32_t esc1 = r1.esc, tot1 = r1.tot;
+        const Look<kO1NV> h1 = ctx_update<kO1NV, true>(reg, r1, v, bump, end, nodes, dense_left, ovf, en1);
         const bool done1 = en1 && h1.found;
-        nxt = en1 ? h1.link : nxt;
+        const uint32_t nxt = h1.link;
         const bool nfresh = en1 && !h1.found;
-        rec_set_link(reg, r2, h2.k, nxt, pend);
         PROF(3)
-        enc_code(low, range, done1 ? esc1 + h1.under : 0u, done1 ? h1.cnt : esc1, h1.tot, o,
-                 done1 || (en1 && esc1 > 0 && esc1 < h1.tot), ok);
+        enc_code(low, range, done1 ? esc1 + h1.under : 0u, done1 ? h1.cnt : esc1, tot1, o,
+                 done1 || (en1 && esc1 > 0 && esc1 < tot1), ok);
         PROF(4)
 
         // next order-2 record: fresh, the one just updated, or a load
         const bool same2 = en2 && nxt * kO2Rec == r2.off;
-        o2_fresh(0, n2);
+        ctx_empty(n2, nxt * kO2Rec, 0u);
         if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
         if (en1) o1_store(reg, r1);
         if (en2) o2_store(reg, r2);
@@ -831,8 +969,7 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
 
         // advance, compress.c:331-336
         if (order >= 1) {
-            if (nfresh) o2_fresh(nxt, n2);
-            else if (same2) n2 = r2;
+            if (same2) n2 = r2;
             r2 = n2;
         }
         // the prefetched order-1 record is stale when it is the one this step updated
@@ -841,8 +978,9 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         b1 = v;
         if (any_lane(nodes >= kMaxNodes)) {                          // compress.c:148-157
             if (nodes >= kMaxNodes) {
-                region_reset(reg, root);
-                rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0;
+                epoch = next_epoch(reg, epoch);
+                root_clear(root);
+                rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0; dense_left = kDenseBudget;
             }
         }
         PROF(8)
@@ -861,11 +999,6 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     b.out_len[pkt] = ok ? o.n : 0u;
 }
 
-DEV void rec2_copy(Rec<kO2Inl>& d, const Rec<kO2Inl>& r)
-{
-    d.off = r.off; d.esc = r.esc; d.len = r.len; d.ext = r.ext; d.tot = r.tot; d.e[0] = r.e[0]; d.e[1] = r.e[1];
-}
-
 // The decoder keeps data-dependent branches: unlike the encoder, each level's
 // work (two divisions, a search) is only needed by the lanes that reach it.
 DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t pkt,
@@ -879,23 +1012,24 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
     InWin in;
     inwin_init(in, b.in + b.in_off[pkt], len);
 
-    region_reset(reg, root);
-    uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1;
+    uint32_t epoch = next_epoch(reg, *reinterpret_cast<const uint32_t*>(reg));
+    root_clear(root);
+    uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1, dense_left = kDenseBudget;
     uint32_t order = 0, b1 = 0;
     uint32_t low = 0, code = 0, range = ~0u;
     for (int k = 0; k < 4; ++k) code = (code << 8) | inwin_take(in, true);   // compress.c:344-350
     bool fail = false, anomaly = false, ovf = false;
     // the next step's records are loaded as soon as the symbol is decoded
-    Rec<kO1Inl> r1;
-    Rec<kO2Inl> r2;
-    o2_fresh(0, r2);
-    rec_clear(r1);
+    Ctx1 r1;
+    Ctx2 r2;
+    ctx_empty(r1, kO1Base, epoch & 0xFFFF);
+    ctx_empty(r2, 0u, 0u);
 
     PROF_DECL
     for (;;) {
         PROF(11)
 #ifdef RC_PROFILE_DRAIN
-        __builtin_amdgcn_s_waitcnt(0);       // diagnostic: charge outstanding memory to slot 8
+        __builtin_amdgcn_s_waitcnt(0);
         PROF(8)
 #endif
         int at = -1;                         // context that produced the symbol (2, 1, 0)
@@ -903,41 +1037,34 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         bool nfresh = false;
 
         if (order >= 2 && r2.esc > 0) {                              // compress.c:529-568
-            const uint32_t tot = rec_total(reg, r2);
+            const uint32_t tot = r2.tot;
             if (r2.esc < tot) {
                 range = udiv(range, tot);
                 uint32_t cd = udiv(code - low, range) & 0xFFFF;
                 if (cd < r2.esc) {
                     dec_code(low, code, range, 0, r2.esc, in, true);
                 } else {
-                    const Hit h = rec_search(reg, r2, cd - r2.esc, true);
-                    if (!h.found) { fail = true; break; }
-                    v = h.val;
-                    rec_bump(reg, r2, h.k, h.cnt, kSubDelta, true);
+                    Look<kO2NV> h;
+                    if (!ctx_search<kO2NV>(reg, r2, cd - r2.esc, false, h, v)) { fail = true; break; }
                     dec_code(low, code, range, r2.esc + h.under, h.cnt, in, true);
-                    r2.tot = (tot + kSubDelta) & 0xFFFF;
-                    rec_rescale(reg, r2, h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit);
-                    nxt = h.link;
+                    ctx_hit<kO2NV>(reg, r2, h, v);
                     at = 2;
                 }
             }
         }
         PROF(0)
         if (at < 0 && order >= 1 && r1.esc > 0) {
-            const uint32_t tot = rec_total(reg, r1);
+            const uint32_t tot = r1.tot;
             if (r1.esc < tot) {
                 range = udiv(range, tot);
                 uint32_t cd = udiv(code - low, range) & 0xFFFF;
                 if (cd < r1.esc) {
                     dec_code(low, code, range, 0, r1.esc, in, true);
                 } else {
-                    const Hit h = rec_search(reg, r1, cd - r1.esc, true);
-                    if (!h.found) { fail = true; break; }
-                    v = h.val;
-                    rec_bump(reg, r1, h.k, h.cnt, kSubDelta, true);
+                    Look<kO1NV> h;
+                    if (!ctx_search<kO1NV>(reg, r1, cd - r1.esc, true, h, v)) { fail = true; break; }
                     dec_code(low, code, range, r1.esc + h.under, h.cnt, in, true);
-                    r1.tot = (tot + kSubDelta) & 0xFFFF;
-                    rec_rescale(reg, r1, h.cnt > 0xFF - 2 * kSubDelta || tot + kSubDelta > kTotalLimit);
+                    ctx_hit<kO1NV>(reg, r1, h, v);
                     nxt = h.link;
                     at = 1;
                 }
@@ -960,28 +1087,25 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
             at = 0;
         }
         PROF(2)
-        Rec<kO1Inl> n1;
-        o1_load(reg, v, n1);                                         // next step's order-1 record
-        // patch the contexts above, compress.c:598-615
-        bool pend = false;
-        uint32_t kpend = 0;
+        Ctx1 n1;
+        o1_load(reg, v, epoch & 0xFFFF, n1);                       // next step's order-1 record
         PROF(3)
+        // patch the contexts above, compress.c:598-615
         if (order >= 2 && at < 2) {
-            const Hit h = sub_update<kO2Inl, kO2MinCap, false>(reg, r2, v, bump, end, nodes, ovf, true);
+            ctx_update<kO2NV, false>(reg, r2, v, bump, end, nodes, dense_left, ovf, true);
             if (ovf) break;
-            if (!h.found) { pend = true; kpend = h.k; }
         }
         PROF(4)
         if (order >= 1 && at < 1) {
-            const Hit h = sub_update<kO1Inl, kO1MinCap, true>(reg, r1, v, bump, end, nodes, ovf, true);
+            const Look<kO1NV> h = ctx_update<kO1NV, true>(reg, r1, v, bump, end, nodes, dense_left, ovf, true);
             if (ovf) break;
             nxt = h.link;
             nfresh = !h.found;
         }
-        rec_set_link(reg, r2, kpend, nxt, pend);
+        if (order >= 1 && at == 2) nxt = ctx_find<kO1NV>(reg, r1, v, true).link;   // (prev, v) via o1[prev]
         PROF(5)
-        Rec<kO2Inl> n2;
-        o2_fresh(nxt, n2);
+        Ctx2 n2;
+        ctx_empty(n2, nxt * kO2Rec, 0u);
         const bool same2 = order >= 2 && nxt * kO2Rec == r2.off;
         if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
         if (order >= 2) o2_store(reg, r2);
@@ -990,14 +1114,15 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
         outwin_put(o, v, true);
         PROF(7)
-        if (order >= 1 && !same2) rec2_copy(r2, n2);
+        if (order >= 1 && !same2) r2 = n2;
         if (!(order >= 1 && v == b1)) r1 = n1;
         if (order < 2) ++order;
         b1 = v;
         if (any_lane(nodes >= kMaxNodes)) {
             if (nodes >= kMaxNodes) {
-                region_reset(reg, root);
-                rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0;
+                epoch = next_epoch(reg, epoch);
+                root_clear(root);
+                rtot = 1 + 256; bump = kArenaBase; nodes = 1; order = 0; dense_left = kDenseBudget;
             }
         }
     }
@@ -1025,11 +1150,13 @@ extern "C" int rc_lane_prof_read(unsigned long long* out, int reset)
 
 extern "C" uint32_t rc_hip_lane_region_bytes(uint32_t max_len)
 {
-    // order-1 table + one 8-B order-2 record per byte + extension blocks
-    // (< 16 B per model node over their lifetime; <= 4094 nodes between resets)
+    // header + order-1 table + one 32-B order-2 record per o1 symbol (<= one
+    // per byte between resets) + dense blocks: a dense context holds > 8
+    // symbols, i.e. > 8 of the <= 2L + 256 (<= 4094) nodes between resets,
+    // and takes <= 800 B, so <= 89 B per node covers any input.
     const uint64_t L = max_len < 4096 ? max_len : 4096;
     const uint64_t nodes = 2 * L + 256 < 4094 ? 2 * L + 256 : 4094;
-    uint64_t bytes = kArenaBase + kO2Rec * L + 16 * nodes + 1024;
+    uint64_t bytes = kArenaBase + kO2Rec * (L + 1) + 89 * nodes + 1024;
     bytes = (bytes + 255) & ~255ull;
     return static_cast<uint32_t>(bytes);
 }

@@ -12,7 +12,10 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     static uint8_t* region = nullptr;
     static uint32_t region_bytes = 0;
     uint32_t need = rc_hip_lane_region_bytes(max_len);
-    if (need > region_bytes) { free(region); region = (uint8_t*) aligned_alloc(256, need); region_bytes = need; }
+    if (need > region_bytes) {
+        free(region); region = (uint8_t*) aligned_alloc(256, need); region_bytes = need;
+        memset(region, 0, need);                                   // like the device pool (epoch 0 = unused)
+    }
     uint64_t ioff = 0, ooff = 0;
     uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0};
     rc_batch_dev b = { in, &ioff, &len, out, &ooff, &cap, out_len, 1, max_len };
