@@ -264,20 +264,30 @@ DEV void ctx_empty(Ctx<NV>& c, uint32_t off, uint32_t tag)
     for (uint32_t d = 0; d < 2 * NV; ++d) c.lnk[d] = 0u;
 }
 
-DEV void o1_load(const uint8_t* reg, uint32_t x, uint32_t epoch, Ctx1& c)
+// o1 records are loaded a step ahead as raw words and decoded only when the
+// step that needs them starts: a select on loaded data placed right after the
+// load would make the wave wait for HBM there.
+struct Raw1 { uint4 q0, q1, q2, q3; uint32_t x; };
+
+DEV void o1_fetch(const uint8_t* reg, uint32_t x, Raw1& w)
 {
     const uint4* p = reinterpret_cast<const uint4*>(reg + kO1Base + x * kO1Rec);
-    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    const bool live = (q0.x & 0xFFFF) == epoch;
-    c.off = kO1Base + x * kO1Rec; c.tag = epoch;
-    c.len = live ? (q0.x >> 16) & 0xFF : 0u;
-    c.dense = live ? q0.x >> 24 : 0u;
-    c.esc = live ? q0.y & 0xFFFF : 0u;
-    c.tot = live ? q0.y >> 16 : 0u;
-    c.ext = q0.z;
-    c.val[0] = live ? q1.x : 0xFFFFFFFFu; c.val[1] = live ? q1.y : 0xFFFFFFFFu; c.val[2] = live ? q1.z : 0xFFFFFFFFu;
-    c.cnt[0] = live ? q1.w : 0u; c.cnt[1] = live ? q2.x : 0u; c.cnt[2] = live ? q2.y : 0u;
-    c.lnk[0] = q2.z; c.lnk[1] = q2.w; c.lnk[2] = q3.x; c.lnk[3] = q3.y; c.lnk[4] = q3.z; c.lnk[5] = q3.w;
+    w.q0 = p[0]; w.q1 = p[1]; w.q2 = p[2]; w.q3 = p[3]; w.x = x;
+}
+
+DEV void o1_decode(const Raw1& w, uint32_t epoch, Ctx1& c)
+{
+    const bool live = (w.q0.x & 0xFFFF) == epoch;
+    c.off = kO1Base + w.x * kO1Rec; c.tag = epoch;
+    c.len = live ? (w.q0.x >> 16) & 0xFF : 0u;
+    c.dense = live ? w.q0.x >> 24 : 0u;
+    c.esc = live ? w.q0.y & 0xFFFF : 0u;
+    c.tot = live ? w.q0.y >> 16 : 0u;
+    c.ext = w.q0.z;
+    c.val[0] = live ? w.q1.x : 0xFFFFFFFFu; c.val[1] = live ? w.q1.y : 0xFFFFFFFFu;
+    c.val[2] = live ? w.q1.z : 0xFFFFFFFFu;
+    c.cnt[0] = live ? w.q1.w : 0u; c.cnt[1] = live ? w.q2.x : 0u; c.cnt[2] = live ? w.q2.y : 0u;
+    c.lnk[0] = w.q2.z; c.lnk[1] = w.q2.w; c.lnk[2] = w.q3.x; c.lnk[3] = w.q3.y; c.lnk[4] = w.q3.z; c.lnk[5] = w.q3.w;
 }
 
 DEV void o1_store(uint8_t* reg, const Ctx1& c)
@@ -289,14 +299,20 @@ DEV void o1_store(uint8_t* reg, const Ctx1& c)
     p[3] = make_uint4(c.lnk[2], c.lnk[3], c.lnk[4], c.lnk[5]);
 }
 
-DEV void o2_load(const uint8_t* reg, uint32_t idx, Ctx2& c)
+struct Raw2 { uint4 q0, q1; };
+
+DEV void o2_fetch(const uint8_t* reg, uint32_t idx, Raw2& w)
 {
     const uint4* p = reinterpret_cast<const uint4*>(reg + idx * kO2Rec);
-    const uint4 q0 = p[0], q1 = p[1];
+    w.q0 = p[0]; w.q1 = p[1];
+}
+
+DEV void o2_decode(const Raw2& w, uint32_t idx, Ctx2& c)
+{
     c.off = idx * kO2Rec; c.tag = 0;
-    c.len = (q0.x >> 16) & 0xFF; c.dense = q0.x >> 24;
-    c.esc = q0.y & 0xFFFF; c.tot = q0.y >> 16; c.ext = q0.z;
-    c.val[0] = q1.x; c.val[1] = q1.y; c.cnt[0] = q1.z; c.cnt[1] = q1.w;
+    c.len = (w.q0.x >> 16) & 0xFF; c.dense = w.q0.x >> 24;
+    c.esc = w.q0.y & 0xFFFF; c.tot = w.q0.y >> 16; c.ext = w.q0.z;
+    c.val[0] = w.q1.x; c.val[1] = w.q1.y; c.cnt[0] = w.q1.z; c.cnt[1] = w.q1.w;
     c.lnk[0] = c.lnk[1] = c.lnk[2] = c.lnk[3] = 0u;
 }
 
@@ -917,9 +933,8 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         PROF(9)
 #endif
         const uint32_t v = inwin_take(in, true);
-        Ctx1 n1;
-        o1_load(reg, v, epoch & 0xFFFF, n1);                       // next step's order-1 record
-        Ctx2 n2;
+        Raw1 n1;
+        o1_fetch(reg, v, n1);                                       // next step's order-1 record
         const bool en2 = order >= 2;
         PROF(0)
 
@@ -946,8 +961,9 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
 
         // next order-2 record: fresh, the one just updated, or a load
         const bool same2 = en2 && nxt * kO2Rec == r2.off;
-        ctx_empty(n2, nxt * kO2Rec, 0u);
-        if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
+        const bool ld2 = order >= 1 && !nfresh && !same2;
+        Raw2 n2;
+        if (ld2) o2_fetch(reg, nxt, n2);
         if (en1) o1_store(reg, r1);
         if (en2) o2_store(reg, r2);
         PROF(5)
@@ -968,12 +984,12 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         if (any_lane(!ok || ovf)) { if (!ok || ovf) break; }
 
         // advance, compress.c:331-336
-        if (order >= 1) {
-            if (same2) n2 = r2;
-            r2 = n2;
+        if (order >= 1 && !same2) {
+            if (ld2) o2_decode(n2, nxt, r2);
+            else ctx_empty(r2, nxt * kO2Rec, 0u);
         }
         // the prefetched order-1 record is stale when it is the one this step updated
-        if (!(en1 && v == b1)) r1 = n1;
+        if (!(en1 && v == b1)) o1_decode(n1, epoch & 0xFFFF, r1);
         order += order < 2 ? 1u : 0u;
         b1 = v;
         if (any_lane(nodes >= kMaxNodes)) {                          // compress.c:148-157
@@ -1087,8 +1103,8 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
             at = 0;
         }
         PROF(2)
-        Ctx1 n1;
-        o1_load(reg, v, epoch & 0xFFFF, n1);                       // next step's order-1 record
+        Raw1 n1;
+        o1_fetch(reg, v, n1);                                       // next step's order-1 record
         PROF(3)
         // patch the contexts above, compress.c:598-615
         if (order >= 2 && at < 2) {
@@ -1104,18 +1120,21 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         }
         if (order >= 1 && at == 2) nxt = ctx_find<kO1NV>(reg, r1, v, true).link;   // (prev, v) via o1[prev]
         PROF(5)
-        Ctx2 n2;
-        ctx_empty(n2, nxt * kO2Rec, 0u);
         const bool same2 = order >= 2 && nxt * kO2Rec == r2.off;
-        if (order >= 1 && !nfresh && !same2) o2_load(reg, nxt, n2);
+        const bool ld2 = order >= 1 && !nfresh && !same2;
+        Raw2 n2;
+        if (ld2) o2_fetch(reg, nxt, n2);
         if (order >= 2) o2_store(reg, r2);
         if (order >= 1 && at <= 1) o1_store(reg, r1);
         PROF(6)
         if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
         outwin_put(o, v, true);
         PROF(7)
-        if (order >= 1 && !same2) r2 = n2;
-        if (!(order >= 1 && v == b1)) r1 = n1;
+        if (order >= 1 && !same2) {
+            if (ld2) o2_decode(n2, nxt, r2);
+            else ctx_empty(r2, nxt * kO2Rec, 0u);
+        }
+        if (!(order >= 1 && v == b1)) o1_decode(n1, epoch & 0xFFFF, r1);
         if (order < 2) ++order;
         b1 = v;
         if (any_lane(nodes >= kMaxNodes)) {
