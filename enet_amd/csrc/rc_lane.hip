@@ -147,22 +147,28 @@ DEV uint32_t root_search(const uint8_t* r, uint32_t code, uint32_t& under, uint3
         g += below ? 1u : 0u;
         prev = below ? ct : prev;
     }
+    // binary search inside the group: 8, 4, 2, 1 symbols, byte sums by SAD
+    // (each symbol also owns the root's minimum count of 1)
     const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
-    uint32_t run = 16 * g + prev, j = 15, at = run, c = 0;
-    bool found = false;
-#pragma unroll
-    for (uint32_t t = 0; t < 16; ++t) {
-        const uint32_t ct = (pick4(t >> 2, q) >> (8 * (t & 3))) & 0xFF;
-        const uint32_t nrun = run + 1 + ct;
-        const bool hit = !found && code < nrun;
-        j = hit ? t : j;
-        at = hit ? run : at;
-        c = hit ? ct : c;
-        found = found || hit;
-        run = nrun;
-    }
-    under = at;
-    cnt = c;
+    uint32_t base = 16 * g + prev, j = 0;
+    uint32_t s = sad(q.x, sad(q.y, 8u));
+    bool hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 8u : 0u;
+    const uint32_t d0 = hi ? q.z : q.x, d1 = hi ? q.w : q.y;
+    s = sad(d0, 4u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 4u : 0u;
+    uint32_t w = hi ? d1 : d0;
+    s = sad(w & 0xFFFFu, 2u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 2u : 0u;
+    w = hi ? (w >> 16) : w;
+    s = (w & 0xFFu) + 1u;
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 1u : 0u;
+    w = hi ? (w >> 8) : w;
+    under = base;
+    cnt = w & 0xFFu;
     return 16 * g + j;
 }
 
