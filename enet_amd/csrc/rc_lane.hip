@@ -34,164 +34,9 @@
 // and packets that exhaust their region are appended to the exact-path list
 // (rc_kernels.hip), which re-runs compress.c's binary-tree model.
 
-#ifndef RC_LANE_HOST_TEST
-#include <hip/hip_runtime.h>
-#else
-#include "lane_host_shim.h"   // tests/proto: host build of the per-lane logic (test only)
-#endif
-#include <stdint.h>
-
-#include "rc_abi_internal.h"
-#include "rc_udiv.h"
-
-#define DEV __device__ __forceinline__
-
-// Diagnostic build only (-DRC_PROFILE, tools/lane_prof.py): per-phase cycle
-// stamps accumulated per wave and summed into g_prof.  The product build
-// compiles every PROF_* to nothing.
-#ifdef RC_PROFILE
-__device__ unsigned long long g_prof[64];
-__device__ __forceinline__ unsigned long long prof_now()
-{
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define PROF_DECL unsigned long long prof_t = prof_now(), prof_acc[12] = {0};
-#define PROF(k) { const unsigned long long t_ = prof_now(); prof_acc[k] += t_ - prof_t; prof_t = t_; }
-#define PROF_FLUSH(base) { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 12; ++k_) atomicAdd(&g_prof[(base) + k_], prof_acc[k_]); }
-#else
-#define PROF_DECL
-#define PROF(k)
-#define PROF_FLUSH(base)
-#endif
+#include "rc_lane_common.h"
 
 namespace {
-
-constexpr uint32_t kTop = 1u << 24;          // compress.c:27
-constexpr uint32_t kBot = 1u << 16;          // compress.c:28
-constexpr uint32_t kRootDelta = 3;           // compress.c:30
-constexpr uint32_t kSubDelta = 2;            // compress.c:35
-constexpr uint32_t kSubEscDelta = 5;         // compress.c:36
-constexpr uint32_t kMaxNodes = 4096 - 2;     // compress.c:150
-constexpr uint32_t kTotalLimit = kBot - 0x100;
-
-constexpr uint32_t kRootStride = 304;        // LDS bytes per lane; 76 dwords (76/4 odd: b128 conflict-free)
-
-DEV uint32_t val_of(uint32_t e) { return e & 0xFF; }
-DEV uint32_t cnt_of(uint32_t e) { return (e >> 8) & 0xFF; }
-DEV uint32_t sad(uint32_t x, uint32_t acc) { return __builtin_amdgcn_sad_u8(x, 0u, acc); }
-DEV uint32_t pick4(uint32_t i, const uint4& q) { return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w; }
-DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
-
-// ------------------------------------------------------------ order 0 (LDS)
-
-DEV void root_clear(uint8_t* r)
-{
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int i = 0; i < 18; ++i) reinterpret_cast<uint4*>(r)[i] = z;
-}
-
-DEV uint32_t root_c(const uint8_t* r, uint32_t g) { return reinterpret_cast<const uint16_t*>(r + 256)[g]; }
-
-// under = v * 1 + sum of counts below v; cnt = count[v] (compress.c:159-199, minimum 1)
-DEV void root_lookup(const uint8_t* r, uint32_t v, uint32_t& under, uint32_t& cnt)
-{
-    const uint32_t g = v >> 4, j = v & 15;
-    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
-    const uint32_t below = g ? root_c(r, g - 1) : 0u;
-    uint32_t within = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) {
-        const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
-        const uint32_t mask = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-        within = sad(pick4(d, q) & mask, within);
-    }
-    cnt = (pick4(j >> 2, q) >> (8 * (j & 3))) & 0xFF;
-    under = v + below + within;
-}
-
-DEV void root_add(uint8_t* r, uint32_t v, uint32_t cnt)
-{
-    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
-    const uint32_t g = v >> 4;
-    uint4* cp = reinterpret_cast<uint4*>(r + 256);
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-        uint4 c = cp[h];
-        uint32_t* w = reinterpret_cast<uint32_t*>(&c);
-#pragma unroll
-        for (uint32_t d = 0; d < 4; ++d) {
-            const uint32_t g0 = 8 * h + 2 * d;
-            w[d] += (g0 >= g ? kRootDelta : 0u) | (g0 + 1 >= g ? (kRootDelta << 16) : 0u);
-        }
-        cp[h] = c;
-    }
-}
-
-// first symbol whose interval [v + C(<v), v + 1 + C(<=v)) holds code
-// (code < 256 + sum); also returns that interval's start (under) and count[v]
-DEV uint32_t root_search(const uint8_t* r, uint32_t code, uint32_t& under, uint32_t& cnt)
-{
-    const uint4 c0 = reinterpret_cast<const uint4*>(r + 256)[0];
-    const uint4 c1 = reinterpret_cast<const uint4*>(r + 256)[1];
-    uint32_t g = 0, prev = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < 16; ++t) {
-        const uint32_t w = pick4((t >> 1) & 3, t < 8 ? c0 : c1);
-        const uint32_t ct = (t & 1) ? (w >> 16) : (w & 0xFFFF);
-        const bool below = 16 * (t + 1) + ct <= code;
-        g += below ? 1u : 0u;
-        prev = below ? ct : prev;
-    }
-    // binary search inside the group: 8, 4, 2, 1 symbols, byte sums by SAD
-    // (each symbol also owns the root's minimum count of 1)
-    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
-    uint32_t base = 16 * g + prev, j = 0;
-    uint32_t s = sad(q.x, sad(q.y, 8u));
-    bool hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 8u : 0u;
-    const uint32_t d0 = hi ? q.z : q.x, d1 = hi ? q.w : q.y;
-    s = sad(d0, 4u);
-    hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 4u : 0u;
-    uint32_t w = hi ? d1 : d0;
-    s = sad(w & 0xFFFFu, 2u);
-    hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 2u : 0u;
-    w = hi ? (w >> 16) : w;
-    s = (w & 0xFFu) + 1u;
-    hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 1u : 0u;
-    w = hi ? (w >> 8) : w;
-    under = base;
-    cnt = w & 0xFFu;
-    return 16 * g + j;
-}
-
-// compress.c:90-112 for the root: halve, rebuild C, return the new total
-DEV uint32_t root_rescale(uint8_t* r)
-{
-    uint32_t sum = 0;
-    uint32_t cw[8];
-#pragma unroll
-    for (uint32_t g = 0; g < 16; ++g) {
-        uint4 q = reinterpret_cast<uint4*>(r)[g];
-        q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
-        q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
-        q.z -= (q.z >> 1) & 0x7F7F7F7Fu;
-        q.w -= (q.w >> 1) & 0x7F7F7F7Fu;
-        reinterpret_cast<uint4*>(r)[g] = q;
-        sum = sad(q.w, sad(q.z, sad(q.y, sad(q.x, sum))));
-        if (g & 1) cw[g >> 1] |= sum << 16; else cw[g >> 1] = sum;
-    }
-    reinterpret_cast<uint4*>(r + 256)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-    reinterpret_cast<uint4*>(r + 256)[1] = make_uint4(cw[4], cw[5], cw[6], cw[7]);
-    return (sum + 1 + 256) & 0xFFFF;
-}
 
 // ------------------------------------------------ order 1/2 contexts (HBM)
 // Per lane region (rc_hip_lane_region_bytes):
@@ -221,35 +66,9 @@ DEV uint32_t root_rescale(uint8_t* r)
 // o2 entries carry no links: the next o2 context (prev, v) is found through
 // o1[prev], which the step has loaded anyway.
 
-constexpr uint32_t kO1Base = 64, kO1Rec = 64, kO1NV = 3, kO2Rec = 32, kO2NV = 2;
+constexpr uint32_t kO1NV = 3, kO2Rec = 32, kO2NV = 2;
 constexpr uint32_t kArenaBase = kO1Base + 256 * kO1Rec;
-constexpr uint32_t kDenseO1 = 32 + 256 + 512, kDenseO2 = 32 + 256;
 constexpr uint32_t kDenseBudget = 0xFFFFFFFFu;   // dense blocks are bounded by the region size
-
-DEV uint32_t dot4(uint32_t a, uint32_t b, uint32_t acc) { return __builtin_amdgcn_udot4(a, b, acc, false); }
-DEV uint32_t bperm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
-DEV uint32_t align8(uint32_t hi, uint32_t lo, uint32_t n) { return __builtin_amdgcn_alignbyte(hi, lo, n); }
-
-// 0x01 in each byte of w that is >= the value behind ny (= 0x01000100 - v * 0x00010001)
-DEV uint32_t swar_ge(uint32_t w, uint32_t ny)
-{
-    const uint32_t te = bperm(0u, w, 0x0C020C00u) + ny;   // bytes 0, 2 in 16-bit halves, + 256 - v
-    const uint32_t to = bperm(0u, w, 0x0C030C01u) + ny;   // bytes 1, 3
-    return bperm(to, te, 0x07030501u);                     // the carry bytes: 1 iff byte >= v
-}
-
-// bytes [0, k) of dword d (k relative to the array start) as a mask
-DEV uint32_t below_mask(int k, int d)
-{
-    const int kk = k - 4 * d;
-    return kk <= 0 ? 0u : (kk >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kk)) - 1u));
-}
-
-DEV uint32_t byte_mask(int k, int d)
-{
-    const int kk = k - 4 * d;
-    return (kk >= 0 && kk < 4) ? (0xFFu << (8 * kk)) : 0u;
-}
 
 template <uint32_t NV>
 struct Ctx {
@@ -341,113 +160,6 @@ DEV uint32_t lnk_get(const Ctx<NV>& c, uint32_t k)
 #pragma unroll
     for (uint32_t i = 0; i < 2 * NV; ++i) w |= c.lnk[i] & (0u - static_cast<uint32_t>(d == i));
     return (w >> (16 * (k & 1))) & 0xFFFF;
-}
-
-// ---------------------------------------------------------------- dense
-// block: C[16] (u16, C[g] = counts of groups 0..g) | counts[256] | links[256] (o1)
-
-struct Dense { uint4 c0, c1, grp; uint32_t link; };
-
-DEV uint32_t dense_c(const Dense& z, uint32_t g)       // C[g]
-{
-    const uint32_t i = (g >> 1) & 3;
-    const uint32_t w = g < 8 ? pick4(i, z.c0) : pick4(i, z.c1);   // (not a select of references)
-    return (g & 1) ? (w >> 16) : (w & 0xFFFF);
-}
-
-// counts below v (minimum 0) and count[v] in a dense context; loads C, v's group and link
-DEV void dense_find(const uint8_t* blk, uint32_t v, bool links, Dense& z, uint32_t& under, uint32_t& cnt)
-{
-    const uint32_t g = v >> 4, j = v & 15;
-    const uint4* p = reinterpret_cast<const uint4*>(blk);
-    z.c0 = p[0]; z.c1 = p[1]; z.grp = p[2 + g];
-    z.link = links ? reinterpret_cast<const uint16_t*>(blk + 288)[v] : 0u;
-    uint32_t within = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) {
-        const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
-        const uint32_t mask = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-        within = sad(pick4(d, z.grp) & mask, within);
-    }
-    under = (g ? dense_c(z, g - 1) : 0u) + within;
-    cnt = (pick4(j >> 2, z.grp) >> (8 * (j & 3))) & 0xFF;
-}
-
-// count[v] += d and C[g..15] += d, given z from dense_find / dense_search for v
-DEV void dense_add(uint8_t* blk, uint32_t v, uint32_t d, Dense& z)
-{
-    const uint32_t g = v >> 4, j = v & 15, bd = d << (8 * (j & 3)), q = j >> 2;
-    z.grp.x += q == 0 ? bd : 0u; z.grp.y += q == 1 ? bd : 0u;
-    z.grp.z += q == 2 ? bd : 0u; z.grp.w += q == 3 ? bd : 0u;
-    // C[t] += d for t >= g: word i holds C[2i] | C[2i + 1] << 16
-#define RC_CADD(w, t) w += ((t) >= g ? d : 0u) | ((t) + 1 >= g ? (d << 16) : 0u)
-    RC_CADD(z.c0.x, 0u); RC_CADD(z.c0.y, 2u); RC_CADD(z.c0.z, 4u); RC_CADD(z.c0.w, 6u);
-    RC_CADD(z.c1.x, 8u); RC_CADD(z.c1.y, 10u); RC_CADD(z.c1.z, 12u); RC_CADD(z.c1.w, 14u);
-#undef RC_CADD
-    uint4* p = reinterpret_cast<uint4*>(blk);
-    p[0] = z.c0; p[1] = z.c1; p[2 + g] = z.grp;
-}
-
-// decoder: symbol whose interval [C(<v), C(<=v)) holds code (minimum 0)
-DEV bool dense_search(const uint8_t* blk, uint32_t code, bool links, Dense& z, uint32_t& v, uint32_t& under,
-                      uint32_t& cnt)
-{
-    const uint4* p = reinterpret_cast<const uint4*>(blk);
-    z.c0 = p[0]; z.c1 = p[1];
-    uint32_t g = 0, prev = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < 16; ++t) {
-        const uint32_t ct = dense_c(z, t);
-        const bool below = ct <= code;
-        g += below ? 1u : 0u;
-        prev = below ? ct : prev;
-    }
-    const bool inside = g < 16;
-    g = inside ? g : 15u;
-    z.grp = p[2 + g];
-    uint32_t base = prev, j = 0;
-    uint32_t s = sad(z.grp.x, sad(z.grp.y, 0u));
-    bool hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 8u : 0u;
-    const uint32_t d0 = hi ? z.grp.z : z.grp.x, d1 = hi ? z.grp.w : z.grp.y;
-    s = sad(d0, 0u);
-    hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 4u : 0u;
-    uint32_t w = hi ? d1 : d0;
-    s = sad(w & 0xFFFFu, 0u);
-    hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 2u : 0u;
-    w = hi ? (w >> 16) : w;
-    s = w & 0xFFu;
-    hi = code >= base + s;
-    base += hi ? s : 0u; j += hi ? 1u : 0u;
-    w = hi ? (w >> 8) : w;
-    v = 16 * g + j;
-    under = base;
-    cnt = w & 0xFFu;
-    z.link = links ? reinterpret_cast<const uint16_t*>(blk + 288)[v] : 0u;
-    return inside && cnt != 0 && code < base + cnt;
-}
-
-// compress.c:90-112 on a dense context; returns sum of the halved counts
-DEV uint32_t dense_rescale(uint8_t* blk)
-{
-    uint4* p = reinterpret_cast<uint4*>(blk);
-    uint32_t sum = 0, cw[8];
-#pragma unroll
-    for (uint32_t g = 0; g < 16; ++g) {
-        uint4 q = p[2 + g];
-        q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
-        q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
-        q.z -= (q.z >> 1) & 0x7F7F7F7Fu;
-        q.w -= (q.w >> 1) & 0x7F7F7F7Fu;
-        p[2 + g] = q;
-        sum = sad(q.w, sad(q.z, sad(q.y, sad(q.x, sum))));
-        if (g & 1) cw[g >> 1] |= sum << 16; else cw[g >> 1] = sum;
-    }
-    p[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-    p[1] = make_uint4(cw[4], cw[5], cw[6], cw[7]);
-    return sum;
 }
 
 // move an inline context to a fresh dense block (where `en`); false = arena full
@@ -695,217 +407,6 @@ DEV void ctx_hit(uint8_t* reg, Ctx<NV>& c, Look<NV>& h, uint32_t v)
     ctx_rescale<NV>(reg, c, h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit);
 }
 
-// ------------------------------------------------------- byte streams (HBM)
-// Each lane walks its own packet.  Byte-wide loads/stores would cost a 64-B
-// sector transfer per byte (a lane's line is evicted between steps under
-// 65536-way interleaving), so bytes move through 16-B register windows:
-// one aligned dwordx4 load / store per 16 bytes; packet edges fall back to
-// byte accesses so nothing outside [p, p+len) is read or written.
-
-// Byte-stream addresses are integers (alignment arithmetic); accesses through
-// them must name the global address space, otherwise they become flat_*
-// operations, which complete out of order and force vmcnt(0) waits -- a full
-// drain of every outstanding load and store, including the prefetches.
-#ifndef RC_LANE_HOST_TEST
-#define GPTR(T, a) ((__attribute__((address_space(1))) T*) (a))
-#define GPTRC(T, a) ((const __attribute__((address_space(1))) T*) (a))
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-DEV uint4 gload16(uintptr_t a) { const v4u32 v = *GPTRC(v4u32, a); return make_uint4(v.x, v.y, v.z, v.w); }
-DEV void gstore16(uintptr_t a, const uint4& w) { v4u32 v = {w.x, w.y, w.z, w.w}; *GPTR(v4u32, a) = v; }
-#else
-#define GPTR(T, a) ((T*) (a))
-#define GPTRC(T, a) ((const T*) (a))
-DEV uint4 gload16(uintptr_t a) { return *GPTRC(uint4, a); }
-DEV void gstore16(uintptr_t a, const uint4& w) { *GPTR(uint4, a) = w; }
-#endif
-
-DEV uint32_t win_get(const uint4& w, uint32_t i) { return (pick4(i >> 2, w) >> (8 * (i & 3))) & 0xFF; }
-
-DEV void win_set(uint4& w, uint32_t i, uint32_t b)
-{
-    const uint32_t sh = 8 * (i & 3), d = i >> 2, m = ~(0xFFu << sh), x = b << sh;
-    w.x = d == 0 ? ((w.x & m) | x) : w.x;
-    w.y = d == 1 ? ((w.y & m) | x) : w.y;
-    w.z = d == 2 ? ((w.z & m) | x) : w.z;
-    w.w = d == 3 ? ((w.w & m) | x) : w.w;
-}
-
-DEV uint4 chunk_load(const uint8_t* lo, const uint8_t* hi, uintptr_t c, bool en)
-{
-    const bool full = c >= reinterpret_cast<uintptr_t>(lo) && c + 16 <= reinterpret_cast<uintptr_t>(hi);
-    uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    if (en && full) w = gload16(c);
-    if (any_lane(en && !full)) {
-        if (en && !full) {
-            for (uint32_t t = 0; t < 16; ++t) {
-                const uintptr_t a = c + t;
-                if (a >= reinterpret_cast<uintptr_t>(lo) && a < reinterpret_cast<uintptr_t>(hi))
-                    win_set(w, t, *GPTRC(uint8_t, a));
-            }
-        }
-    }
-    return w;
-}
-
-// sequential reader of [p, p+len); bytes past the end read as 0 (compress.c:366-367).
-// Three 16-B chunks in flight: the chunk loaded when the reader advances is
-// first read 16 bytes later, so no step waits on it.
-struct InWin { const uint8_t* p; uint32_t len, pos; uint4 cur, nxt, fut; };
-
-DEV void inwin_init(InWin& s, const uint8_t* p, uint32_t len)
-{
-    s.p = p; s.len = len; s.pos = 0;
-    const uintptr_t c = reinterpret_cast<uintptr_t>(p) & ~static_cast<uintptr_t>(15);
-    s.cur = chunk_load(p, p + len, c, true);
-    s.nxt = chunk_load(p, p + len, c + 16, true);
-    s.fut = chunk_load(p, p + len, c + 32, true);
-    // settle these before the step loop: a load still pending at the loop
-    // header makes the compiler wait for vmcnt(0) at the top of every step
-    __builtin_amdgcn_s_waitcnt(0);   // (the builtin, which the waitcnt pass understands)
-}
-
-// next byte where `en` (0 past the end)
-DEV uint32_t inwin_take(InWin& s, bool en)
-{
-    const uintptr_t a = reinterpret_cast<uintptr_t>(s.p) + s.pos;
-    const bool live = en && s.pos < s.len;
-    const uint32_t b = live ? win_get(s.cur, a & 15) : 0u;
-    s.pos += live ? 1u : 0u;
-    const bool adv = live && (a & 15) == 15;
-    if (any_lane(adv)) {                  // advance; fetch the chunk three ahead
-        // component-wise: a select of whole vectors is lowered through scratch
-        s.cur.x = adv ? s.nxt.x : s.cur.x; s.cur.y = adv ? s.nxt.y : s.cur.y;
-        s.cur.z = adv ? s.nxt.z : s.cur.z; s.cur.w = adv ? s.nxt.w : s.cur.w;
-        s.nxt.x = adv ? s.fut.x : s.nxt.x; s.nxt.y = adv ? s.fut.y : s.nxt.y;
-        s.nxt.z = adv ? s.fut.z : s.nxt.z; s.nxt.w = adv ? s.fut.w : s.nxt.w;
-        // the load lands in `fut` directly; the rest of the step does not
-        // read it, so only this (one-in-16) step waits for it
-        const uintptr_t c = (a & ~static_cast<uintptr_t>(15)) + 48;
-        const uintptr_t lo = reinterpret_cast<uintptr_t>(s.p), hi = lo + s.len;
-        const bool full = c >= lo && c + 16 <= hi;
-        if (adv && full) s.fut = gload16(c);
-        if (any_lane(adv && !full)) {
-            if (adv && !full) s.fut = chunk_load(s.p, s.p + s.len, c, true);
-        }
-    }
-    return b;
-}
-
-struct OutWin { uint8_t* p; uint32_t cap, n; uint4 w; };
-
-DEV void outwin_edge(uint8_t* p, uint32_t n, uintptr_t c, const uint4& w)
-{
-    for (uint32_t t = 0; t < 16; ++t) {
-        const uintptr_t a = c + t;
-        if (a >= reinterpret_cast<uintptr_t>(p) && a < reinterpret_cast<uintptr_t>(p) + n)
-            *GPTR(uint8_t, a) = static_cast<uint8_t>(win_get(w, t));
-    }
-}
-
-// append a byte where `en` (caller guarantees n < cap)
-DEV void outwin_put(OutWin& o, uint32_t byte, bool en)
-{
-    const uintptr_t a = reinterpret_cast<uintptr_t>(o.p) + o.n;
-    uint4 w = o.w;
-    win_set(w, a & 15, byte);
-    o.w.x = en ? w.x : o.w.x; o.w.y = en ? w.y : o.w.y;
-    o.w.z = en ? w.z : o.w.z; o.w.w = en ? w.w : o.w.w;
-    o.n += en ? 1u : 0u;
-    const bool flush = en && (a & 15) == 15;
-    if (any_lane(flush)) {
-        const uintptr_t c = a & ~static_cast<uintptr_t>(15);
-        const bool whole = c >= reinterpret_cast<uintptr_t>(o.p);
-        if (flush && whole) gstore16(c, o.w);
-        if (any_lane(flush && !whole)) {
-            if (flush && !whole) outwin_edge(o.p, o.n, c, o.w);
-        }
-    }
-}
-
-DEV void outwin_finish(OutWin& o, bool en)
-{
-    const uintptr_t a = reinterpret_cast<uintptr_t>(o.p) + o.n - 1;
-    if (en && o.n > 0 && (a & 15) != 15) outwin_edge(o.p, o.n, a & ~static_cast<uintptr_t>(15), o.w);
-}
-
-// ------------------------------------------------------------- range coder
-
-
-// compress.c:121-137 where `en`; clears `ok` when the output is full (the
-// whole compress call then returns 0, compress.c:116-117)
-DEV void enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total,
-                  OutWin& o, bool en, bool& ok)
-{
-    en = en && ok;
-    const uint32_t r = udiv(range, en ? total : 1u);
-    low = en ? low + under * r : low;
-    range = en ? r * count : range;
-    bool more = en;
-    while (any_lane(more)) {
-        const bool carry = (low ^ (low + range)) >= kTop;
-        const bool stop = carry && range >= kBot;
-        more = more && !stop;
-        if (!any_lane(more)) break;
-        range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
-        const bool full = more && o.n >= o.cap;
-        ok = ok && !full;
-        more = more && !full;
-        outwin_put(o, low >> 24, more);
-        range = more ? range << 8 : range;
-        low = more ? low << 8 : low;
-    }
-}
-
-// compress.c:352 (truncated to u16 at :545/:575); divides range by total where `en`
-DEV uint32_t dec_read(uint32_t& range, uint32_t low, uint32_t code, uint32_t total, bool en)
-{
-    const uint32_t r = udiv(range, en ? total : 1u);
-    range = en ? r : range;
-    return udiv(code - low, en ? r : 1u) & 0xFFFF;
-}
-
-// compress.c:354-371 where `en`
-DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count,
-                  InWin& in, bool en)
-{
-    low = en ? low + under * range : low;
-    range = en ? range * count : range;
-    bool more = en;
-    while (any_lane(more)) {
-        const bool carry = (low ^ (low + range)) >= kTop;
-        const bool stop = carry && range >= kBot;
-        more = more && !stop;
-        if (!any_lane(more)) break;
-        range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
-        const uint32_t b = inwin_take(in, more);
-        code = more ? ((code << 8) | b) : code;
-        range = more ? range << 8 : range;
-        low = more ? low << 8 : low;
-    }
-}
-
-DEV void flag_exact(const rc_workspace_dev& ws, uint32_t pkt)
-{
-    const uint32_t slot = atomicAdd(&ws.counters[0], 1u);
-    ws.flag_list[slot] = pkt;
-}
-
-// ------------------------------------------------------------ one packet
-
-// next epoch of the lane's region (a packet start or a model reset); on wrap
-// the o1 tags are cleared so that no stale record can match again
-DEV uint32_t next_epoch(uint8_t* reg, uint32_t e)
-{
-    e += 1;
-    if (any_lane((e & 0xFFFF) == 0)) {
-        if ((e & 0xFFFF) == 0) {
-            for (uint32_t x = 0; x < 256; ++x) *reinterpret_cast<uint32_t*>(reg + kO1Base + x * kO1Rec) = 0u;
-            e += 1;
-        }
-    }
-    *reinterpret_cast<uint32_t*>(reg) = e;
-    return e;
-}
 
 DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t pkt,
                       uint8_t* reg, uint8_t* root)
@@ -913,9 +414,10 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
     const uint32_t len = b.in_len[pkt];
     const uint32_t cap = b.out_cap[pkt];
     if (len == 0) { b.out_len[pkt] = 0; return; }                   // compress.c:257
-    InWin in;
-    inwin_init(in, b.in + b.in_off[pkt], len);
-    OutWin o = { b.out + b.out_off[pkt], cap, 0u, make_uint4(0u, 0u, 0u, 0u) };
+    ByteSrc in;
+    src_init(in, b.in + b.in_off[pkt], len);
+    ByteSink o;
+    sink_init(o, b.out + b.out_off[pkt], cap);
     const uint32_t end = ws.lane_region;
 
     uint32_t epoch = next_epoch(reg, *reinterpret_cast<const uint32_t*>(reg));
@@ -938,7 +440,7 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         __builtin_amdgcn_s_waitcnt(0);
         PROF(9)
 #endif
-        const uint32_t v = inwin_take(in, true);
+        const uint32_t v = src_byte(in);
         Raw1 n1;
         o1_fetch(reg, v, n1);                                       // next step's order-1 record
         const bool en2 = order >= 2;
@@ -998,6 +500,7 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         if (!(en1 && v == b1)) o1_decode(n1, epoch & 0xFFFF, r1);
         order += order < 2 ? 1u : 0u;
         b1 = v;
+        src_refill(in, true);
         if (any_lane(nodes >= kMaxNodes)) {                          // compress.c:148-157
             if (nodes >= kMaxNodes) {
                 epoch = next_epoch(reg, epoch);
@@ -1014,10 +517,10 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         const bool more = ok && low != 0;
         const bool full = more && o.n >= o.cap;
         ok = ok && !full;
-        outwin_put(o, low >> 24, more && !full);
+        sink_put(o, low >> 24, 1, more && !full);
         low = (more && !full) ? low << 8 : low;
     }
-    outwin_finish(o, ok);
+    sink_finish(o, ok);
     b.out_len[pkt] = ok ? o.n : 0u;
 }
 
@@ -1029,17 +532,21 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
     const uint32_t len = b.in_len[pkt];
     const uint32_t cap = b.out_cap[pkt];
     if (len == 0) { b.out_len[pkt] = 0; return; }                   // compress.c:513
-    OutWin o = { b.out + b.out_off[pkt], cap, 0u, make_uint4(0u, 0u, 0u, 0u) };
+    ByteSink o;
+    sink_init(o, b.out + b.out_off[pkt], cap);
     const uint32_t end = ws.lane_region;
-    InWin in;
-    inwin_init(in, b.in + b.in_off[pkt], len);
+    ByteSrc in;
+    src_init(in, b.in + b.in_off[pkt], len);
 
     uint32_t epoch = next_epoch(reg, *reinterpret_cast<const uint32_t*>(reg));
     root_clear(root);
     uint32_t rtot = 1 + 256, bump = kArenaBase, nodes = 1, dense_left = kDenseBudget;
     uint32_t order = 0, b1 = 0;
     uint32_t low = 0, code = 0, range = ~0u;
-    for (int k = 0; k < 4; ++k) code = (code << 8) | inwin_take(in, true);   // compress.c:344-350
+    code = static_cast<uint32_t>(in.la >> 32);                   // compress.c:344-350 (0 past the end)
+    in.la <<= 32;
+    in.na -= 4;
+    src_refill(in, true);
     bool fail = false, anomaly = false, ovf = false;
     // the next step's records are loaded as soon as the symbol is decoded
     Ctx1 r1;
@@ -1134,7 +641,7 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         if (order >= 1 && at <= 1) o1_store(reg, r1);
         PROF(6)
         if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
-        outwin_put(o, v, true);
+        sink_put(o, v, 1, true);
         PROF(7)
         if (order >= 1 && !same2) {
             if (ld2) o2_decode(n2, nxt, r2);
@@ -1143,6 +650,7 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         if (!(order >= 1 && v == b1)) o1_decode(n1, epoch & 0xFFFF, r1);
         if (order < 2) ++order;
         b1 = v;
+        src_refill(in, true);
         if (any_lane(nodes >= kMaxNodes)) {
             if (nodes >= kMaxNodes) {
                 epoch = next_epoch(reg, epoch);
@@ -1153,7 +661,7 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
     }
     PROF_FLUSH(16)
     if (ovf || anomaly) { flag_exact(ws, pkt); return; }
-    outwin_finish(o, !fail);
+    sink_finish(o, !fail);
     b.out_len[pkt] = fail ? 0u : o.n;
 }
 
