@@ -146,7 +146,8 @@ def main():
     t_dom = t_dec if dom_is_dec else t_comp
     alg = alg_d if dom_is_dec else alg_c
     achieved = alg / t_dom / 1e9
-    kname = "rc_decompress_lane" if dom_is_dec else "rc_compress_lane"
+    kname = ("rc_decompress_" if dom_is_dec else "rc_compress_") + {"lane2": "lane", "wave": "wave"}.get(
+        os.environ.get("ENET_RC_KERNEL", ""), "lane3")
     traffic, tsrc = measured_traffic(kname, args.workload, n)
     roofline = {
         "kernel": kname,

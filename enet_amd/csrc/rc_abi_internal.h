@@ -44,8 +44,9 @@ typedef struct {
 } rc_workspace_dev;
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */
-#define RC_KERNEL_LANE 0u   /* one packet per lane (default) */
+#define RC_KERNEL_LANE 0u   /* one packet per lane, model v2 (rc_lane.hip) */
 #define RC_KERNEL_WAVE 1u   /* one packet per wavefront */
+#define RC_KERNEL_LANE3 2u  /* one packet per lane, model v3 (rc_lane3.hip, default) */
 
 #define RC_EXACT_POOL_BYTES 98304u   /* 4096 nodes x 16 B (compress.c:42-46) + 4096 x 8 B rescale frames */
 
@@ -54,7 +55,8 @@ int rc_hip_compress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *str
 int rc_hip_decompress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
-uint32_t rc_hip_lane_region_bytes(uint32_t max_len);
+uint32_t rc_hip_lane_region_bytes(uint32_t max_len);    /* model v2 */
+uint32_t rc_hip_lane3_region_bytes(uint32_t max_len);   /* model v3 */
 
 /* CRC-32 of each packet (rc_crc32.hip): crc_out[i] = enet_crc32 (packet.c:143-163)
  * of in[in_off[i] .. +in_len[i]).  tables: rc_hip_crc32_table_words() words
@@ -65,7 +67,7 @@ uint32_t rc_hip_crc32_table_words(void);
 void rc_hip_crc32_build_tables(uint32_t *t);
 
 /* Kernel introspection for bench/profiling. */
-const char *rc_hip_fast_kernel_name(int decompress);
+const char *rc_hip_fast_kernel_name(int decompress, uint32_t kernel);
 uint32_t    rc_hip_lds_bytes(uint32_t max_len);
 
 #ifdef __cplusplus

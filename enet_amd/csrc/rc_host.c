@@ -72,7 +72,8 @@ static int ws_reserve(rc_ctx *c, size_t n)
 
 static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 {
-    uint32_t region = rc_hip_lane_region_bytes(max_len ? max_len : 4096);
+    uint32_t region = c->ws.kernel == RC_KERNEL_LANE3 ? rc_hip_lane3_region_bytes(max_len ? max_len : 4096)
+                                                      : rc_hip_lane_region_bytes(max_len ? max_len : 4096);
     size_t slots = n < c->max_slots ? n : c->max_slots;
     slots = (slots + 255) & ~(size_t) 255;
     if (slots <= c->ws.lane_slots && region <= c->ws.lane_region) return 0;
@@ -130,7 +131,9 @@ void *enet_range_coder_create(void)
     }
     {
         const char *k = getenv("ENET_RC_KERNEL");
-        c->ws.kernel = (k && strcmp(k, "wave") == 0) ? RC_KERNEL_WAVE : RC_KERNEL_LANE;
+        c->ws.kernel = RC_KERNEL_LANE3;
+        if (k && strcmp(k, "wave") == 0) c->ws.kernel = RC_KERNEL_WAVE;
+        if (k && strcmp(k, "lane2") == 0) c->ws.kernel = RC_KERNEL_LANE;
         const char *a = getenv("ENET_RC_LANES");
         c->ws.lane_active = 64;
         if (a && (atoi(a) == 32 || atoi(a) == 16)) c->ws.lane_active = (uint32_t) atoi(a);
@@ -173,7 +176,7 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     if (n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
     if (ws_reserve(c, n) != 0) return (int) hipErrorOutOfMemory;
-    if (c->ws.kernel == RC_KERNEL_LANE && lanes_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
+    if (c->ws.kernel != RC_KERNEL_WAVE && lanes_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
     rc_batch_dev b;
     b.in = in; b.in_off = in_off; b.in_len = in_len;
     b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;

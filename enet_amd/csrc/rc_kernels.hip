@@ -1044,9 +1044,11 @@ extern "C" uint32_t rc_hip_lds_bytes(uint32_t max_len) { return lds_bytes_for(ma
 extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
                                   void* stream);   // rc_lane.hip
 
-extern "C" const char* rc_hip_fast_kernel_name(int decompress)
+extern "C" const char* rc_hip_fast_kernel_name(int decompress, uint32_t kernel)
 {
-    return decompress ? "rc_decompress_lane" : "rc_compress_lane";
+    if (kernel == RC_KERNEL_WAVE) return decompress ? "rc_decompress_wave" : "rc_compress_wave";
+    if (kernel == RC_KERNEL_LANE) return decompress ? "rc_decompress_lane" : "rc_compress_lane";
+    return decompress ? "rc_decompress_lane3" : "rc_compress_lane3";
 }
 
 static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
@@ -1056,7 +1058,7 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     if (b->n > ws->n_cap) return static_cast<int>(hipErrorInvalidValue);
     hipError_t err = hipMemsetAsync(ws->counters, 0, 4 * sizeof(uint32_t), st);
     if (err != hipSuccess) return static_cast<int>(err);
-    if (ws->kernel == RC_KERNEL_LANE) {
+    if (ws->kernel != RC_KERNEL_WAVE) {
         const int rc = rc_hip_lane_launch(decompress ? 1 : 0, b, ws, stream);
         if (rc != 0) return rc;
     } else {

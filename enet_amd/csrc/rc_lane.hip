@@ -440,6 +440,7 @@ DEV void compress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_
         __builtin_amdgcn_s_waitcnt(0);
         PROF(9)
 #endif
+        sink_flush(o);
         const uint32_t v = src_byte(in);
         Raw1 n1;
         o1_fetch(reg, v, n1);                                       // next step's order-1 record
@@ -561,6 +562,7 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
         __builtin_amdgcn_s_waitcnt(0);
         PROF(8)
 #endif
+        sink_flush(o);
         int at = -1;                         // context that produced the symbol (2, 1, 0)
         uint32_t v = 0, nxt = 0;
         bool nfresh = false;
@@ -667,19 +669,6 @@ DEV void decompress_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint3
 
 }  // namespace
 
-#ifdef RC_PROFILE
-// diagnostic build: copy out (and optionally clear) the phase counters
-extern "C" int rc_lane_prof_read(unsigned long long* out, int reset)
-{
-    hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 64);
-    if (e == hipSuccess && reset) {
-        static const unsigned long long z[64] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
-    }
-    return static_cast<int>(e);
-}
-#endif
 
 extern "C" uint32_t rc_hip_lane_region_bytes(uint32_t max_len)
 {
@@ -820,6 +809,9 @@ void rc_compress_lane(rc_batch_dev b, rc_workspace_dev ws) { lane_main<false>(b,
 extern "C" __global__ __launch_bounds__(256)
 void rc_decompress_lane(rc_batch_dev b, rc_workspace_dev ws) { lane_main<true>(b, ws); }
 
+extern "C" int rc_hip_lane3_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
+                                   uint32_t blocks, void* stream);   // rc_lane3.hip
+
 extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
                                   void* stream)
 {
@@ -843,6 +835,7 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
         hipLaunchKernelGGL(rc_len_scatter, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins, ws->order);
         w.order = ws->order;
     }
+    if (ws->kernel == RC_KERNEL_LANE3) return rc_hip_lane3_launch(decompress, b, &w, blocks, stream);
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(256), lds, st, *b, w);
     else

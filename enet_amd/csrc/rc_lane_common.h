@@ -188,8 +188,10 @@ DEV uint32_t byte_mask(int k, int d)
     return (kk >= 0 && kk < 4) ? (0xFFu << (8 * kk)) : 0u;
 }
 
-// order-1 table: 256 records of 64 B after a 64-B lane header (epoch)
-constexpr uint32_t kO1Base = 64, kO1Rec = 64;
+// lane region: [0, 64) header (epoch), [64, 128) a scratch record for
+// stores and loads whose result is not used (rc_lane3.hip keeps its memory
+// operations unconditional), then the order-1 table: 256 records of 64 B
+constexpr uint32_t kDummyRec = 64, kO1Base = 128, kO1Rec = 64;
 // dense block sizes: C[16] u16 + counts[256] (+ a u16 per symbol for order-1 contexts)
 constexpr uint32_t kDenseO1 = 32 + 256 + 512, kDenseO2 = 32 + 256;
 
@@ -308,8 +310,9 @@ DEV uint32_t dense_rescale(uint8_t* blk)
 //          per step it is topped up by one aligned dword from a 16-B chunk
 //          register; the chunk after that one is loaded a chunk ahead, so the
 //          only wait on input data is for a load issued ~16 bytes earlier.
-//   output (ByteSink): bytes collect in a 64-bit register and leave as
-//          aligned dword stores.
+//   output (ByteSink): bytes collect in a 64-bit register, then in a 16-B
+//          window; a full window is stored at the top of the next step
+//          (sink_flush), before that step's loads.
 // Packet edges (unaligned starts, the last partial chunk) take byte-wise
 // paths behind wave-uniform guards, so nothing outside [p, p+len) is read or
 // written.  Bytes past the end of the input read as 0 (compress.c:366-367).
@@ -441,27 +444,60 @@ DEV uint32_t src_shift_in(ByteSrc& s, uint32_t code, uint32_t k)
 }
 
 struct ByteSink {
-    uint64_t acc;           // pending bytes, byte 0 belongs at `addr`
-    uint32_t nb, n, cap;    // pending bytes (incl. the skipped lead of an unaligned start); produced; capacity
-    uintptr_t addr, lo;     // 4-aligned address of acc byte 0; packet output start
+    uint64_t acc;           // bytes not yet in the window; byte 0 belongs at waddr + 4 * ws
+    uint32_t nb, ws;        // bytes in acc; dwords filled in w
+    uint4 w, wp;            // the 16-B window being filled; a full one awaiting its store
+    bool pend;              // wp holds a full window (sink_flush stores it)
+    uintptr_t waddr, wpaddr, lo;   // 16-aligned addresses of w and wp; packet output start
+    uint32_t n, cap;        // bytes produced; capacity
 };
 
 DEV void sink_init(ByteSink& o, uint8_t* p, uint32_t cap)
 {
     o.lo = reinterpret_cast<uintptr_t>(p);
-    o.addr = o.lo & ~static_cast<uintptr_t>(3);
+    o.waddr = o.lo & ~static_cast<uintptr_t>(15);
+    o.wpaddr = o.waddr;
+    o.ws = static_cast<uint32_t>(o.lo & 15) >> 2;     // (the lead before an unaligned start is never stored)
     o.nb = static_cast<uint32_t>(o.lo & 3);
     o.acc = 0;
+    o.w = make_uint4(0u, 0u, 0u, 0u);
+    o.wp = o.w;
+    o.pend = false;
     o.n = 0;
     o.cap = cap;
 }
 
-// bytes acc[0, k) at addr + i, skipping those before the packet start
-DEV void sink_bytes(const ByteSink& o, uint32_t k)
+// bytes [0, k) of (w, tail) at a + i, skipping those before the packet start
+DEV void sink_bytes(uintptr_t a, const uint4& w, uint64_t tail, uint32_t k, uintptr_t lo)
 {
+    const uint64_t w0 = w.x | (static_cast<uint64_t>(w.y) << 32), w1 = w.z | (static_cast<uint64_t>(w.w) << 32);
 #pragma unroll 1
-    for (uint32_t t = 0; t < k; ++t)
-        if (o.addr + t >= o.lo) *GPTR(uint8_t, o.addr + t) = static_cast<uint8_t>(o.acc >> (8 * t));
+    for (uint32_t t = 0; t < k; ++t) {
+        const uint64_t src = t < 8 ? w0 : (t < 16 ? w1 : tail);
+        if (a + t >= lo) *GPTR(uint8_t, a + t) = static_cast<uint8_t>(src >> (8 * (t & 7)));
+    }
+}
+
+DEV void sink_store(uintptr_t a, const uint4& w, uintptr_t lo, bool en)
+{
+    const bool edge = en && a < lo;
+#ifndef RC_LANE_HOST_TEST
+    if (en && !edge) { v4u32 v = {w.x, w.y, w.z, w.w}; *GPTR(v4u32, a) = v; }
+#else
+    if (en && !edge) *GPTR(uint4, a) = w;
+#endif
+    if (any_lane(edge)) {
+        if (edge) sink_bytes(a, w, 0, 16, lo);
+    }
+}
+
+// Stores the window completed by the previous step.  Called at the top of a
+// step, before that step issues its loads: a store issued after a load makes
+// the next wait for that load wait for the store as well (vmcnt is in order).
+DEV void sink_flush(ByteSink& o)
+{
+    sink_store(o.wpaddr, o.wp, o.lo, o.pend);
+    o.pend = false;
 }
 
 // append k <= 3 bytes m (first byte in bits 7..0) where `en`; the caller has
@@ -471,21 +507,35 @@ DEV void sink_put(ByteSink& o, uint32_t m, uint32_t k, bool en)
     o.acc |= en ? (static_cast<uint64_t>(m) << (8 * o.nb)) : 0ull;
     o.nb += en ? k : 0u;
     o.n += en ? k : 0u;
-    const bool flush = o.nb >= 4;
-    const bool edge = flush && o.addr < o.lo;
-    if (flush && !edge) *GPTR(uint32_t, o.addr) = static_cast<uint32_t>(o.acc);
-    if (any_lane(edge)) {
-        if (edge) sink_bytes(o, 4);
-    }
-    o.acc = flush ? (o.acc >> 32) : o.acc;
-    o.nb -= flush ? 4u : 0u;
-    o.addr += flush ? 4 : 0;
+    const bool mv = o.nb >= 4;
+    const uint32_t d = static_cast<uint32_t>(o.acc);
+    o.w.x = (mv && o.ws == 0) ? d : o.w.x; o.w.y = (mv && o.ws == 1) ? d : o.w.y;
+    o.w.z = (mv && o.ws == 2) ? d : o.w.z; o.w.w = (mv && o.ws == 3) ? d : o.w.w;
+    o.acc = mv ? (o.acc >> 32) : o.acc;
+    o.nb -= mv ? 4u : 0u;
+    o.ws += mv ? 1u : 0u;
+    const bool full = o.ws == 4;
+    if (any_lane(full && o.pend)) sink_flush(o);       // a second window in one step (rare)
+    o.wp.x = full ? o.w.x : o.wp.x; o.wp.y = full ? o.w.y : o.wp.y;
+    o.wp.z = full ? o.w.z : o.wp.z; o.wp.w = full ? o.w.w : o.wp.w;
+    o.wpaddr = full ? o.waddr : o.wpaddr;
+    o.pend = o.pend || full;
+    o.w.x = full ? 0u : o.w.x; o.w.y = full ? 0u : o.w.y; o.w.z = full ? 0u : o.w.z; o.w.w = full ? 0u : o.w.w;
+    o.ws = full ? 0u : o.ws;
+    o.waddr += full ? 16 : 0;
 }
 
+// the pending window, then what is left in w and acc
 DEV void sink_finish(ByteSink& o, bool en)
 {
-    if (any_lane(en && o.nb > 0)) {
-        if (en && o.nb > 0) sink_bytes(o, o.nb);
+    if (any_lane(en)) {
+        if (en) {
+            sink_flush(o);
+            const uint32_t d = static_cast<uint32_t>(o.acc);     // nb <= 3: the partial dword at slot ws
+            uint4 w = o.w;
+            w.x = o.ws == 0 ? d : w.x; w.y = o.ws == 1 ? d : w.y; w.z = o.ws == 2 ? d : w.z; w.w = o.ws == 3 ? d : w.w;
+            sink_bytes(o.waddr, w, 0, 4 * o.ws + o.nb, o.lo);
+        }
     }
 }
 
@@ -592,3 +642,17 @@ DEV uint32_t next_epoch(uint8_t* reg, uint32_t e)
 }
 
 }  // namespace
+
+#if defined(RC_PROFILE) && !defined(RC_LANE_HOST_TEST)
+// diagnostic build: copy out (and optionally clear) the phase counters
+extern "C" int rc_lane_prof_read(unsigned long long* out, int reset)
+{
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 64);
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[64] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+    }
+    return static_cast<int>(e);
+}
+#endif

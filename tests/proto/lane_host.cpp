@@ -2,7 +2,17 @@
 #define RC_LANE_HOST_TEST 1
 #include <stdlib.h>
 #include <string.h>
+#ifdef LANE3
+#include "../../enet_amd/csrc/rc_lane3.hip"
+#define REGION_BYTES rc_hip_lane3_region_bytes
+#define COMPRESS_ONE compress_one3
+#define DECOMPRESS_ONE decompress_one3
+#else
 #include "../../enet_amd/csrc/rc_lane.hip"
+#define REGION_BYTES rc_hip_lane_region_bytes
+#define COMPRESS_ONE compress_one
+#define DECOMPRESS_ONE decompress_one
+#endif
 
 static uint8_t g_root[304] __attribute__((aligned(16)));
 
@@ -11,7 +21,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
 {
     static uint8_t* region = nullptr;
     static uint32_t region_bytes = 0;
-    uint32_t need = rc_hip_lane_region_bytes(max_len);
+    uint32_t need = REGION_BYTES(max_len);
     if (need > region_bytes) {
         free(region); region = (uint8_t*) aligned_alloc(256, need); region_bytes = need;
         memset(region, 0, need);                                   // like the device pool (epoch 0 = unused)
@@ -22,7 +32,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     rc_workspace_dev ws = {};
     ws.flag_list = flags; ws.counters = counters; ws.lane_region = need; ws.lane_pool = region; ws.lane_active = 64;
     *out_len = 0xFFFFFFFFu;
-    if (decompress) decompress_one(b, ws, 0, region, g_root);
-    else compress_one(b, ws, 0, region, g_root);
+    if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root);
+    else COMPRESS_ONE(b, ws, 0, region, g_root);
     return counters[0] ? 1 : 0;   // 1 = routed to the exact path
 }

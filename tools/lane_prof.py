@@ -26,6 +26,11 @@ import torch  # noqa: E402
 
 from enet_amd import RangeCoder, compress_batch, decompress_batch, get_lib, synth  # noqa: E402
 
+V3 = "3" in os.environ.get("LANE_PROF_LIB", "")
+COMP3 = ["top (record decode)", "o2 lookup", "o2 encode", "o1 lookup", "o1 encode", "root", "advance (updates, stores)",
+         "input refill", "", "DRAIN (outstanding memory)"]
+DEC3 = ["top (record decode)", "o2 decode", "o1 decode", "root decode", "lookups", "advance (updates, stores)",
+        "output + refill", "", "", "DRAIN (outstanding memory)", "", ""]
 COMP = ["take+o1 prefetch", "o2 update", "o2 encode", "o1 update+link", "o1 encode", "o2 load+stores",
         "root lookup/add", "root encode+rescale", "advance/reset", "DRAIN (outstanding memory)"]
 DEC = ["o2 decode", "o1 decode", "root decode", "o1 prefetch", "o2 patch", "o1 patch+link",
@@ -52,7 +57,8 @@ def main():
         torch.cuda.synchronize()
         lib.rc_lane_prof_read(buf.ctypes.data, 1)
         steps = (n // 64) * 1200
-        comp = {COMP[k]: round(float(buf[k]) / steps, 1) for k in range(10)}
+        names = COMP3 if V3 else COMP
+        comp = {names[k]: round(float(buf[k]) / steps, 1) for k in range(10) if names[k]}
         comp["TOTAL"] = round(float(buf[:12].sum()) / steps, 1)
         res["compress_cycles_per_wave_step"] = comp
         back, bo, bl = decompress_batch(rc, out, oo, ol, dlen.clone(), max_len=int(ol.max().item()))
@@ -61,7 +67,8 @@ def main():
         back, bo, bl = decompress_batch(rc, out, oo, ol, dlen.clone(), max_len=int(ol.max().item()))
         torch.cuda.synchronize()
         lib.rc_lane_prof_read(buf.ctypes.data, 1)
-        dec = {DEC[k]: round(float(buf[16 + k]) / steps, 1) for k in range(12) if DEC[k]}
+        names = DEC3 if V3 else DEC
+        dec = {names[k]: round(float(buf[16 + k]) / steps, 1) for k in range(12) if names[k]}
         dec["TOTAL"] = round(float(buf[16:28].sum()) / steps, 1)
         res["decompress_cycles_per_wave_step"] = dec
         res["roundtrip_ok"] = bool(torch.equal(back, din))
