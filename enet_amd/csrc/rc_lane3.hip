@@ -361,6 +361,116 @@ DEV void ctx_update(uint8_t* reg, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v, uint3
     ctx_rescale<NV, O2>(reg, c, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
 }
 
+// ------------------------------------------------------------ order 0
+// Per lane: counts[256] (u8) in LDS; the 16 group boundaries in registers,
+// D[t] = 16 (t + 1) + the counts of symbols < 16 (t + 1) -- the cumulative
+// frequency including every symbol's minimum 1 (compress.c:159-199) -- as
+// packed u16 pairs d[i] = D[2i] | D[2i + 1] << 16.  The root total is
+// 1 + D[15].  A lookup reads one 16-B group from LDS; an update writes one
+// byte; the decoder finds the group with packed compares (no LDS reads).
+constexpr uint32_t kRootStride3 = 272;   // 68 dwords per lane: b128 group reads are conflict-free
+
+struct Root { uint32_t d[8]; };
+
+
+DEV void root3_clear(uint8_t* r, Root& R)
+{
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) reinterpret_cast<uint4*>(r)[i] = z;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) R.d[i] = (32 * i + 16) | ((32 * i + 32) << 16);
+}
+
+// D[t] for t in [-1, 15] (D[-1] = 0), by a masked OR (no indexed registers)
+DEV uint32_t root3_D(const Root& R, uint32_t t)
+{
+    const uint32_t i = t >> 1;
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) w |= R.d[k] & (0u - static_cast<uint32_t>(i == k));
+    return (t & 1) ? (w >> 16) : (w & 0xFFFF);
+}
+
+// under = cumulative frequency below v, cnt = count[v] (compress.c:159-199, minimum 1)
+DEV void root3_lookup(const uint8_t* r, const Root& R, uint32_t v, uint32_t& under, uint32_t& cnt)
+{
+    const uint32_t g = v >> 4, j = v & 15;
+    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    uint32_t within = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+        const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
+        const uint32_t mask = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+        within = sad(pick4(d, q) & mask, within);
+    }
+    cnt = (pick4(j >> 2, q) >> (8 * (j & 3))) & 0xFF;
+    under = root3_D(R, g - 1) + j + within;
+}
+
+DEV void root3_add(uint8_t* r, Root& R, uint32_t v, uint32_t cnt)
+{
+    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
+    cum_add(R.d, v >> 4, kRootDelta);
+}
+
+// Decoder: the symbol whose interval holds code (code < root total - 1):
+// g = #{t : D[t] <= code} by packed saturating compares, then halving on byte
+// sums inside group g.  Returns v; under = its cumulative frequency, cnt = count[v].
+DEV uint32_t root3_search(const uint8_t* r, const Root& R, uint32_t code, uint32_t& under, uint32_t& cnt)
+{
+    const uint32_t x1 = (code + 1) * 0x00010001u;
+    uint32_t acc = 0, pm = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t b = pk_min(pk_subsat(x1, R.d[i]), 0x00010001u);   // 1 where D <= code
+        acc = pk_add(acc, b);
+        pm = pk_max(pm, pk_mul(R.d[i], b));
+    }
+    const uint32_t g = (acc & 0xFFFF) + (acc >> 16);
+    const uint32_t prev = max(pm & 0xFFFF, pm >> 16);                 // D[g - 1], 0 for g = 0
+    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    uint32_t base = prev, j = 0;
+    uint32_t s = sad(q.x, sad(q.y, 8u));
+    bool hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 8u : 0u;
+    const uint32_t d0 = hi ? q.z : q.x, d1 = hi ? q.w : q.y;
+    s = sad(d0, 4u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 4u : 0u;
+    uint32_t w = hi ? d1 : d0;
+    s = sad(w & 0xFFFFu, 2u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 2u : 0u;
+    w = hi ? (w >> 16) : w;
+    s = (w & 0xFFu) + 1u;
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 1u : 0u;
+    w = hi ? (w >> 8) : w;
+    under = base;
+    cnt = w & 0xFFu;
+    return 16 * g + j;
+}
+
+// compress.c:90-112 for the root: halve the counts, rebuild D; returns the new total
+DEV uint32_t root3_rescale(uint8_t* r, Root& R)
+{
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < 16; ++g) {
+        uint4 q = reinterpret_cast<uint4*>(r)[g];
+        q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
+        q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
+        q.z -= (q.z >> 1) & 0x7F7F7F7Fu;
+        q.w -= (q.w >> 1) & 0x7F7F7F7Fu;
+        reinterpret_cast<uint4*>(r)[g] = q;
+        sum = sad(q.w, sad(q.z, sad(q.y, sad(q.x, sum))));
+        const uint32_t dg = sum + 16 * (g + 1);
+        if (g & 1) R.d[g >> 1] |= dg << 16; else R.d[g >> 1] = dg;
+    }
+    return (sum + 1 + 256) & 0xFFFF;
+}
+
 // ------------------------------------------------------------ lane state
 
 // Everything a lane carries from one step to the next.  Contexts of step i:
@@ -551,7 +661,8 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
     const uint32_t end = ws.lane_region;
     Lane L;
     lane_init(L, reg);
-    root_clear(root);
+    Root R;
+    root3_clear(root, R);
     uint32_t rtot = 1 + 256;
     uint32_t low = 0, range = ~0u;
     bool ok = true;
@@ -595,12 +706,12 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         // root, compress.c:318-329
         const bool en0 = !done2 && !done1;
         uint32_t under0, cnt0;
-        root_lookup(root, v, under0, cnt0);
-        if (en0) root_add(root, v, cnt0);
+        root3_lookup(root, R, v, under0, cnt0);
+        if (en0) root3_add(root, R, v, cnt0);
         enc_code(low, range, 1 + under0, 1 + cnt0, rtot, o, en0, ok);
         rtot = en0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
         const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit);
-        if (any_lane(rs0)) { if (rs0) rtot = root_rescale(root); }
+        if (any_lane(rs0)) { if (rs0) rtot = root3_rescale(root, R); }
         PROF(5)
         if (any_lane(!ok)) { if (!ok) break; }
         lane_advance<true>(L, reg, end, v, done2 ? 2 : done1 ? 1 : 0, h1, h2);
@@ -635,7 +746,8 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     src_init(in, bt.in + bt.in_off[pkt], len);
     Lane L;
     lane_init(L, reg);
-    root_clear(root);
+    Root R;
+    root3_clear(root, R);
     uint32_t rtot = 1 + 256;
     uint32_t low = 0, range = ~0u;
     uint32_t code = static_cast<uint32_t>(in.la >> 32);            // compress.c:344-350 (0 past the end)
@@ -698,11 +810,11 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (cd < 1) { dec_code(low, code, range, 0, 1, in, true); break; }   // end of stream
             if (cd - 1 >= rtot - 1) { anomaly = true; break; }           // past symbol 255
             uint32_t under, cnt;
-            v = root_search(root, cd - 1, under, cnt);
-            root_add(root, v, cnt);
+            v = root3_search(root, R, cd - 1, under, cnt);
+            root3_add(root, R, v, cnt);
             dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
             rtot = (rtot + kRootDelta) & 0xFFFF;
-            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root_rescale(root);
+            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale(root, R);
             at = 0;
         }
         PROF(3)
@@ -749,7 +861,7 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (l >= act) return;
     const uint32_t local = wave * act + l;
-    uint8_t* root = smem + local * kRootStride;
+    uint8_t* root = smem + local * kRootStride3;
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
@@ -773,7 +885,7 @@ extern "C" int rc_hip_lane3_launch(int decompress, const rc_batch_dev* b, const 
                                    uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStride;
+    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStride3;
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane3, dim3(blocks), dim3(256), lds, st, *b, *ws);
     else

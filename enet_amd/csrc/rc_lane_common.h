@@ -53,8 +53,65 @@ constexpr uint32_t kRootStride = 304;        // LDS bytes per lane; 76 dwords (7
 DEV uint32_t val_of(uint32_t e) { return e & 0xFF; }
 DEV uint32_t cnt_of(uint32_t e) { return (e >> 8) & 0xFF; }
 DEV uint32_t sad(uint32_t x, uint32_t acc) { return __builtin_amdgcn_sad_u8(x, 0u, acc); }
-DEV uint32_t pick4(uint32_t i, const uint4& q) { return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w; }
+// component i of q as a masked OR: a select chain on a lane-varying index
+// compiles to branches, or to a dynamically indexed scratch load
+DEV uint32_t pick4(uint32_t i, const uint4& q)
+{
+    return (q.x & (0u - static_cast<uint32_t>(i == 0))) | (q.y & (0u - static_cast<uint32_t>(i == 1))) |
+           (q.z & (0u - static_cast<uint32_t>(i == 2))) | (q.w & (0u - static_cast<uint32_t>(i == 3)));
+}
 DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+// ---- packed u16 pairs (the 16 cumulative group sums of a 256-symbol context)
+#ifndef RC_LANE_HOST_TEST
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+DEV u16x2 as2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+DEV uint32_t as1(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+// (inline asm: the compiler rewrites min(subsat(x, d), 1) into per-half
+// compares and selects, four times the instructions)
+DEV uint32_t pk_subsat(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+DEV uint32_t pk_min(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+DEV uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c)     // a * b + c per u16 half
+{
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+DEV uint32_t pk_max(uint32_t a, uint32_t b) { return as1(__builtin_elementwise_max(as2(a), as2(b))); }
+DEV uint32_t pk_add(uint32_t a, uint32_t b) { return as1(as2(a) + as2(b)); }
+DEV uint32_t pk_mul(uint32_t a, uint32_t b) { return as1(as2(a) * as2(b)); }
+#else
+template <class F> uint32_t pk2(uint32_t a, uint32_t b, F f)
+{
+    return (f(a & 0xFFFF, b & 0xFFFF) & 0xFFFF) | ((f(a >> 16, b >> 16) & 0xFFFF) << 16);
+}
+inline uint32_t pk_subsat(uint32_t a, uint32_t b) { return pk2(a, b, [](uint32_t x, uint32_t y) { return x > y ? x - y : 0u; }); }
+inline uint32_t pk_min(uint32_t a, uint32_t b) { return pk2(a, b, [](uint32_t x, uint32_t y) { return x < y ? x : y; }); }
+inline uint32_t pk_max(uint32_t a, uint32_t b) { return pk2(a, b, [](uint32_t x, uint32_t y) { return x > y ? x : y; }); }
+inline uint32_t pk_add(uint32_t a, uint32_t b) { return pk2(a, b, [](uint32_t x, uint32_t y) { return x + y; }); }
+inline uint32_t pk_mul(uint32_t a, uint32_t b) { return pk2(a, b, [](uint32_t x, uint32_t y) { return x * y; }); }
+inline uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) { return pk_add(pk_mul(a, b), c); }
+#endif
+
+// C[t] += d for every t >= g, C as 8 packed pairs (C[2i] | C[2i+1] << 16):
+// per pair, (t + 1) -sat g is nonzero exactly where t >= g
+DEV void cum_add(uint32_t* c, uint32_t g, uint32_t d)
+{
+    const uint32_t gg = g * 0x00010001u, dd = d * 0x00010001u;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i)
+        c[i] = pk_mad(pk_min(pk_subsat((2 * i + 1) | ((2 * i + 2) << 16), gg), 0x00010001u), dd, c[i]);
+}
 
 // ------------------------------------------------------------ order 0 (LDS)
 
@@ -232,10 +289,10 @@ DEV void dense_add(uint8_t* blk, uint32_t v, uint32_t d, Dense& z)
     z.grp.x += q == 0 ? bd : 0u; z.grp.y += q == 1 ? bd : 0u;
     z.grp.z += q == 2 ? bd : 0u; z.grp.w += q == 3 ? bd : 0u;
     // C[t] += d for t >= g: word i holds C[2i] | C[2i + 1] << 16
-#define RC_CADD(w, t) w += ((t) >= g ? d : 0u) | ((t) + 1 >= g ? (d << 16) : 0u)
-    RC_CADD(z.c0.x, 0u); RC_CADD(z.c0.y, 2u); RC_CADD(z.c0.z, 4u); RC_CADD(z.c0.w, 6u);
-    RC_CADD(z.c1.x, 8u); RC_CADD(z.c1.y, 10u); RC_CADD(z.c1.z, 12u); RC_CADD(z.c1.w, 14u);
-#undef RC_CADD
+    uint32_t cw[8] = {z.c0.x, z.c0.y, z.c0.z, z.c0.w, z.c1.x, z.c1.y, z.c1.z, z.c1.w};
+    cum_add(cw, g, d);
+    z.c0 = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    z.c1 = make_uint4(cw[4], cw[5], cw[6], cw[7]);
     uint4* p = reinterpret_cast<uint4*>(blk);
     p[0] = z.c0; p[1] = z.c1; p[2 + g] = z.grp;
 }
@@ -334,13 +391,7 @@ DEV uint4 gload16(uintptr_t a) { return *GPTRC(uint4, a); }
 
 DEV uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
-// dword q (0..3) of a chunk, as a masked OR: the compiler turns a select
-// chain between fields into a dynamically indexed scratch load
-DEV uint32_t sel4(uint32_t q, const uint4& c)
-{
-    return (c.x & (0u - static_cast<uint32_t>(q == 0))) | (c.y & (0u - static_cast<uint32_t>(q == 1))) |
-           (c.z & (0u - static_cast<uint32_t>(q == 2))) | (c.w & (0u - static_cast<uint32_t>(q == 3)));
-}
+DEV uint32_t sel4(uint32_t q, const uint4& c) { return pick4(q, c); }
 
 // the aligned 16-B chunk at c, zero outside [lo, hi)
 DEV uint4 chunk_load(uintptr_t lo, uintptr_t hi, uintptr_t c, bool en)
@@ -558,7 +609,8 @@ DEV void enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count
                   ByteSink& o, bool en, bool& ok)
 {
     en = en && ok;
-    const uint32_t r = udiv(range, en ? total : 1u);
+    if (!any_lane(en)) return;
+    const uint32_t r = udiv16(range, en ? total : 1u);
     low = en ? low + under * r : low;
     range = en ? r * count : range;
     const uint32_t k = en ? settled_bytes(low, range) : 0u;
@@ -587,9 +639,9 @@ DEV void enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count
 // compress.c:352 (truncated to u16 at :545/:575); divides range by total where `en`
 DEV uint32_t dec_read(uint32_t& range, uint32_t low, uint32_t code, uint32_t total, bool en)
 {
-    const uint32_t r = udiv(range, en ? total : 1u);
+    const uint32_t r = udiv16(range, en ? total : 1u);
     range = en ? r : range;
-    return udiv(code - low, en ? r : 1u) & 0xFFFF;
+    return udiv_lo16(code - low, en ? r : 1u);
 }
 
 // compress.c:354-371 where `en`

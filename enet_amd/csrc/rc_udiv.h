@@ -23,6 +23,37 @@ __device__ __forceinline__ uint32_t udiv(uint32_t a, uint32_t b)
     q += (a - q * b >= b) ? 1u : 0u;
     return q;
 }
+
+// The coder's divisions by a context total (b < 2^16) in single precision:
+// a first quotient from a float reciprocal (within 2^10 / b + 1 of a / b), a
+// second one from the remainder (|r| < 2^17, exact in float), then one
+// remainder check.  Exact for all a and 1 <= b <= 65535 (tests/test_udiv.py).
+__device__ __forceinline__ uint32_t udiv16(uint32_t a, uint32_t b)
+{
+    const float rb = __builtin_amdgcn_rcpf(static_cast<float>(b));
+    uint32_t q = static_cast<uint32_t>(static_cast<float>(a) * rb);
+    const int32_t r = static_cast<int32_t>(a - q * b);
+    q += static_cast<int32_t>(static_cast<float>(r) * rb);
+    const int32_t r2 = static_cast<int32_t>(a - q * b);
+    q += r2 < 0 ? 0xFFFFFFFFu : (r2 >= static_cast<int32_t>(b) ? 1u : 0u);
+    return q;
+}
+
+// floor(a / b) & 0xFFFF for any b >= 1 (the decoder's READ, compress.c:352):
+// single precision while the quotient is below 2^16 (every valid stream:
+// code - low < range), udiv otherwise.
+__device__ __forceinline__ uint32_t udiv_lo16(uint32_t a, uint32_t b)
+{
+    const float qf = static_cast<float>(a) * __builtin_amdgcn_rcpf(static_cast<float>(b));
+    uint32_t q = static_cast<uint32_t>(qf);
+    const uint64_t m = static_cast<uint64_t>(q) * b;
+    q += m > a ? 0xFFFFFFFFu : (a - static_cast<uint32_t>(m) >= b ? 1u : 0u);
+    const bool wide = qf >= 65000.0f;
+    if (__builtin_amdgcn_ballot_w64(wide) != 0) q = wide ? udiv(a, b) : q;
+    return q & 0xFFFF;
+}
 #else
 inline uint32_t udiv(uint32_t a, uint32_t b) { return a / b; }
+inline uint32_t udiv16(uint32_t a, uint32_t b) { return a / b; }
+inline uint32_t udiv_lo16(uint32_t a, uint32_t b) { return (a / b) & 0xFFFF; }
 #endif

@@ -26,6 +26,17 @@ extern "C" __global__ void udiv_check(uint64_t seed, uint32_t iters, unsigned lo
         const uint32_t q = a0 / b;
         const uint32_t cases[4] = {a0, q * b, q * b ? q * b - 1 : 0u, 0xFFFFFFFFu};
         for (int c = 0; c < 4; ++c) nbad += udiv(cases[c], b) != cases[c] / b;
+        // udiv16: divisors below 2^16 (context totals)
+        const uint32_t b16 = (b & 0xFFFF) ? (b & 0xFFFF) : 1u;
+        const uint32_t q16 = a0 / b16;
+        const uint32_t c16[4] = {a0, q16 * b16, q16 * b16 ? q16 * b16 - 1 : 0u, 0xFFFFFFFFu};
+        for (int c = 0; c < 4; ++c) nbad += udiv16(c16[c], b16) != c16[c] / b16;
+        // udiv_lo16: any divisor, low 16 bits of the quotient
+        for (int c = 0; c < 4; ++c) nbad += udiv_lo16(cases[c], b) != ((cases[c] / b) & 0xFFFF);
+        // quotients just below 2^16 (a READ at the top of a context's range)
+        const uint32_t bq = b > 65536 ? b >> 16 : (b ? b : 1u), qq = 65535u - (uint32_t) (x & 1023);
+        const uint64_t aq = (uint64_t) qq * bq + (x >> 53) % bq;
+        if (aq <= 0xFFFFFFFFull) nbad += udiv_lo16((uint32_t) aq, bq) != (((uint32_t) aq / bq) & 0xFFFF);
     }
     if (nbad) atomicAdd(bad, nbad);
 }
