@@ -485,8 +485,10 @@ struct Lane {
     uint32_t info;              // o2 info of (a, b)
     uint32_t ipos;              // dense holder: region offset of that info (0 = inline holder)
     uint32_t a, b, order, epoch, bump, qoff;
-    bool same, fwd, prv_dirty, q_dirty, q_fwd, ovf;
-    bool nsame, fromprv;        // where the next step's R[v] comes from (lane_prefetch)
+    // (flags as 0/1 words: the compiler keeps a bool as a 64-bit lane mask in
+    // SGPRs, and a dozen loop-carried ones spill into VGPR lanes)
+    uint32_t same, fwd, prv_dirty, q_dirty, q_fwd, ovf;
+    uint32_t nsame, fromprv;    // where the next step's R[v] comes from (lane_prefetch)
 };
 
 DEV void lane_init(Lane& L, uint8_t* reg)
@@ -585,7 +587,9 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, L
         }
         if (any_lane(big)) {
             if (big && !L.ovf) {
-                ctx_update<6, false>(reg, L.q, h2, v, L.bump, end, L.ovf, true);
+                bool ovf = L.ovf != 0;
+                ctx_update<6, false>(reg, L.q, h2, v, L.bump, end, ovf, true);
+                L.ovf = ovf;
                 L.q_dirty = true;
             }
         }
@@ -602,8 +606,11 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, L
     }
     // ---- 2. o1 context b, compress.c:286-316 (its lookup, when the decoder did not need it)
     if (!HAVE_H1 && L.order >= 1 && at == 2) h1 = ctx_find<3, true>(reg, L.cur, v);
-    if (L.order >= 1 && at <= 1)
-        ctx_update<3, true>(reg, L.cur, h1, v, L.bump, end, L.ovf, true);
+    if (L.order >= 1 && at <= 1) {
+        bool ovf = L.ovf != 0;
+        ctx_update<3, true>(reg, L.cur, h1, v, L.bump, end, ovf, true);
+        L.ovf = ovf;
+    }
     // ---- 3. next step: contexts (b, v)
     uint32_t ninfo = 0, nipos = 0;
     if (L.order >= 1) {
