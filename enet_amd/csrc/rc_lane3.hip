@@ -313,7 +313,7 @@ DEV bool densify(uint8_t* reg, Ctx<NV, O2>& c, uint32_t& bump, uint32_t end)
 template <uint32_t NV, bool O2>
 DEV void ctx_rescale(uint8_t* reg, Ctx<NV, O2>& c, bool en)
 {
-    if (!any_lane(en)) return;
+    if (!rare_lane(en)) return;
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t d = 0; d < NV; ++d) {
@@ -321,7 +321,7 @@ DEV void ctx_rescale(uint8_t* reg, Ctx<NV, O2>& c, bool en)
         c.cnt[d] = en ? h : c.cnt[d];
         sum = sad(h, sum);
     }
-    if (any_lane(en && c.dense != 0)) {
+    if (rare_lane(en && c.dense != 0)) {
         if (en && c.dense != 0) sum = dense_rescale(reg + c.ext);
     }
     c.esc -= en ? (c.esc >> 1) : 0u;
@@ -342,7 +342,7 @@ DEV void ctx_update(uint8_t* reg, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v, uint3
     for (uint32_t d = 0; d < NV; ++d) c.cnt[d] += (en && h.found && inl) ? (h.eq[d] << 1) : 0u;
     inline_insert<NV, O2>(c, h.k, v, ins && inl && c.len < cap);
     const bool grow = ins && inl && c.len >= cap;
-    if (any_lane(grow || (en && !inl))) {
+    if (rare_lane(grow || (en && !inl))) {
         if (grow) {
             const bool ok = densify<NV, O2>(reg, c, bump, end);
             ovf = ovf || !ok;
@@ -723,7 +723,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         if (any_lane(!ok)) { if (!ok) break; }
         lane_advance<true>(L, reg, end, v, done2 ? 2 : done1 ? 1 : 0, h1, h2);
         PROF(6)
-        if (any_lane(L.ovf)) { if (L.ovf) break; }
+        if (rare_lane(L.ovf)) { if (L.ovf) break; }
         PROF(7)
     }
     PROF_FLUSH(0)

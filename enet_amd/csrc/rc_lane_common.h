@@ -61,6 +61,9 @@ DEV uint32_t pick4(uint32_t i, const uint4& q)
            (q.z & (0u - static_cast<uint32_t>(i == 2))) | (q.w & (0u - static_cast<uint32_t>(i == 3)));
 }
 DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+// the same for paths that are rare per wave: their blocks are laid out away
+// from the hot loop (instruction-cache locality, fall-through hot path)
+DEV bool rare_lane(bool p) { return __builtin_expect(__builtin_amdgcn_ballot_w64(p) != 0, 0); }
 
 // ---- packed u16 pairs (the 16 cumulative group sums of a 256-symbol context)
 #ifndef RC_LANE_HOST_TEST
@@ -399,7 +402,7 @@ DEV uint4 chunk_load(uintptr_t lo, uintptr_t hi, uintptr_t c, bool en)
     const bool full = c >= lo && c + 16 <= hi;
     uint4 w = make_uint4(0u, 0u, 0u, 0u);
     if (en && full) w = gload16(c);
-    if (any_lane(en && !full && c < hi && c + 16 > lo)) {
+    if (rare_lane(en && !full && c < hi && c + 16 > lo)) {
         if (en && !full) {
             uint64_t d0 = 0, d1 = 0;          // (shifts, not an indexed array: that would live in scratch)
 #pragma unroll 1
@@ -441,7 +444,7 @@ DEV void src_refill(ByteSrc& s, bool en)
         const uintptr_t a = s.next;
         const bool full = a + 16 <= s.hi;           // (a > lo always holds here)
         if (adv && full) s.n = gload16(a);
-        if (any_lane(adv && !full)) {
+        if (rare_lane(adv && !full)) {
             if (adv && !full) s.n = chunk_load(s.lo, s.hi, a, true);
         }
         s.next += adv ? 16 : 0;
@@ -461,7 +464,7 @@ DEV void src_init(ByteSrc& s, const uint8_t* p, uint32_t len)
     s.la = static_cast<uint64_t>(bswap(sel4(s.q, s.c)) << (8 * sk)) << 32;
     s.na = 4 - sk;
     s.q += 1;
-    if (any_lane(s.q == 4)) {
+    if (rare_lane(s.q == 4)) {
         const bool adv = s.q == 4;
         s.c.x = adv ? s.n.x : s.c.x; s.c.y = adv ? s.n.y : s.c.y;
         s.c.z = adv ? s.n.z : s.c.z; s.c.w = adv ? s.n.w : s.c.w;
@@ -537,7 +540,7 @@ DEV void sink_store(uintptr_t a, const uint4& w, uintptr_t lo, bool en)
 #else
     if (en && !edge) *GPTR(uint4, a) = w;
 #endif
-    if (any_lane(edge)) {
+    if (rare_lane(edge)) {
         if (edge) sink_bytes(a, w, 0, 16, lo);
     }
 }
@@ -566,7 +569,7 @@ DEV void sink_put(ByteSink& o, uint32_t m, uint32_t k, bool en)
     o.nb -= mv ? 4u : 0u;
     o.ws += mv ? 1u : 0u;
     const bool full = o.ws == 4;
-    if (any_lane(full && o.pend)) sink_flush(o);       // a second window in one step (rare)
+    if (rare_lane(full && o.pend)) sink_flush(o);      // a second window in one step
     o.wp.x = full ? o.w.x : o.wp.x; o.wp.y = full ? o.w.y : o.wp.y;
     o.wp.z = full ? o.w.z : o.wp.z; o.wp.w = full ? o.w.w : o.wp.w;
     o.wpaddr = full ? o.waddr : o.wpaddr;
@@ -579,7 +582,7 @@ DEV void sink_put(ByteSink& o, uint32_t m, uint32_t k, bool en)
 // the pending window, then what is left in w and acc
 DEV void sink_finish(ByteSink& o, bool en)
 {
-    if (any_lane(en)) {
+    if (rare_lane(en)) {
         if (en) {
             sink_flush(o);
             const uint32_t d = static_cast<uint32_t>(o.acc);     // nb <= 3: the partial dword at slot ws
@@ -621,7 +624,7 @@ DEV void enc_code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count
     low = put ? low << (8 * k) : low;
     range = put ? range << (8 * k) : range;
     bool more = put && range < kBot;
-    while (any_lane(more)) {
+    while (rare_lane(more)) {
         const bool carry = (low ^ (low + range)) >= kTop;
         const bool stop = carry && range >= kBot;
         more = more && !stop;
@@ -657,7 +660,7 @@ DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under
     low <<= 8 * kk;
     range <<= 8 * kk;
     bool more = en && (!fast || range < kBot);
-    while (any_lane(more)) {
+    while (rare_lane(more)) {
         const bool carry = (low ^ (low + range)) >= kTop;
         const bool stop = carry && range >= kBot;
         more = more && !stop;
@@ -683,7 +686,7 @@ DEV void flag_exact(const rc_workspace_dev& ws, uint32_t pkt)
 DEV uint32_t next_epoch(uint8_t* reg, uint32_t e)
 {
     e += 1;
-    if (any_lane((e & 0xFFFF) == 0)) {
+    if (rare_lane((e & 0xFFFF) == 0)) {
         if ((e & 0xFFFF) == 0) {
             for (uint32_t x = 0; x < 256; ++x) *reinterpret_cast<uint32_t*>(reg + kO1Base + x * kO1Rec) = 0u;
             e += 1;
