@@ -63,7 +63,11 @@ DEV uint32_t pick4(uint32_t i, const uint4& q)
 DEV bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 // the same for paths that are rare per wave: their blocks are laid out away
 // from the hot loop (instruction-cache locality, fall-through hot path)
+#ifndef RC_HOTPATH_ONLY
 DEV bool rare_lane(bool p) { return __builtin_expect(__builtin_amdgcn_ballot_w64(p) != 0, 0); }
+#else   // static analysis only (tools/phase_asm.sh): the rare paths compiled out
+DEV bool rare_lane(bool) { return false; }
+#endif
 
 // ---- packed u16 pairs (the 16 cumulative group sums of a 256-symbol context)
 #ifndef RC_LANE_HOST_TEST

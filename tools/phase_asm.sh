@@ -4,7 +4,8 @@
 # instruction count between consecutive s_memtime stamps (rare paths included).
 cd "$(dirname "$0")/../enet_amd/csrc"
 K=${1:-compress}
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include -I. -DRC_PROFILE --cuda-device-only -S rc_lane3.hip -o /tmp/l3p.s 2>/dev/null
+EXTRA=${2:-}
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include -I. -DRC_PROFILE $EXTRA --cuda-device-only -S rc_lane3.hip -o /tmp/l3p.s 2>/dev/null
 awk "/^rc_${K}_lane3:/,/s_endpgm/" /tmp/l3p.s > /tmp/kp.s
 grep -n "s_memtime" /tmp/kp.s | cut -d: -f1 > /tmp/marks
 prev=""
