@@ -17,12 +17,23 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module")
-def coder():
+@pytest.fixture(scope="module", params=["lane3", "lane2"])
+def coder(request):
+    """Every test runs on the default lane kernels (model v3, rc_lane3.hip) and
+    on model v2 (rc_lane.hip), selected when the coder context is created."""
+    import os
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from enet_amd import RangeCoder
-    c = RangeCoder()
+    old = os.environ.get("ENET_RC_KERNEL")
+    os.environ["ENET_RC_KERNEL"] = request.param
+    try:
+        c = RangeCoder()
+    finally:
+        if old is None:
+            os.environ.pop("ENET_RC_KERNEL", None)
+        else:
+            os.environ["ENET_RC_KERNEL"] = old
     yield c
     c.close()
 
