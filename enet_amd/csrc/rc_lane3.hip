@@ -720,14 +720,16 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit);
         if (any_lane(rs0)) { if (rs0) rtot = root3_rescale(root, R); }
         PROF(5)
-        if (any_lane(!ok)) { if (!ok) break; }
+        // no loop exit between the record load (lane_prefetch) and the record
+        // store (lane_advance): an exit path there makes the compiler's vmcnt
+        // bookkeeping wait for the store at the top of every step
         lane_advance<true>(L, reg, end, v, done2 ? 2 : done1 ? 1 : 0, h1, h2);
         PROF(6)
-        if (rare_lane(L.ovf)) { if (L.ovf) break; }
+        if (rare_lane(!ok || L.ovf)) { if (!ok || L.ovf) break; }
         PROF(7)
     }
     PROF_FLUSH(0)
-    if (L.ovf) { flag_exact(ws, pkt); return; }
+    if (ok && L.ovf) { flag_exact(ws, pkt); return; }
     // flush, compress.c:139-146
     while (any_lane(ok && low != 0)) {
         const bool more = ok && low != 0;
@@ -830,16 +832,16 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         if (at == 0 && L.order >= 1) h1 = ctx_find<3, true>(reg, L.cur, v);
         if (at == 2 && L.order >= 1) h1 = ctx_find<3, true>(reg, L.cur, v);
         if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, L.q, v);
-        if (o.n >= o.cap) { fail = true; break; }                    // compress.c:617
+        fail = o.n >= o.cap;                                         // compress.c:617
         PROF(4)
-        lane_advance<true>(L, reg, end, v, at, h1, h2);
+        lane_advance<true>(L, reg, end, v, at, h1, h2);             // (see compress_one3)
         PROF(5)
-        if (L.ovf) break;
+        if (fail || L.ovf) break;
         sink_put(o, v, 1, true);
         PROF(6)
     }
     PROF_FLUSH(16)
-    if (L.ovf || anomaly) { flag_exact(ws, pkt); return; }
+    if ((L.ovf && !fail) || anomaly) { flag_exact(ws, pkt); return; }
     sink_finish(o, !fail);
     bt.out_len[pkt] = fail ? 0u : o.n;
 }
