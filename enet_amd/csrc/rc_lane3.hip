@@ -774,7 +774,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         if (o.n >= kMaxLen3) { anomaly = true; break; }             // a model reset could follow: exact path
         lane_top(L);
         sink_flush(o);
-        src_refill(in, true);
+        src_fill(in, true);
         PROF(0)
         int at = -1;
         uint32_t v = 0;
@@ -838,6 +838,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         PROF(5)
         if (fail || L.ovf) break;
         sink_put(o, v, 1, true);
+        src_adv(in);
         PROF(6)
     }
     PROF_FLUSH(16)

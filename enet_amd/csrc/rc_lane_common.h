@@ -426,13 +426,27 @@ DEV uint4 chunk_load(uintptr_t lo, uintptr_t hi, uintptr_t c, bool en)
 struct ByteSrc {
     uint64_t la;            // lookahead, next byte in bits 63..56
     uint32_t na, q;         // bytes in la; next dword of c
-    uint4 c, n;             // current chunk; the chunk after it (in flight)
+    uint4 c, n;             // current chunk; the chunk after it (in flight, unmasked)
     uintptr_t next, lo, hi; // address of the chunk after n; packet bounds
+    uintptr_t last;         // the aligned chunk holding byte hi - 1
 };
 
-// one more dword into the lookahead where it has room for it (na <= 4);
-// moves to the next chunk when c is used up
-DEV void src_refill(ByteSrc& s, bool en)
+// bytes of the chunk at a that lie below hi (the rest reads as 0)
+DEV uint4 chunk_mask_hi(uint4 w, uintptr_t a, uintptr_t hi)
+{
+    const uint32_t v = hi <= a ? 0u : (hi - a >= 16 ? 16u : static_cast<uint32_t>(hi - a));
+    uint32_t m[4];
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+        const uint32_t k = v > 4 * d ? min(v - 4 * d, 4u) : 0u;
+        m[d] = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
+    }
+    return make_uint4(w.x & m[0], w.y & m[1], w.z & m[2], w.w & m[3]);
+}
+
+// one more dword into the lookahead where it has room for it (na <= 4).
+// Leaves q == 4 when c is used up; src_adv then moves to the next chunk.
+DEV void src_fill(ByteSrc& s, bool en)
 {
     const bool need = en && s.na <= 4;
     const uint32_t d = bswap(sel4(s.q, s.c));
@@ -440,25 +454,40 @@ DEV void src_refill(ByteSrc& s, bool en)
     s.la |= need ? (static_cast<uint64_t>(d) << sh) : 0ull;
     s.na += need ? 4u : 0u;
     s.q += need ? 1u : 0u;
+}
+
+// c := n where c is used up, and load the chunk after it into n.  The load is
+// issued for every lane of the wave (lanes that keep n reload it): a load
+// predicated per lane makes the compiler copy its result into n right away,
+// i.e. wait for it, behind every store in flight.  Chunks past the packet read
+// the last one in bounds; bytes past the packet are masked when n is used.
+// The decoder calls this at the end of a step: a loop exit between this load
+// and the next use of n would make that use wait for vmcnt(0).
+DEV void src_adv(ByteSrc& s)
+{
     const bool adv = s.q == 4;
     if (any_lane(adv)) {
-        s.c.x = adv ? s.n.x : s.c.x; s.c.y = adv ? s.n.y : s.c.y;
-        s.c.z = adv ? s.n.z : s.c.z; s.c.w = adv ? s.n.w : s.c.w;
+        const uint4 m = chunk_mask_hi(s.n, s.next - 16, s.hi);
+        s.c.x = adv ? m.x : s.c.x; s.c.y = adv ? m.y : s.c.y;
+        s.c.z = adv ? m.z : s.c.z; s.c.w = adv ? m.w : s.c.w;
         s.q = adv ? 0u : s.q;
-        const uintptr_t a = s.next;
-        const bool full = a + 16 <= s.hi;           // (a > lo always holds here)
-        if (adv && full) s.n = gload16(a);
-        if (rare_lane(adv && !full)) {
-            if (adv && !full) s.n = chunk_load(s.lo, s.hi, a, true);
-        }
         s.next += adv ? 16 : 0;
+        const uintptr_t a = s.next - 16;
+        s.n = gload16(a <= s.last ? a : s.last);
     }
+}
+
+DEV void src_refill(ByteSrc& s, bool en)
+{
+    src_fill(s, en);
+    src_adv(s);
 }
 
 DEV void src_init(ByteSrc& s, const uint8_t* p, uint32_t len)
 {
     s.lo = reinterpret_cast<uintptr_t>(p);
     s.hi = s.lo + len;
+    s.last = (s.hi - 1) & ~static_cast<uintptr_t>(15);
     const uintptr_t a = s.lo & ~static_cast<uintptr_t>(15);
     s.c = chunk_load(s.lo, s.hi, a, true);
     s.n = chunk_load(s.lo, s.hi, a + 16, true);
@@ -670,7 +699,8 @@ DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under
         more = more && !stop;
         if (!any_lane(more)) break;
         range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
-        src_refill(in, more && in.na == 0);
+        src_adv(in);                       // (the decoder's top src_fill may have used c up)
+        src_fill(in, more && in.na == 0);
         code = src_shift_in(in, code, more ? 1u : 0u);
         range = more ? range << 8 : range;
         low = more ? low << 8 : low;
