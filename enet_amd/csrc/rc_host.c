@@ -15,6 +15,7 @@
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
@@ -74,6 +75,8 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 {
     uint32_t region = c->ws.kernel == RC_KERNEL_LANE3 ? rc_hip_lane3_region_bytes(max_len ? max_len : 4096)
                                                       : rc_hip_lane_region_bytes(max_len ? max_len : 4096);
+    const char *ov = getenv("ENET_RC_REGION");      /* diagnostic: smaller regions (overflows take the exact path) */
+    if (ov && atoi(ov) > 0 && (uint32_t) atoi(ov) < region) region = ((uint32_t) atoi(ov) + 255) & ~255u;
     size_t slots = n < c->max_slots ? n : c->max_slots;
     slots = (slots + 255) & ~(size_t) 255;
     if (slots <= c->ws.lane_slots && region <= c->ws.lane_region) return 0;
@@ -87,6 +90,8 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     if (hipMemset(c->ws.lane_pool, 0, slots * (size_t) region) != hipSuccess) return -1;
     c->ws.lane_slots = (uint32_t) slots;
     c->ws.lane_region = region;
+    if (getenv("ENET_RC_DEBUG"))
+        fprintf(stderr, "enet_rc: lane pool %p, %zu slots x %u B\n", c->ws.lane_pool, slots, region);
     return 0;
 }
 

@@ -366,13 +366,40 @@ DEV void ctx_update(uint8_t* reg, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v, uint3
 // D[t] = 16 (t + 1) + the counts of symbols < 16 (t + 1) -- the cumulative
 // frequency including every symbol's minimum 1 (compress.c:159-199) -- as
 // packed u16 pairs d[i] = D[2i] | D[2i + 1] << 16.  The root total is
-// 1 + D[15].  A lookup reads one 16-B group from LDS; an update writes one
-// byte; the decoder finds the group with packed compares (no LDS reads).
-constexpr uint32_t kRootStride3 = 272;   // 68 dwords per lane: b128 group reads are conflict-free
+// 1 + D[15].  The encoder also keeps a copy of D in LDS after the counts, so
+// that a lookup is three independent LDS reads (the symbol's 16-B group, D of
+// the groups below, the prefix mask of its position in the group from a
+// block-wide table) and no register selects; an update writes one byte (and
+// the encoder's copy of D).  The decoder finds the group with packed compares
+// on the registers (no LDS reads).
+constexpr uint32_t kRootStride3 = 304;   // counts[256], D[16] (u16), pad
+constexpr uint32_t kRootD = 256;
 
 struct Root { uint32_t d[8]; };
 
+// the block-wide table of prefix masks: entry j has bytes 0..j-1 set
+DEV void root3_mask_init(uint8_t* tab, uint32_t j)
+{
+    uint32_t w[4];
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+        const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
+        w[d] = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+    }
+    reinterpret_cast<uint4*>(tab)[j] = make_uint4(w[0], w[1], w[2], w[3]);
+}
 
+template <bool COPY>
+DEV void root3_store_d(uint8_t* r, const Root& R)
+{
+    if (COPY) {
+        uint4* p = reinterpret_cast<uint4*>(r + kRootD);
+        p[0] = make_uint4(R.d[0], R.d[1], R.d[2], R.d[3]);
+        p[1] = make_uint4(R.d[4], R.d[5], R.d[6], R.d[7]);
+    }
+}
+
+template <bool COPY>
 DEV void root3_clear(uint8_t* r, Root& R)
 {
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -380,38 +407,27 @@ DEV void root3_clear(uint8_t* r, Root& R)
     for (int i = 0; i < 16; ++i) reinterpret_cast<uint4*>(r)[i] = z;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) R.d[i] = (32 * i + 16) | ((32 * i + 32) << 16);
-}
-
-// D[t] for t in [-1, 15] (D[-1] = 0), by a masked OR (no indexed registers)
-DEV uint32_t root3_D(const Root& R, uint32_t t)
-{
-    const uint32_t i = t >> 1;
-    uint32_t w = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) w |= R.d[k] & (0u - static_cast<uint32_t>(i == k));
-    return (t & 1) ? (w >> 16) : (w & 0xFFFF);
+    root3_store_d<COPY>(r, R);
 }
 
 // under = cumulative frequency below v, cnt = count[v] (compress.c:159-199, minimum 1)
-DEV void root3_lookup(const uint8_t* r, const Root& R, uint32_t v, uint32_t& under, uint32_t& cnt)
+DEV void root3_lookup(const uint8_t* r, const uint8_t* mtab, uint32_t v, uint32_t& under, uint32_t& cnt)
 {
     const uint32_t g = v >> 4, j = v & 15;
     const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
-    uint32_t within = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) {
-        const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
-        const uint32_t mask = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-        within = sad(pick4(d, q) & mask, within);
-    }
-    cnt = (pick4(j >> 2, q) >> (8 * (j & 3))) & 0xFF;
-    under = root3_D(R, g - 1) + j + within;
+    const uint4 m = *reinterpret_cast<const uint4*>(mtab + 16 * j);
+    const uint32_t dprev = reinterpret_cast<const uint16_t*>(r + kRootD)[static_cast<int>(g) - 1];   // (g = 0: unused)
+    cnt = r[v];
+    const uint32_t within = sad(q.w & m.w, sad(q.z & m.z, sad(q.y & m.y, sad(q.x & m.x, 0u))));
+    under = (g ? dprev : 0u) + j + within;
 }
 
+template <bool COPY>
 DEV void root3_add(uint8_t* r, Root& R, uint32_t v, uint32_t cnt)
 {
     r[v] = static_cast<uint8_t>(cnt + kRootDelta);
     cum_add(R.d, v >> 4, kRootDelta);
+    root3_store_d<COPY>(r, R);
 }
 
 // Decoder: the symbol whose interval holds code (code < root total - 1):
@@ -453,6 +469,7 @@ DEV uint32_t root3_search(const uint8_t* r, const Root& R, uint32_t code, uint32
 }
 
 // compress.c:90-112 for the root: halve the counts, rebuild D; returns the new total
+template <bool COPY>
 DEV uint32_t root3_rescale(uint8_t* r, Root& R)
 {
     uint32_t sum = 0;
@@ -468,6 +485,7 @@ DEV uint32_t root3_rescale(uint8_t* r, Root& R)
         const uint32_t dg = sum + 16 * (g + 1);
         if (g & 1) R.d[g >> 1] |= dg << 16; else R.d[g >> 1] = dg;
     }
+    root3_store_d<COPY>(r, R);
     return (sum + 1 + 256) & 0xFFFF;
 }
 
@@ -655,7 +673,8 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, L
 
 // ------------------------------------------------------------ one packet
 
-DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg, uint8_t* root)
+DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg, uint8_t* root,
+                       const uint8_t* mtab)
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
@@ -669,7 +688,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
     Lane L;
     lane_init(L, reg);
     Root R;
-    root3_clear(root, R);
+    root3_clear<true>(root, R);
     uint32_t rtot = 1 + 256;
     uint32_t low = 0, range = ~0u;
     bool ok = true;
@@ -681,6 +700,9 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         PROF(9)
 #endif
         const uint32_t v = src_byte(in);
+        // the root lookup only needs v: its LDS latency overlaps the steps below
+        uint32_t under0, cnt0;
+        root3_lookup(root, mtab, v, under0, cnt0);
         lane_top(L);
         sink_flush(o);
         src_refill(in, true);
@@ -712,13 +734,11 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         PROF(4)
         // root, compress.c:318-329
         const bool en0 = !done2 && !done1;
-        uint32_t under0, cnt0;
-        root3_lookup(root, R, v, under0, cnt0);
-        if (en0) root3_add(root, R, v, cnt0);
+        if (en0) root3_add<true>(root, R, v, cnt0);
         enc_code(low, range, 1 + under0, 1 + cnt0, rtot, o, en0, ok);
         rtot = en0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
         const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit);
-        if (any_lane(rs0)) { if (rs0) rtot = root3_rescale(root, R); }
+        if (any_lane(rs0)) { if (rs0) rtot = root3_rescale<true>(root, R); }
         PROF(5)
         // no loop exit between the record load (lane_prefetch) and the record
         // store (lane_advance): an exit path there makes the compiler's vmcnt
@@ -756,7 +776,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     Lane L;
     lane_init(L, reg);
     Root R;
-    root3_clear(root, R);
+    root3_clear<false>(root, R);
     uint32_t rtot = 1 + 256;
     uint32_t low = 0, range = ~0u;
     uint32_t code = static_cast<uint32_t>(in.la >> 32);            // compress.c:344-350 (0 past the end)
@@ -820,10 +840,10 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (cd - 1 >= rtot - 1) { anomaly = true; break; }           // past symbol 255
             uint32_t under, cnt;
             v = root3_search(root, R, cd - 1, under, cnt);
-            root3_add(root, R, v, cnt);
+            root3_add<false>(root, R, v, cnt);
             dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
             rtot = (rtot + kRootDelta) & 0xFFFF;
-            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale(root, R);
+            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
             at = 0;
         }
         PROF(3)
@@ -869,6 +889,11 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t act = ws.lane_active;
     const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+    uint8_t* mtab = smem + 4 * act * kRootStride3;
+    if (!DECOMP) {
+        if (threadIdx.x < 16) root3_mask_init(mtab, threadIdx.x);
+        __syncthreads();
+    }
     if (l >= act) return;
     const uint32_t local = wave * act + l;
     uint8_t* root = smem + local * kRootStride3;
@@ -879,7 +904,7 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
         const uint32_t pkt = order ? order[i] : i;
         if (DECOMP) decompress_one3(b, ws, pkt, reg, root);
-        else compress_one3(b, ws, pkt, reg, root);
+        else compress_one3(b, ws, pkt, reg, root, mtab);
     }
 }
 
@@ -895,7 +920,7 @@ extern "C" int rc_hip_lane3_launch(int decompress, const rc_batch_dev* b, const 
                                    uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStride3;
+    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStride3 + 256;   // + the mask table
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane3, dim3(blocks), dim3(256), lds, st, *b, *ws);
     else

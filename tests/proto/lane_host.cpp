@@ -15,6 +15,13 @@
 #endif
 
 static uint8_t g_root[304] __attribute__((aligned(16)));
+#ifdef LANE3
+static uint8_t g_mtab[256] __attribute__((aligned(16)));
+static bool g_mtab_init = [] { for (uint32_t j = 0; j < 16; ++j) root3_mask_init(g_mtab, j); return true; }();
+#define COMPRESS_ARGS , g_mtab
+#else
+#define COMPRESS_ARGS
+#endif
 
 extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t cap,
                              uint32_t max_len, uint32_t* out_len)
@@ -33,6 +40,6 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     ws.flag_list = flags; ws.counters = counters; ws.lane_region = need; ws.lane_pool = region; ws.lane_active = 64;
     *out_len = 0xFFFFFFFFu;
     if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root);
-    else COMPRESS_ONE(b, ws, 0, region, g_root);
+    else COMPRESS_ONE(b, ws, 0, region, g_root COMPRESS_ARGS);
     return counters[0] ? 1 : 0;   // 1 = routed to the exact path
 }
