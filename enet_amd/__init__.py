@@ -132,6 +132,63 @@ class RangeCoder:
             raise RuntimeError(f"enet_rc_crc32_batch_host failed: HIP error {rc}")
         return int(out[0])
 
+    def _dgram(self, fn, inp, in_off, in_len, out, out_off, out_len, checksum, seed, stream):
+        import torch
+        for t in (inp, in_off, in_len, out, out_off, out_len):
+            if not (t.is_cuda and t.is_contiguous()):
+                raise ValueError("datagram tensors must be contiguous device tensors")
+        assert inp.dtype == torch.uint8 and out.dtype == torch.uint8
+        assert in_off.dtype == torch.int64 and out_off.dtype == torch.int64
+        assert in_len.dtype == torch.int32 and out_len.dtype == torch.int32
+        n = in_len.numel()
+        if checksum:
+            assert seed is not None and seed.is_cuda and seed.dtype == torch.int32 and seed.numel() >= n
+        if stream is None:
+            stream = torch.cuda.current_stream(inp.device)
+        rc = fn(self.ctx, inp.data_ptr(), in_off.data_ptr(), in_len.data_ptr(), n, 1 if checksum else 0,
+                seed.data_ptr() if checksum else None, out.data_ptr(), out_off.data_ptr(), out_len.data_ptr(),
+                C.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"enet_rc datagram batch failed: HIP error {rc}")
+
+    def datagram_encode_batch(self, inp, in_off, in_len, out, out_off, out_len, checksum=False, seed=None,
+                              stream=None):
+        """protocol.c:1686-1718 for n assembled datagrams (device tensors): wire
+        datagrams into out at out_off (slot >= in_len), lengths into out_len.
+        seed: int32 tensor of connectIDs (or 0) when checksum."""
+        self._dgram(self.lib.enet_rc_datagram_encode_batch_device, inp, in_off, in_len, out, out_off, out_len,
+                    checksum, seed, stream)
+
+    def datagram_decode_batch(self, inp, in_off, in_len, out, out_off, out_len, checksum=False, seed=None,
+                              stream=None):
+        """protocol.c:1022-1091 for n received datagrams (device tensors): 4096-B
+        slots of out at out_off get header + commands; out_len 0 = dropped."""
+        self._dgram(self.lib.enet_rc_datagram_decode_batch_device, inp, in_off, in_len, out, out_off, out_len,
+                    checksum, seed, stream)
+
+    def datagrams(self, decode: bool, datagrams, checksum=False, seeds=None):
+        """Host-memory convenience over the *_batch_host calls: list of bytes in,
+        list of bytes out (b"" where protocol.c drops the datagram)."""
+        import numpy as np
+        n = len(datagrams)
+        if n == 0:
+            return []
+        ln = np.array([len(d) for d in datagrams], np.uint32)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+        blob = np.frombuffer(b"".join(datagrams) + b"\0" * 16, np.uint8).copy()
+        slot = 4096 if decode else int(max(ln.max(), 1))
+        out_off = (np.arange(n, dtype=np.uint64) * np.uint64(slot))
+        out = np.zeros(n * slot + 16, np.uint8)
+        out_len = np.zeros(n, np.uint32)
+        sd = np.asarray(seeds if seeds is not None else np.zeros(n), dtype=np.uint32)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        fn = self.lib.enet_rc_datagram_decode_batch_host if decode else self.lib.enet_rc_datagram_encode_batch_host
+        rc = fn(self.ctx, p(blob), p(off), p(ln), n, 1 if checksum else 0, p(sd), p(out), p(out_off), p(out_len))
+        if rc != 0:
+            raise RuntimeError(f"enet_rc datagram host batch failed: HIP error {rc}")
+        return [out[int(out_off[i]): int(out_off[i]) + int(out_len[i])].tobytes() for i in range(n)]
+
     def last_exact_count(self) -> int:
         return int(self.lib.enet_rc_last_exact_count(self.ctx))
 

@@ -55,6 +55,19 @@ def _load() -> C.CDLL:
     lib.enet_rc_crc32_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
     lib.enet_rc_crc32_batch_host.restype = C.c_int
     lib.enet_rc_crc32_batch_host.argtypes = [vp, vp, vp, vp, sz, vp]
+    dg_dev = [vp, vp, vp, vp, sz, C.c_int, vp, vp, vp, vp, vp]
+    dg_host = [vp, vp, vp, vp, sz, C.c_int, vp, vp, vp, vp]
+    for name, args in (("enet_rc_datagram_encode_batch_device", dg_dev),
+                       ("enet_rc_datagram_decode_batch_device", dg_dev),
+                       ("enet_rc_datagram_encode_batch_host", dg_host),
+                       ("enet_rc_datagram_decode_batch_host", dg_host)):
+        f = getattr(lib, name)
+        f.restype = C.c_int
+        f.argtypes = args
+    lib.enet_rc_socket_receive_batch.restype = C.c_int
+    lib.enet_rc_socket_receive_batch.argtypes = [C.c_int, vp, sz, sz, vp, vp]
+    lib.enet_rc_socket_send_batch.restype = C.c_int
+    lib.enet_rc_socket_send_batch.argtypes = [C.c_int, vp, vp, vp, vp, sz]
     lib.enet_rc_crc32.restype = u32
     lib.enet_rc_crc32.argtypes = [C.POINTER(ENetBuffer), sz]
     lib.enet_rc_last_exact_count.restype = u32

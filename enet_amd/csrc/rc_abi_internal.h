@@ -66,6 +66,34 @@ int rc_hip_crc32(const uint8_t *in, const uint64_t *in_off, const uint32_t *in_l
 uint32_t rc_hip_crc32_table_words(void);
 void rc_hip_crc32_build_tables(uint32_t *t);
 
+/* Datagram framing (rc_dgram.hip).  All pointers in
+ * device memory; p_*, q_*, c_len, s_*, crc, want are workspace arrays of n. */
+typedef struct {
+    const uint8_t  *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    uint8_t        *out;
+    const uint64_t *out_off;
+    uint32_t       *out_len;
+    const uint32_t *seed;       /* checksum field value while summing: connectID or 0 */
+    uint64_t       *p_off;      /* command range of each datagram (coder input) */
+    uint32_t       *p_len;
+    uint64_t       *q_off;      /* its slot in out (coder output) */
+    uint32_t       *q_cap;
+    uint32_t       *c_len;      /* coder result */
+    uint8_t        *scratch;    /* encode: n x 4096 B, the datagrams the checksum covers */
+    uint64_t       *s_off;
+    uint32_t       *s_len;
+    uint32_t       *crc;
+    uint32_t       *want;       /* decode: received checksum field */
+    uint32_t        n;
+    uint32_t        checksum;   /* the host has a checksum callback (4-B field in the header) */
+} rc_dgram_dev;
+
+enum { RC_DGRAM_ENC_PREP = 0, RC_DGRAM_ENC_STAGE, RC_DGRAM_ENC_FINISH,
+       RC_DGRAM_DEC_PREP, RC_DGRAM_DEC_STAGE, RC_DGRAM_DEC_FINISH };
+int rc_hip_dgram_launch(int stage, const rc_dgram_dev *g, void *stream);
+
 /* Kernel introspection for bench/profiling. */
 const char *rc_hip_fast_kernel_name(int decompress, uint32_t kernel);
 uint32_t    rc_hip_lds_bytes(uint32_t max_len);

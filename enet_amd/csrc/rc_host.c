@@ -43,6 +43,11 @@ typedef struct {
     uint32_t last_exact;
     uint32_t max_slots;             /* lanes with a model region (ENET_RC_SLOTS) */
     uint32_t *crc_tables;           /* device: slice-by-16 + shift tables (rc_crc32.hip) */
+    /* datagram framing workspace (rc_dgram.hip): per-datagram arrays + checksum scratch */
+    uint8_t *dg_arrays;
+    size_t dg_cap;
+    uint8_t *dg_scratch;
+    size_t dg_scratch_cap;
 } rc_ctx;
 
 static void *ctx_alloc(size_t n) { return enet_malloc ? enet_malloc(n) : malloc(n); }
@@ -165,6 +170,8 @@ void enet_range_coder_destroy(void *context)
     if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
     if (c->crc_tables) hipFree(c->crc_tables);
+    if (c->dg_arrays) hipFree(c->dg_arrays);
+    if (c->dg_scratch) hipFree(c->dg_scratch);
     if (c->d_stage) hipFree(c->d_stage);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -273,6 +280,152 @@ int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64
                                   const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
     return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+}
+
+/* --------------------------------------------------- datagram framing (§8f) */
+
+#define DG_MTU 4096u                /* ENET_PROTOCOL_MAXIMUM_MTU (protocol.h:13) */
+
+static int dgram_reserve(rc_ctx *c, size_t n, int scratch)
+{
+    if (n > c->dg_cap) {
+        size_t cap = c->dg_cap ? c->dg_cap : 1024;
+        while (cap < n) cap *= 2;
+        hipStreamSynchronize(c->stream);
+        if (c->dg_arrays) hipFree(c->dg_arrays);
+        c->dg_arrays = NULL; c->dg_cap = 0;
+        if (hipMalloc((void **) &c->dg_arrays, cap * (3 * 8 + 6 * 4)) != hipSuccess) return -1;
+        c->dg_cap = cap;
+    }
+    if (scratch && n * DG_MTU > c->dg_scratch_cap) {
+        hipStreamSynchronize(c->stream);
+        if (c->dg_scratch) hipFree(c->dg_scratch);
+        c->dg_scratch = NULL; c->dg_scratch_cap = 0;
+        if (hipMalloc((void **) &c->dg_scratch, n * DG_MTU) != hipSuccess) return -1;
+        c->dg_scratch_cap = n * DG_MTU;
+    }
+    return 0;
+}
+
+/* protocol.c:1686-1718 (send) or :1022-1091 (receive) for a batch of whole
+ * datagrams: frame, code the command ranges with the lane kernels, checksum. */
+static int run_dgram(rc_ctx *c, int decode, const uint8_t *in, const uint64_t *in_off,
+                     const uint32_t *in_len, size_t n, int checksum, const uint32_t *seed,
+                     uint8_t *out, const uint64_t *out_off, uint32_t *out_len, void *stream)
+{
+    if (!c || n > 0xFFFFFFFFu || (checksum && !seed)) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    if (dgram_reserve(c, n, checksum && !decode) != 0) return (int) hipErrorOutOfMemory;
+    uint8_t *a = c->dg_arrays;
+    const size_t cap = c->dg_cap;
+    rc_dgram_dev g;
+    g.in = in; g.in_off = in_off; g.in_len = in_len;
+    g.out = out; g.out_off = out_off; g.out_len = out_len;
+    g.seed = seed;
+    g.p_off = (uint64_t *) a;
+    g.q_off = (uint64_t *) (a + cap * 8);
+    g.s_off = (uint64_t *) (a + cap * 16);
+    g.p_len = (uint32_t *) (a + cap * 24);
+    g.q_cap = (uint32_t *) (a + cap * 28);
+    g.c_len = (uint32_t *) (a + cap * 32);
+    g.s_len = (uint32_t *) (a + cap * 36);
+    g.crc = (uint32_t *) (a + cap * 40);
+    g.want = (uint32_t *) (a + cap * 44);
+    g.scratch = c->dg_scratch;
+    g.n = (uint32_t) n;
+    g.checksum = checksum ? 1u : 0u;
+    int rc = rc_hip_dgram_launch(decode ? RC_DGRAM_DEC_PREP : RC_DGRAM_ENC_PREP, &g, stream);
+    if (rc) return rc;
+    rc = run_device(c, decode, in, g.p_off, g.p_len, n, DG_MTU, out, g.q_off, g.q_cap, g.c_len, stream);
+    if (rc) return rc;
+    rc = rc_hip_dgram_launch(decode ? RC_DGRAM_DEC_STAGE : RC_DGRAM_ENC_STAGE, &g, stream);
+    if (rc) return rc;
+    if (checksum) {
+        rc = decode ? rc_hip_crc32(out, out_off, g.s_len, (uint32_t) n, g.crc, c->crc_tables, stream)
+                    : rc_hip_crc32(g.scratch, g.s_off, g.s_len, (uint32_t) n, g.crc, c->crc_tables, stream);
+        if (rc) return rc;
+        rc = rc_hip_dgram_launch(decode ? RC_DGRAM_DEC_FINISH : RC_DGRAM_ENC_FINISH, &g, stream);
+    }
+    return rc;
+}
+
+int enet_rc_datagram_encode_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                                         const uint32_t *in_len, size_t n, int checksum,
+                                         const uint32_t *seed, uint8_t *out, const uint64_t *out_off,
+                                         uint32_t *out_len, void *stream)
+{
+    return run_dgram((rc_ctx *) context, 0, in, in_off, in_len, n, checksum, seed, out, out_off,
+                     out_len, stream);
+}
+
+int enet_rc_datagram_decode_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                                         const uint32_t *in_len, size_t n, int checksum,
+                                         const uint32_t *seed, uint8_t *out, const uint64_t *out_off,
+                                         uint32_t *out_len, void *stream)
+{
+    return run_dgram((rc_ctx *) context, 1, in, in_off, in_len, n, checksum, seed, out, out_off,
+                     out_len, stream);
+}
+
+/* Host-pointer variants: one pinned staging area, H2D, the device path, D2H
+ * of the lengths and of each slot's used bytes only. */
+static int run_dgram_host(rc_ctx *c, int decode, const uint8_t *in, const uint64_t *in_off,
+                          const uint32_t *in_len, size_t n, int checksum, const uint32_t *seed,
+                          uint8_t *out, const uint64_t *out_off, uint32_t *out_len)
+{
+    if (!c || n > 0xFFFFFFFFu || (checksum && !seed)) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    uint64_t in_bytes = 0, out_bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t e = in_off[i] + in_len[i];
+        if (e > in_bytes) in_bytes = e;
+        uint64_t f = out_off[i] + (decode ? DG_MTU : in_len[i]);
+        if (f > out_bytes) out_bytes = f;
+    }
+    size_t a_ioff = (in_bytes + 15) & ~(size_t) 15;
+    size_t a_ilen = a_ioff + n * 8;
+    size_t a_seed = (a_ilen + n * 4 + 15) & ~(size_t) 15;
+    size_t a_ooff = (a_seed + n * 4 + 15) & ~(size_t) 15;
+    size_t a_olen = (a_ooff + n * 8 + 15) & ~(size_t) 15;
+    size_t a_out = (a_olen + n * 4 + 15) & ~(size_t) 15;
+    size_t total = a_out + out_bytes + 16;
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    if (stage_reserve(c, total) != 0) return (int) hipErrorOutOfMemory;
+    uint8_t *h = c->h_stage, *d = c->d_stage;
+    memcpy(h, in, in_bytes);
+    memcpy(h + a_ioff, in_off, n * 8);
+    memcpy(h + a_ilen, in_len, n * 4);
+    if (checksum) memcpy(h + a_seed, seed, n * 4);
+    memcpy(h + a_ooff, out_off, n * 8);
+    hipError_t err = hipMemcpyAsync(d, h, a_olen, hipMemcpyHostToDevice, c->stream);
+    if (err != hipSuccess) return (int) err;
+    int rc = run_dgram(c, decode, d, (const uint64_t *) (d + a_ioff), (const uint32_t *) (d + a_ilen), n,
+                       checksum, (const uint32_t *) (d + a_seed), d + a_out, (const uint64_t *) (d + a_ooff),
+                       (uint32_t *) (d + a_olen), (void *) c->stream);
+    if (rc) return rc;
+    err = hipMemcpyAsync(h + a_olen, d + a_olen, total - 16 - a_olen, hipMemcpyDeviceToHost, c->stream);
+    if (err != hipSuccess) return (int) err;
+    err = hipStreamSynchronize(c->stream);
+    if (err != hipSuccess) return (int) err;
+    memcpy(out_len, h + a_olen, n * 4);
+    for (size_t i = 0; i < n; ++i)
+        if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
+    return 0;
+}
+
+int enet_rc_datagram_encode_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                                       const uint32_t *in_len, size_t n, int checksum, const uint32_t *seed,
+                                       uint8_t *out, const uint64_t *out_off, uint32_t *out_len)
+{
+    return run_dgram_host((rc_ctx *) context, 0, in, in_off, in_len, n, checksum, seed, out, out_off, out_len);
+}
+
+int enet_rc_datagram_decode_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                                       const uint32_t *in_len, size_t n, int checksum, const uint32_t *seed,
+                                       uint8_t *out, const uint64_t *out_off, uint32_t *out_len)
+{
+    return run_dgram_host((rc_ctx *) context, 1, in, in_off, in_len, n, checksum, seed, out, out_off, out_len);
 }
 
 /* ------------------------------------------------------------------ CRC-32 */

@@ -39,6 +39,7 @@ typedef struct _ENetCompressor {
     void (*destroy)(void *context);
 } ENetCompressor;
 typedef struct _ENetHost ENetHost;
+typedef struct _ENetAddress { enet_uint32 host; enet_uint16 port; } ENetAddress;   /* enet.h:85-89 */
 #endif
 
 /* =================================================================== drop-in
@@ -111,6 +112,60 @@ int enet_rc_crc32_batch_host(void *context, const uint8_t *in, const uint64_t *i
  * host->checksum = enet_rc_crc32.  Uses a process-wide GPU context; aborts if
  * no GPU is usable (there is no CPU fallback). */
 enet_uint32 enet_rc_crc32(const ENetBuffer *buffers, size_t bufferCount);
+
+/* ========================================================= datagram framing
+ * Whole ENet wire datagrams in and out: the framing
+ * of protocol.c around the compressor and checksum callbacks, for n datagrams
+ * in one pass.  Layout (protocol.h:48-53): big-endian peerID word (bit 14
+ * COMPRESSED, bit 15 SENT_TIME), big-endian sentTime if SENT_TIME, a 4-byte
+ * checksum field if `checksum` (the host has a checksum callback), then the
+ * commands.  seed[i] is the value the checksum field holds while summing: the
+ * peer's connectID, or 0 for peerID 0xFFF (protocol.c:1079, :1711); it may be
+ * NULL when checksum == 0.  Datagrams are at most 4096 bytes
+ * (ENET_PROTOCOL_MAXIMUM_MTU).
+ *
+ * Encode replaces protocol.c:1686-1718 for each datagram: in[i] is the
+ * datagram as assembled (header, checksum field, uncompressed commands; the
+ * COMPRESSED bit is ignored); out[out_off[i] ..] receives the wire datagram --
+ * commands range-coded with outLimit = their length and used only if smaller
+ * (COMPRESSED set), checksum (enet_crc32 of the uncompressed datagram with
+ * the final header and the seed in the field) filled in; out_len[i] is its
+ * length (<= in_len[i]), 0 if the datagram is shorter than its header.
+ *
+ * Decode replaces protocol.c:1022-1091: in[i] is a received datagram;
+ * out[out_off[i] ..] (4096 bytes per slot) receives what protocol.c goes on
+ * parsing -- header + decompressed commands, checksum field holding the seed
+ * -- and out_len[i] its length, or 0 where protocol.c drops the datagram
+ * (shorter than 2 bytes or its header, decompression failing or longer than
+ * 4096 - headerSize, checksum mismatch).  Peer-state checks (:1035-1050) stay
+ * with the caller.  Return value as for the batch calls. */
+int enet_rc_datagram_encode_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                                         const uint32_t *in_len, size_t n, int checksum,
+                                         const uint32_t *seed, uint8_t *out, const uint64_t *out_off,
+                                         uint32_t *out_len, void *stream);
+int enet_rc_datagram_decode_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
+                                         const uint32_t *in_len, size_t n, int checksum,
+                                         const uint32_t *seed, uint8_t *out, const uint64_t *out_off,
+                                         uint32_t *out_len, void *stream);
+int enet_rc_datagram_encode_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                                       const uint32_t *in_len, size_t n, int checksum, const uint32_t *seed,
+                                       uint8_t *out, const uint64_t *out_off, uint32_t *out_len);
+int enet_rc_datagram_decode_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
+                                       const uint32_t *in_len, size_t n, int checksum, const uint32_t *seed,
+                                       uint8_t *out, const uint64_t *out_off, uint32_t *out_len);
+
+/* ============================================================ batched I/O
+ * enet_socket_receive / enet_socket_send (unix.c:440-528) for many datagrams
+ * per system call (recvmmsg / sendmmsg), non-blocking.  Receive: up to max
+ * datagrams into buf + i * slot_bytes, lengths[i] (0 for a truncated one,
+ * which the reference skips, unix.c:509-512), addresses[i] (may be NULL);
+ * returns the count (0 if none is queued) or -1.  Send: datagram i is
+ * buf[off[i] .. +len[i]) to addresses[i] (NULL: a connected socket); returns
+ * how many went out, or -1.  Host memory only; no GPU needed. */
+int enet_rc_socket_receive_batch(int socket, uint8_t *buf, size_t slot_bytes, size_t max,
+                                 uint32_t *lengths, ENetAddress *addresses);
+int enet_rc_socket_send_batch(int socket, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                              const ENetAddress *addresses, size_t n);
 
 /* ============================================================ introspection */
 /* Number of packets of the last batch that took the exact (binary-tree) path. */

@@ -206,3 +206,65 @@ def crc32_batch(data: np.ndarray, off: np.ndarray, ln: np.ndarray, kind: str = "
         buf[0].dataLength = int(ln[i])
         out[i] = lib.enet_crc32(buf, 1)
     return out
+
+
+# ----------------------------------------------------------- datagram framing
+# Restatement of protocol.c's framing around the compressor and checksum
+# callbacks -- test oracle for
+# enet_rc_datagram_{encode,decode}_batch_*.
+MTU = 4096                      # ENET_PROTOCOL_MAXIMUM_MTU (protocol.h:13) = sizeof packetData[1]
+
+
+def _header_size(b0: int, checksum: bool) -> int:
+    # protocol.c:1033-1035: 2 bytes, 4 with SENT_TIME (bit 15), + 4 for the checksum
+    return (4 if b0 & 0x80 else 2) + (4 if checksum else 0)
+
+
+def _crc(data: bytes, kind: str = "port") -> int:
+    arr = np.frombuffer(bytes(data) + b"\0", np.uint8)
+    return int(crc32_batch(arr, np.zeros(1, np.uint64), np.array([len(data)], np.uint32), kind)[0])
+
+
+def datagram_encode(dgram: bytes, checksum: bool, seed: int, coder: "Coder") -> bytes:
+    """protocol.c:1686-1718 for one assembled datagram (header, checksum field,
+    uncompressed commands).  b"" for a datagram shorter than its header."""
+    if len(dgram) < 2 or len(dgram) > MTU:
+        return b""
+    hs = _header_size(dgram[0], checksum)
+    if len(dgram) < hs:
+        return b""
+    cmds = dgram[hs:]
+    L = len(cmds)
+    c, packed = coder.compress(cmds, out_limit=L, in_limit=L) if L else (0, b"")   # :1688-1694
+    comp = 0 < c < L                                                                 # :1696
+    b0 = (dgram[0] & ~0x40) | (0x40 if comp else 0)                                  # :1698, :1708
+    head = bytes([b0]) + dgram[1:hs - (4 if checksum else 0)]
+    if checksum:                                                                     # :1709-1718
+        crc = _crc(head + int(seed).to_bytes(4, "little") + cmds)
+        head += crc.to_bytes(4, "little")
+    return head + (packed if comp else cmds)
+
+
+def datagram_decode(wire: bytes, checksum: bool, seed: int, coder: "Coder") -> bytes:
+    """protocol.c:1022-1091 for one received datagram: the bytes it goes on to
+    parse (header + commands, checksum field = seed), or b"" where it drops it."""
+    if len(wire) < 2:                                                                # :1022-1023
+        return b""
+    hs = _header_size(wire[0], checksum)
+    if len(wire) < hs:
+        return b""
+    if wire[0] & 0x40:                                                               # :1052-1070
+        r, data = coder.decompress(wire[hs:], MTU - hs)
+        if r <= 0 or r > MTU - hs:
+            return b""
+        d = wire[:hs] + data
+    else:
+        if len(wire) > MTU:
+            return b""
+        d = bytes(wire)
+    if checksum:                                                                     # :1072-1091
+        want = int.from_bytes(d[hs - 4:hs], "little")
+        d = d[:hs - 4] + int(seed).to_bytes(4, "little") + d[hs:]
+        if _crc(d) != want:
+            return b""
+    return d

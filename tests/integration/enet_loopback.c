@@ -58,12 +58,43 @@ static double now(void)
     return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
+/* ENET_LOOPBACK_DUMP=path: every received datagram (as on the wire) and the
+ * checksum seed protocol.c would use for it (:1079) are appended to path as
+ * JSON lines, through the host's intercept hook (protocol.c:1259-1274); used
+ * by tests/golden/make_dgram_golden.py to pin the datagram framing to real
+ * ENet traffic.  ENET_LOOPBACK_CHECKSUM=1 enables enet_crc32 (enet.h:564). */
+static FILE *g_dump;
+
+static int ENET_CALLBACK dump_datagram(ENetHost *host, ENetEvent *event)
+{
+    (void) event;
+    const enet_uint8 *d = host->receivedData;
+    size_t n = host->receivedDataLength;
+    enet_uint32 seed = 0;
+    if (n >= 2) {
+        unsigned pid = (((unsigned) d[0] << 8) | d[1]) & 0x0FFFu;
+        if (pid != 0x0FFFu && pid < host->peerCount) seed = host->peers[pid].connectID;
+    }
+    fprintf(g_dump, "{\"checksum\": %d, \"seed\": %u, \"wire\": \"", host->checksum != NULL, seed);
+    for (size_t i = 0; i < n; ++i) fprintf(g_dump, "%02x", d[i]);
+    fprintf(g_dump, "\"}\n");
+    return 0;   /* protocol.c goes on handling it */
+}
+
 static ENetHost *mk_host(const ENetAddress *a, int *rc)
 {
     ENetHost *h = enet_host_create(a, 4, 2, 0, 0);
     if (!h) { fprintf(stderr, "enet_host_create failed\n"); exit(2); }
     *rc = enet_host_compress_with_range_coder(h);
     if (*rc != 0) { fprintf(stderr, "enet_host_compress_with_range_coder = %d\n", *rc); exit(3); }
+    const char *ck = getenv("ENET_LOOPBACK_CHECKSUM");
+    if (ck && atoi(ck)) h->checksum = enet_crc32;
+    const char *dp = getenv("ENET_LOOPBACK_DUMP");
+    if (dp) {
+        if (!g_dump) g_dump = fopen(dp, "w");
+        if (!g_dump) { fprintf(stderr, "cannot open %s\n", dp); exit(2); }
+        h->intercept = dump_datagram;
+    }
     return h;
 }
 
@@ -174,5 +205,6 @@ int main(int argc, char **argv)
     if (server) enet_host_destroy(sv.host);
     if (client) enet_host_destroy(cl.host);
     enet_deinitialize();
+    if (g_dump) fclose(g_dump);
     return ok ? 0 : 1;
 }
