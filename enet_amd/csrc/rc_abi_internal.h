@@ -94,6 +94,11 @@ enum { RC_DGRAM_ENC_PREP = 0, RC_DGRAM_ENC_STAGE, RC_DGRAM_ENC_FINISH,
        RC_DGRAM_DEC_PREP, RC_DGRAM_DEC_STAGE, RC_DGRAM_DEC_FINISH };
 int rc_hip_dgram_launch(int stage, const rc_dgram_dev *g, void *stream);
 
+/* Pack out_len[i] bytes of each packet (at out_off[i]) back to back into
+ * packed (rc_pack.hip); bsum: ceil(n / 1024) + 1 words, bsum[last] = total. */
+int rc_hip_pack(const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len, uint32_t n,
+                uint64_t *bsum, uint8_t *packed, void *stream);
+
 /* Kernel introspection for bench/profiling. */
 const char *rc_hip_fast_kernel_name(int decompress, uint32_t kernel);
 uint32_t    rc_hip_lds_bytes(uint32_t max_len);

@@ -48,6 +48,11 @@ typedef struct {
     size_t dg_cap;
     uint8_t *dg_scratch;
     size_t dg_scratch_cap;
+    /* host-pointer calls: outputs packed back to back before D2H (rc_pack.hip) */
+    uint8_t *d_pack;
+    size_t d_pack_cap;
+    uint64_t *d_bsum;
+    size_t d_bsum_cap;
 } rc_ctx;
 
 static void *ctx_alloc(size_t n) { return enet_malloc ? enet_malloc(n) : malloc(n); }
@@ -172,6 +177,8 @@ void enet_range_coder_destroy(void *context)
     if (c->crc_tables) hipFree(c->crc_tables);
     if (c->dg_arrays) hipFree(c->dg_arrays);
     if (c->dg_scratch) hipFree(c->dg_scratch);
+    if (c->d_pack) hipFree(c->d_pack);
+    if (c->d_bsum) hipFree(c->d_bsum);
     if (c->d_stage) hipFree(c->d_stage);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -218,6 +225,97 @@ int enet_rc_decompress_batch_device(void *context, const uint8_t *in, const uint
 
 /* Host-memory batch: [in | in_off | in_len | out_off | out_cap | out_len | out]
  * packed into one pinned buffer, one H2D, kernels, one D2H of out_len+out. */
+/* ---- host-side copies on several threads (the staging memcpy in and the
+ * scatter of the packed results out are the largest host costs) */
+typedef struct {
+    int kind;                       /* 0: memcpy range, 1: scatter packets */
+    uint8_t *dst;
+    const uint8_t *src;
+    size_t bytes;
+    const uint64_t *out_off, *poff;
+    const uint32_t *len;
+    size_t lo, hi;
+} copy_job;
+
+static void *copy_worker(void *p)
+{
+    copy_job *j = (copy_job *) p;
+    if (j->kind == 0) {
+        memcpy(j->dst, j->src, j->bytes);
+    } else {
+        for (size_t i = j->lo; i < j->hi; ++i)
+            if (j->len[i]) memcpy(j->dst + j->out_off[i], j->src + j->poff[i], j->len[i]);
+    }
+    return NULL;
+}
+
+#define COPY_THREADS 8
+#define COPY_MIN_BYTES (4u << 20)
+
+static void par_run(copy_job *jobs, int k)
+{
+    pthread_t t[COPY_THREADS];
+    int started[COPY_THREADS] = {0};
+    for (int i = 1; i < k; ++i) started[i] = pthread_create(&t[i], NULL, copy_worker, &jobs[i]) == 0;
+    copy_worker(&jobs[0]);
+    for (int i = 1; i < k; ++i) {
+        if (started[i]) pthread_join(t[i], NULL);
+        else copy_worker(&jobs[i]);
+    }
+}
+
+static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
+{
+    int k = bytes >= COPY_MIN_BYTES ? COPY_THREADS : 1;
+    copy_job jobs[COPY_THREADS];
+    size_t per = (bytes + k - 1) / k;
+    for (int i = 0; i < k; ++i) {
+        size_t lo = (size_t) i * per, hi = lo + per < bytes ? lo + per : bytes;
+        jobs[i].kind = 0;
+        jobs[i].dst = dst + lo; jobs[i].src = src + lo; jobs[i].bytes = hi > lo ? hi - lo : 0;
+    }
+    par_run(jobs, k);
+}
+
+/* packets [lo, hi): out + out_off[i] <- packed + poff[i], len[i] bytes */
+static void par_scatter(uint8_t *out, const uint64_t *out_off, const uint8_t *packed, const uint64_t *poff,
+                        const uint32_t *len, size_t lo, size_t hi, uint64_t bytes)
+{
+    int k = bytes >= COPY_MIN_BYTES ? COPY_THREADS : 1;
+    copy_job jobs[COPY_THREADS];
+    const size_t n = hi - lo, per = (n + k - 1) / k;
+    for (int i = 0; i < k; ++i) {
+        jobs[i].kind = 1;
+        jobs[i].dst = out; jobs[i].src = packed; jobs[i].out_off = out_off; jobs[i].poff = poff; jobs[i].len = len;
+        jobs[i].lo = lo + ((size_t) i * per < n ? (size_t) i * per : n);
+        jobs[i].hi = lo + ((size_t) (i + 1) * per < n ? (size_t) (i + 1) * per : n);
+    }
+    par_run(jobs, k);
+}
+
+static int pack_reserve(rc_ctx *c, size_t bytes, size_t blocks)
+{
+    if (bytes > c->d_pack_cap) {
+        hipStreamSynchronize(c->stream);
+        if (c->d_pack) hipFree(c->d_pack);
+        c->d_pack = NULL; c->d_pack_cap = 0;
+        if (hipMalloc((void **) &c->d_pack, bytes) != hipSuccess) return -1;
+        c->d_pack_cap = bytes;
+    }
+    if (blocks + 1 > c->d_bsum_cap) {
+        hipStreamSynchronize(c->stream);
+        if (c->d_bsum) hipFree(c->d_bsum);
+        c->d_bsum = NULL; c->d_bsum_cap = 0;
+        if (hipMalloc((void **) &c->d_bsum, (blocks + 1) * 8) != hipSuccess) return -1;
+        c->d_bsum_cap = blocks + 1;
+    }
+    return 0;
+}
+
+/* Host pointers: inputs copied (on several threads) into pinned staging, one
+ * H2D, the device path, then the results packed back to back on the device
+ * (rc_pack.hip) so that only the produced bytes cross PCIe, and scattered to
+ * out_off on the host. */
 static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
                     const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
                     const uint32_t *out_cap, uint32_t *out_len)
@@ -243,29 +341,77 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     size_t total = a_out + out_bytes + 16;
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
     if (stage_reserve(c, total) != 0) return (int) hipErrorOutOfMemory;
+    const size_t blocks = (n + 1023) / 1024;
+    if (pack_reserve(c, out_bytes + 16, blocks) != 0) return (int) hipErrorOutOfMemory;
     uint8_t *h = c->h_stage, *d = c->d_stage;
-    memcpy(h + a_in, in, in_bytes);
     memcpy(h + a_ioff, in_off, n * 8);
     memcpy(h + a_ilen, in_len, n * 4);
     memcpy(h + a_ooff, out_off, n * 8);
     memcpy(h + a_ocap, out_cap, n * 4);
-    hipError_t err = hipMemcpyAsync(d, h, a_olen, hipMemcpyHostToDevice, c->stream);
+    hipError_t err = hipMemcpyAsync(d + a_ioff, h + a_ioff, a_olen - a_ioff, hipMemcpyHostToDevice, c->stream);
     if (err != hipSuccess) return (int) err;
+    /* the payload in chunks: the staging copy of chunk k+1 overlaps the DMA of chunk k */
+    const size_t chunk = in_bytes >= (16u << 20) ? (in_bytes + 3) / 4 : in_bytes;
+    for (size_t lo = 0; lo < in_bytes; lo += chunk) {
+        const size_t m = in_bytes - lo < chunk ? in_bytes - lo : chunk;
+        par_memcpy(h + a_in + lo, in + lo, m);
+        err = hipMemcpyAsync(d + a_in + lo, h + a_in + lo, m, hipMemcpyHostToDevice, c->stream);
+        if (err != hipSuccess) return (int) err;
+    }
     int rc = run_device(c, decompress, d + a_in, (const uint64_t *) (d + a_ioff),
                         (const uint32_t *) (d + a_ilen), n, max_len, d + a_out,
                         (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_ocap),
                         (uint32_t *) (d + a_olen), (void *) c->stream);
     if (rc != 0) return rc;
-    err = hipMemcpyAsync(h + a_olen, d + a_olen, total - 16 - a_olen, hipMemcpyDeviceToHost, c->stream);
+    if (out_bytes <= (1u << 20)) {
+        /* small batches (the per-datagram drop-in calls): one D2H of the slots,
+         * fewer launches and syncs than packing */
+        err = hipMemcpyAsync(h + a_olen, d + a_olen, total - 16 - a_olen, hipMemcpyDeviceToHost, c->stream);
+        if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+        if (err != hipSuccess) return (int) err;
+        memcpy(out_len, h + a_olen, n * 4);
+        for (size_t i = 0; i < n; ++i)
+            if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
+        return 0;
+    }
+    rc = rc_hip_pack(d + a_out, (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_olen), (uint32_t) n,
+                     c->d_bsum, c->d_pack, (void *) c->stream);
+    if (rc != 0) return rc;
+    uint64_t packed = 0;
+    err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(&packed, c->d_bsum + blocks, 8, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     if (err != hipSuccess) return (int) err;
-    err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
-    if (err != hipSuccess) return (int) err;
-    err = hipStreamSynchronize(c->stream);
-    if (err != hipSuccess) return (int) err;
+    if (packed > out_bytes) return (int) hipErrorUnknown;
     memcpy(out_len, h + a_olen, n * 4);
-    for (size_t i = 0; i < n; ++i)
-        if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
-    return 0;
+    uint64_t *poff = (uint64_t *) malloc((n + 1) * sizeof(uint64_t));
+    if (!poff) return (int) hipErrorOutOfMemory;
+    uint64_t acc = 0;
+    for (size_t i = 0; i < n; ++i) { poff[i] = acc; acc += out_len[i]; }
+    poff[n] = acc;
+    /* D2H in packet groups; the scatter of group g overlaps the DMA of g+1 */
+    const int groups = packed >= (16u << 20) ? 4 : 1;
+    hipEvent_t ev[4];
+    int nev = 0;
+    size_t first[5];
+    for (int g = 0; g <= groups; ++g) first[g] = n * (size_t) g / (size_t) groups;
+    for (int g = 0; g < groups && err == hipSuccess; ++g) {
+        const uint64_t lo = poff[first[g]], hi = poff[first[g + 1]];
+        if (hi > lo) err = hipMemcpyAsync(h + a_out + lo, c->d_pack + lo, hi - lo, hipMemcpyDeviceToHost, c->stream);
+        if (err == hipSuccess) err = hipEventCreateWithFlags(&ev[g], hipEventDisableTiming);
+        if (err == hipSuccess) { nev = g + 1; err = hipEventRecord(ev[g], c->stream); }
+    }
+    for (int g = 0; g < nev && err == hipSuccess; ++g) {
+        err = hipEventSynchronize(ev[g]);
+        if (err == hipSuccess)
+            par_scatter(out, out_off, h + a_out, poff, out_len, first[g], first[g + 1],
+                        poff[first[g + 1]] - poff[first[g]]);
+    }
+    for (int g = 0; g < nev; ++g) hipEventDestroy(ev[g]);
+    free(poff);
+    return err == hipSuccess ? 0 : (int) err;
 }
 
 int enet_rc_compress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
@@ -300,6 +446,8 @@ static int dgram_reserve(rc_ctx *c, size_t n, int scratch)
     if (scratch && n * DG_MTU > c->dg_scratch_cap) {
         hipStreamSynchronize(c->stream);
         if (c->dg_scratch) hipFree(c->dg_scratch);
+    if (c->d_pack) hipFree(c->d_pack);
+    if (c->d_bsum) hipFree(c->d_bsum);
         c->dg_scratch = NULL; c->dg_scratch_cap = 0;
         if (hipMalloc((void **) &c->dg_scratch, n * DG_MTU) != hipSuccess) return -1;
         c->dg_scratch_cap = n * DG_MTU;
