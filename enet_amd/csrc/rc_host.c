@@ -98,6 +98,9 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     if (hipMalloc(&c->ws.lane_pool, slots * (size_t) region) != hipSuccess) return -1;
     /* lane regions start at epoch 0: no order-1 record is live (rc_lane.hip) */
     if (hipMemset(c->ws.lane_pool, 0, slots * (size_t) region) != hipSuccess) return -1;
+    /* hipMemset runs on the null stream, which the context's non-blocking
+     * stream (and a caller's) does not wait for: finish it before any kernel */
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
     c->ws.lane_slots = (uint32_t) slots;
     c->ws.lane_region = region;
     if (getenv("ENET_RC_DEBUG"))
@@ -437,14 +440,14 @@ static int dgram_reserve(rc_ctx *c, size_t n, int scratch)
     if (n > c->dg_cap) {
         size_t cap = c->dg_cap ? c->dg_cap : 1024;
         while (cap < n) cap *= 2;
-        hipStreamSynchronize(c->stream);
+        hipDeviceSynchronize();             /* (the device calls run on the caller's stream) */
         if (c->dg_arrays) hipFree(c->dg_arrays);
         c->dg_arrays = NULL; c->dg_cap = 0;
         if (hipMalloc((void **) &c->dg_arrays, cap * (3 * 8 + 6 * 4)) != hipSuccess) return -1;
         c->dg_cap = cap;
     }
     if (scratch && n * DG_MTU > c->dg_scratch_cap) {
-        hipStreamSynchronize(c->stream);
+        hipDeviceSynchronize();
         if (c->dg_scratch) hipFree(c->dg_scratch);
     if (c->d_pack) hipFree(c->d_pack);
     if (c->d_bsum) hipFree(c->d_bsum);

@@ -230,3 +230,31 @@ def test_wave_kernel_fixtures(wave_coder):
     test_compress_fixtures(wave_coder)
     test_decompress_fixtures_incl_garbage(wave_coder)
     test_c1_digest(wave_coder)
+
+
+def test_host_pointer_batches_large(coder):
+    """enet_rc_{compress,decompress}_batch_host on a batch large enough for the
+    chunked staging copies, device-side packing and chunked D2H (rc_host.c
+    run_host, rc_pack.hip): bit-exact against the oracle, ragged offsets."""
+    import ctypes as C
+    from oracle.pyoracle import compress_batch as ocompress, fnv_digest
+    d, o, l = synth.mixed_batch(30000)          # > 16 MB each way: the chunked copies
+    lib = coder.lib
+    n = len(l)
+    ln = l.astype(np.uint32)
+    cap = (2 * ln.astype(np.int64) + 64).astype(np.uint32)
+    coff = np.zeros(n, np.uint64)
+    coff[1:] = np.cumsum(cap[:-1].astype(np.uint64) + 3)          # gaps: slots not back to back
+    cout = np.zeros(int(coff[-1] + cap[-1]) + 16, np.uint8)
+    clen = np.zeros(n, np.uint32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    assert lib.enet_rc_compress_batch_host(coder.ctx, p(d), p(o), p(ln), n, p(cout), p(coff), p(cap), p(clen)) == 0
+    want, wo, wcap, wl = ocompress(d, o, l, "port")
+    assert np.array_equal(clen, wl)
+    assert fnv_digest(cout, coff, clen) == fnv_digest(want, wo, wl)
+    dout = np.zeros(int(o[-1]) + int(l[-1]) + 16, np.uint8)
+    dlen = np.zeros(n, np.uint32)
+    assert lib.enet_rc_decompress_batch_host(coder.ctx, p(cout), p(coff), p(clen), n, p(dout), p(o), p(ln),
+                                             p(dlen)) == 0
+    assert np.array_equal(dlen, ln)
+    assert np.array_equal(dout[: d.size], d)
