@@ -79,7 +79,9 @@ int enet_host_compress_with_range_coder(ENetHost *host);
  * Return value: 0 on success, otherwise a HIP error code. */
 
 /* All pointers are DEVICE pointers; work is enqueued on `stream` (a
- * hipStream_t; NULL = the default null stream) and not waited for. */
+ * hipStream_t; NULL = the default null stream) and not waited for.  The
+ * calls of one context share its device workspace: issue them on one stream,
+ * or order the streams, as for any buffer reused across streams. */
 int enet_rc_compress_batch_device(void *context, const uint8_t *in, const uint64_t *in_off,
                                   const uint32_t *in_len, size_t n, uint32_t max_len,
                                   uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
