@@ -202,7 +202,10 @@ def main():
         leg("datagram_path", datagram_path, coder, dev, stream)
 
     if world > 1 and not args.no_rccl:
-        rs = rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank)
+        try:
+            rs = rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank)
+        except Exception as e:  # noqa: BLE001  (the main line is already measured)
+            rs = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
             result["rccl_scatter_gather"] = rs
 
