@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6.3 TB/s achievable
+RANDOM_RMW_CEILING_GBPS = 3900.0   # line traffic of the lane kernels' access pattern (membench MB_AHEAD)
 GIB = float(1 << 30)
 
 
@@ -159,6 +160,15 @@ def main():
         "alg_bytes_per_launch": alg, "launch_ms": round(t_dom * 1e3, 4),
         "compress_ms": round(t_comp * 1e3, 4), "decompress_ms": round(t_dec * 1e3, 4),
     }
+    if traffic:
+        # what the kernel actually moves: PMC HBM bytes per launch / this launch time,
+        # against the peak and against the measured ceiling of its access pattern
+        # (random 128-B line read + 64-B write per record step, tools/mb/membench.hip
+        # MB_AHEAD, profiles/r1_membench_ahead.log: ~3.9 TB/s)
+        rate = traffic / t_dom / 1e9
+        roofline["traffic_GBps"] = round(rate, 1)
+        roofline["traffic_frac_of_peak"] = round(rate / HBM_PEAK_GBPS, 4)
+        roofline["traffic_frac_of_random_rmw_ceiling"] = round(rate / RANDOM_RMW_CEILING_GBPS, 3)
 
     result = {
         "metric": "GiB/s device-resident range-coder (de)compress, 64Ki×1200B pkts, 1/2/4/8 GPU",
