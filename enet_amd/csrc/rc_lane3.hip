@@ -33,8 +33,9 @@
 // is forwarded from registers when v is one of the two contexts in flight.
 //
 // Packets longer than 1919 bytes can reach compress.c's model reset
-// (:148-157) and go to the exact path (rc_kernels.hip), as do corrupt
-// streams whose root code points past symbol 255 and region overflows.
+// (:148-157): the lanes count compress.c's nodes and reset at the same byte
+// (lane_reset).  Corrupt streams whose root code points past symbol 255 and
+// region overflows go to the exact path (rc_kernels.hip).
 
 #ifndef RC_LANE_HOST_TEST
 #include <hip/hip_runtime.h>
@@ -52,6 +53,7 @@ namespace {
 constexpr uint32_t kRec = 64;                       // order-1 record, big order-2 record
 constexpr uint32_t kArena3 = kO1Base + 256 * kRec;  // arena start (after header and order-1 table)
 constexpr uint32_t kMaxLen3 = 1919;                 // <= 2*1919 + 256 nodes < 4094: no reset (compress.c:150)
+constexpr uint32_t kNodeLimit = 4096 - 2;           // compress.c:148-157: sizeof symbols / sizeof ENetSymbol - order
 constexpr uint32_t kInlineMax = 127;                // inline order-2 counts stay below 0x80
 
 // o2 info (u16) of an order-1 symbol: the state of the order-2 context it heads
@@ -507,6 +509,7 @@ struct Lane {
     // SGPRs, and a dozen loop-carried ones spill into VGPR lanes)
     uint32_t same, fwd, prv_dirty, q_dirty, q_fwd, ovf;
     uint32_t nsame, fromprv;    // where the next step's R[v] comes from (lane_prefetch)
+    uint32_t nodes;             // compress.c's nextSymbol: 1 (root) + the (context, value) pairs created
 };
 
 DEV void lane_init(Lane& L, uint8_t* reg)
@@ -517,6 +520,21 @@ DEV void lane_init(Lane& L, uint8_t* reg)
     L.eqp[0] = L.eqp[1] = L.eqp[2] = 0u;
     L.same = false; L.fwd = true; L.prv_dirty = false; L.q_dirty = false; L.q_fwd = true; L.ovf = false;
     L.nsame = false; L.fromprv = false;
+    L.nodes = 1;
+}
+
+// compress.c:148-157: the model starts over (new epoch: every order-1 record
+// reads as empty; arena from the start; order 0), as at a packet start.  The
+// caller clears the root.  Loads in flight read as empty under the new epoch.
+DEV void lane_reset(Lane& L, uint8_t* reg)
+{
+    L.epoch = next_epoch(reg, L.epoch) & 0xFFFF;
+    ctx_clear(L.cur); ctx_clear(L.prv); ctx_clear(L.q);
+    L.info = 0; L.ipos = 0; L.a = 0; L.b = 0; L.order = 0; L.bump = kArena3; L.qoff = 0;
+    L.eqp[0] = L.eqp[1] = L.eqp[2] = 0u;
+    L.same = false; L.fwd = true; L.prv_dirty = false; L.q_dirty = false; L.q_fwd = true;
+    L.nsame = false; L.fromprv = false;
+    L.nodes = 1;
 }
 
 // top of a step: the records loaded by the previous step become registers
@@ -564,12 +582,18 @@ DEV void o2_stats(const Lane& L, uint32_t& esc, uint32_t& tot)
 //   2. update the o1 context b (at <= 1): bump or insert
 //   3. the o2 info of (b, v) and where it lives, the loads for step i+1
 template <bool HAVE_H1>
-DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, Look<3>& h1, Look<6>& h2)
+DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, Look<3>& h1, Look<6>& h2,
+                      bool new0, bool track)
 {
+    // nodes compress.c creates this step: v in each visited context that lacks
+    // it (the order-2 context is always visited, order 1 when order 2 did not
+    // code v, the root when neither did -- new0, from the caller)
+    uint32_t created = new0 ? 1u : 0u;
     // ---- 1. o2 context (a, b), compress.c:286-316
     uint32_t o2_new = 0;
     if (L.order >= 2) {
         const bool big = info_big(L.info);
+        if (track) created += (big ? !h2.found : !(L.info != 0 && (L.info & 0xFF) == v)) ? 1u : 0u;
         uint32_t ni = L.info;
         // inline: empty -> (v, 2); (v, c) -> (v, c + 2) while c + 2 <= 127.
         // (A hit is v == the symbol, whatever level decoded v: a corrupt
@@ -625,10 +649,12 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, L
     // ---- 2. o1 context b, compress.c:286-316 (its lookup, when the decoder did not need it)
     if (!HAVE_H1 && L.order >= 1 && at == 2) h1 = ctx_find<3, true>(reg, L.cur, v);
     if (L.order >= 1 && at <= 1) {
+        if (track) created += h1.found ? 0u : 1u;
         bool ovf = L.ovf != 0;
         ctx_update<3, true>(reg, L.cur, h1, v, L.bump, end, ovf, true);
         L.ovf = ovf;
     }
+    if (track) L.nodes += created;
     // ---- 3. next step: contexts (b, v)
     uint32_t ninfo = 0, nipos = 0;
     if (L.order >= 1) {
@@ -679,7 +705,6 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
     if (len == 0) { bt.out_len[pkt] = 0; return; }                   // compress.c:257
-    if (len > kMaxLen3) { flag_exact(ws, pkt); return; }
     ByteSrc in;
     src_init(in, bt.in + bt.in_off[pkt], len);
     ByteSink o;
@@ -693,6 +718,9 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
     uint32_t low = 0, range = ~0u;
     bool ok = true;
 
+    // compress.c's node count only matters for packets that can reach the
+    // model reset (> 1919 bytes); a wave counts when any of its lanes has one
+    const bool track = any_lane(len > kMaxLen3);
     PROF_DECL
     for (uint32_t i = 0; i < len; ++i) {
 #ifdef RC_PROFILE_DRAIN
@@ -743,9 +771,14 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         // no loop exit between the record load (lane_prefetch) and the record
         // store (lane_advance): an exit path there makes the compiler's vmcnt
         // bookkeeping wait for the store at the top of every step
-        lane_advance<true>(L, reg, end, v, done2 ? 2 : done1 ? 1 : 0, h1, h2);
+        lane_advance<true>(L, reg, end, v, done2 ? 2 : done1 ? 1 : 0, h1, h2, en0 && cnt0 == 0, track);
         PROF(6)
         if (rare_lane(!ok || L.ovf)) { if (!ok || L.ovf) break; }
+        if (track) {                                                  // compress.c:332 -> :148-157
+            if (rare_lane(L.nodes >= kNodeLimit)) {
+                if (L.nodes >= kNodeLimit) { lane_reset(L, reg); root3_clear<true>(root, R); rtot = 1 + 256; }
+            }
+        }
         PROF(7)
     }
     PROF_FLUSH(0)
@@ -791,7 +824,6 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         __builtin_amdgcn_s_waitcnt(0);
         PROF(9)
 #endif
-        if (o.n >= kMaxLen3) { anomaly = true; break; }             // a model reset could follow: exact path
         lane_top(L);
         sink_flush(o);
         src_fill(in, true);
@@ -801,6 +833,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         Look<3> h1;
         Look<6> h2;
         h1.found = false;
+        bool new0 = false;
         // order 2, compress.c:529-568
         uint32_t esc2, tot2;
         o2_stats(L, esc2, tot2);
@@ -840,6 +873,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (cd - 1 >= rtot - 1) { anomaly = true; break; }           // past symbol 255
             uint32_t under, cnt;
             v = root3_search(root, R, cd - 1, under, cnt);
+            new0 = cnt == 0;
             root3_add<false>(root, R, v, cnt);
             dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
             rtot = (rtot + kRootDelta) & 0xFFFF;
@@ -854,9 +888,12 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, L.q, v);
         fail = o.n >= o.cap;                                         // compress.c:617
         PROF(4)
-        lane_advance<true>(L, reg, end, v, at, h1, h2);             // (see compress_one3)
+        lane_advance<true>(L, reg, end, v, at, h1, h2, new0, true); // (see compress_one3)
         PROF(5)
         if (fail || L.ovf) break;
+        if (rare_lane(L.nodes >= kNodeLimit)) {                      // compress.c:617-621 -> :148-157
+            if (L.nodes >= kNodeLimit) { lane_reset(L, reg); root3_clear<false>(root, R); rtot = 1 + 256; }
+        }
         sink_put(o, v, 1, true);
         src_adv(in);
         PROF(6)
@@ -876,8 +913,12 @@ extern "C" uint32_t rc_hip_lane3_region_bytes(uint32_t max_len)
     // >= 2 symbols (64 B per 2 bytes), a dense order-2 block > 24 (288 B per
     // 24 bytes), a dense order-1 block > 12 symbols of its own (800 B per 12
     // bytes): <= 32 + 12 + 67 B per byte, plus alignment slack.
+    // Longer packets reset the model at 4094 nodes (compress.c:148-157); one
+    // model's arena is then bounded by its nodes: <= 67 B per order-1 symbol,
+    // <= 44 B + 64-B alignment slack per two order-2 symbols; 80 B per node.
+    // (An overflow is still caught: the packet takes the exact path.)
     const uint64_t L = max_len < kMaxLen3 ? max_len : kMaxLen3;
-    uint64_t bytes = kArena3 + 112 * L + 4096;
+    uint64_t bytes = max_len <= kMaxLen3 ? kArena3 + 112 * L + 4096 : kArena3 + 80ull * kNodeLimit + 4096;
     bytes = (bytes + 255) & ~255ull;
     return static_cast<uint32_t>(bytes);
 }

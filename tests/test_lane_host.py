@@ -47,7 +47,7 @@ def test_lane_logic_compress_fixtures(lane):
         if c["in_limit"] != len(c["input"]):
             continue
         r = lane(0, c["input"], c["out_limit"])
-        if r[0] == "exact":      # v3 hands packets that can reach the model reset to the exact path
+        if r[0] == "exact":      # (allowed only for packets long enough to reach the model reset)
             assert lane.version == "v3" and len(c["input"]) > 1919
             continue
         assert r[0] == c["ret"], (len(c["input"]), c["out_limit"])
