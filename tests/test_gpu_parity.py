@@ -258,3 +258,34 @@ def test_host_pointer_batches_large(coder):
                                              p(dlen)) == 0
     assert np.array_equal(dlen, ln)
     assert np.array_equal(dout[: d.size], d)
+
+
+def test_long_packets_batch_vs_oracle(coder):
+    """2048 packets of 1900-4096 B (random, low-entropy, runs): compress.c's
+    model reset at 4094 nodes happens inside the lane kernels (rc_lane3.hip
+    lane_reset); bit-exact against the oracle and back."""
+    from oracle.pyoracle import compress_batch as ocompress, fnv_digest
+    rng = np.random.default_rng(23)
+    pk = []
+    for i in range(2048):
+        n = int(rng.integers(1900, 4097))
+        k = i % 4
+        if k == 0:
+            p = rng.integers(0, 256, n, dtype=np.uint8)
+        elif k == 1:
+            p = rng.integers(0, 256, n, dtype=np.uint8) & np.uint8(rng.integers(1, 64))
+        elif k == 2:
+            p = (np.cumsum(rng.integers(-2, 3, n)) & 0xFF).astype(np.uint8)
+        else:
+            p = np.repeat(rng.integers(0, 256, n // 16 + 1, dtype=np.uint8), 16)[:n]
+        pk.append(p.tobytes())
+    d, o, l = _pack(pk)
+    out, oo, cap, ol = ocompress(d, o, l, "port")
+    res = _run(coder, False, pk, [int(c) for c in cap])
+    gl = np.array([r[0] for r in res], np.uint32)
+    assert np.array_equal(gl, ol)
+    blob = np.frombuffer(b"".join(r[1] for r in res), np.uint8)
+    goff = np.concatenate([[0], np.cumsum(gl[:-1].astype(np.uint64))]).astype(np.uint64)
+    assert fnv_digest(blob, goff, gl) == fnv_digest(out, oo, ol)
+    back = _run(coder, True, [r[1] for r in res], [len(p) for p in pk])
+    assert all(b == (len(p), p) for b, p in zip(back, pk))
