@@ -210,6 +210,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_dgram:
         leg("datagram_path", datagram_path, coder, dev, stream)
+        leg("per_datagram_call", per_datagram_call, coder, d, o, l)
 
     if world > 1 and not args.no_rccl:
         try:
@@ -349,6 +350,37 @@ def datagram_path(coder, dev, stream):
                               "note": "recvmmsg (256 per call) into pinned staging + H2D + GPU decode "
                                       "+ D2H of 4096-B slots, best of 3 (sender not timed)"}
     return res
+
+
+def per_datagram_call(coder, d, o, l):
+    """The drop-in surface as protocol.c uses it: one enet_range_coder_compress
+    / _decompress call per 1200-B datagram (host memory in and out, one launch
+    and two copies each).  Latency per call; the batch API is the throughput path."""
+    import ctypes as C
+    from enet_amd._lib import ENetBuffer
+    lib = coder.lib
+    m = 200
+    src = [C.create_string_buffer(d[int(o[i]): int(o[i]) + int(l[i])].tobytes(), int(l[i])) for i in range(m)]
+    bufs = [C.byref(ENetBuffer(C.cast(b, C.c_void_p), int(l[i]))) for i, b in enumerate(src)]
+    out = C.create_string_buffer(4096)
+    back = C.create_string_buffer(4096)
+    for i in range(5):
+        lib.enet_range_coder_compress(coder.ctx, bufs[i], 1, int(l[i]), out, 4096)
+    t0 = time.perf_counter()
+    sizes = [lib.enet_range_coder_compress(coder.ctx, bufs[i], 1, int(l[i]), out, 4096) for i in range(m)]
+    t1 = time.perf_counter()
+    packed = []
+    for i in range(m):
+        r = lib.enet_range_coder_compress(coder.ctx, bufs[i], 1, int(l[i]), out, 4096)
+        packed.append(C.create_string_buffer(out.raw[:r], r))
+    t2 = time.perf_counter()
+    ok = True
+    for i in range(m):
+        r = lib.enet_range_coder_decompress(coder.ctx, packed[i], sizes[i], back, 4096)
+        ok = ok and r == int(l[i]) and back.raw[:r] == src[i].raw
+    t3 = time.perf_counter()
+    return {"datagram_bytes": int(l[0]), "calls": m, "compress_us": round((t1 - t0) / m * 1e6, 1),
+            "decompress_us": round((t3 - t2) / m * 1e6, 1), "roundtrip_ok": ok}
 
 
 def pcie_inclusive(coder, d, o, l, args):
