@@ -143,7 +143,7 @@ DEV void rec2_store(uint8_t* reg, uint32_t off, const Rec2& c)
 template <uint32_t NV>
 struct Look {
     uint32_t k, under, cnt, info;   // slot (insertion slot if absent), counts below, count, o2 info
-    bool found;
+    uint32_t found;                 // 0 / 1 (a word: a bool would be an SGPR lane mask)
     uint32_t eq[NV];                // 0x01 in the byte of the found slot
     Dense z;                        // dense contexts: C, the symbol's group, its o2 info
 };
@@ -185,7 +185,7 @@ DEV Look<NV> ctx_find(const uint8_t* reg, const Ctx<NV, O2>& c, uint32_t v)
             h.under = u; h.cnt = n; h.info = h.z.link;
         }
     }
-    h.found = h.cnt != 0;
+    h.found = h.cnt != 0 ? 1u : 0u;
     return h;
 }
 
@@ -225,7 +225,7 @@ DEV bool ctx_search(const uint8_t* reg, const Ctx<NV, O2>& c, uint32_t code, Loo
             h.under = u; h.cnt = n; v = vv; h.info = h.z.link;
         }
     }
-    h.found = ok;
+    h.found = ok ? 1u : 0u;
     return ok;
 }
 
@@ -742,7 +742,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         const bool en2 = L.order >= 2 && esc2 != 0;
         const bool big = info_big(L.info);
         Look<6> h2;
-        h2.found = (L.info & 0xFF) == v; h2.under = 0; h2.cnt = L.info >> 8;
+        h2.found = (L.info & 0xFF) == v ? 1u : 0u; h2.under = 0; h2.cnt = L.info >> 8;
         if (any_lane(en2 && big)) {
             if (en2 && big) h2 = ctx_find<6, false>(reg, L.q, v);
         }
@@ -832,7 +832,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         uint32_t v = 0;
         Look<3> h1;
         Look<6> h2;
-        h1.found = false;
+        h1.found = 0u;
         bool new0 = false;
         // order 2, compress.c:529-568
         uint32_t esc2, tot2;
