@@ -230,6 +230,24 @@ def test_wave_kernel_fixtures(wave_coder):
     test_compress_fixtures(wave_coder)
     test_decompress_fixtures_incl_garbage(wave_coder)
     test_c1_digest(wave_coder)
+    test_long_packets_and_model_reset(wave_coder)
+    test_random_fuzz_vs_oracle(wave_coder)
+
+
+def test_small_batches_vs_oracle(coder):
+    """Batches of <= 64 packets (the per-datagram calls among them) run on the
+    wavefront-per-packet kernel (rc_kernels.hip launch): bit-exact, all sizes."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(31)
+    for n in (1, 7, 64):
+        pk = [rng.integers(0, int(rng.choice([2, 17, 256])), size=int(rng.integers(1, 4097)),
+                           dtype=np.uint8).tobytes() for _ in range(n)]
+        caps = [2 * len(p) + 64 for p in pk]
+        res = _run(coder, False, pk, caps)
+        assert res == [port.compress(p, out_limit=c) for p, c in zip(pk, caps)]
+        back = _run(coder, True, [r[1] for r in res], [len(p) for p in pk])
+        assert back == [(len(p), p) for p in pk]
 
 
 def test_host_pointer_batches_large(coder):
