@@ -9,6 +9,7 @@
  *   enet_loopback both   PORT COUNT   two hosts in this process
  *   enet_loopback server PORT COUNT   echo COUNT packets back, then exit
  *   enet_loopback client PORT COUNT   send COUNT packets, check the echoes
+ *   enet_loopback fan PORT COUNT K    K peers between two hosts in this process
  *
  * Payloads are low-entropy "game state" records so that datagrams compress
  * (protocol.c:1696 only sends the compressed form when it is smaller).
@@ -22,6 +23,12 @@
 #include <enet/enet.h>
 
 extern const char *enet_rc_version(void) __attribute__((weak));
+
+#ifdef ENET_LOOPBACK_DEFERRED
+/* loopback_deferred: the hosts run in deferred-batch mode (rc_deferred.c,
+ * include/enet_rc_deferred.h): one GPU batch per send / receive pass */
+#include "enet_rc_deferred.h"
+#endif
 
 static uint64_t mix(uint64_t *s)
 {
@@ -81,14 +88,20 @@ static int ENET_CALLBACK dump_datagram(ENetHost *host, ENetEvent *event)
     return 0;   /* protocol.c goes on handling it */
 }
 
-static ENetHost *mk_host(const ENetAddress *a, int *rc)
+static ENetHost *mk_host(const ENetAddress *a, size_t peers, int *rc)
 {
-    ENetHost *h = enet_host_create(a, 4, 2, 0, 0);
+    ENetHost *h = enet_host_create(a, peers, 2, 0, 0);
     if (!h) { fprintf(stderr, "enet_host_create failed\n"); exit(2); }
+    const char *ck = getenv("ENET_LOOPBACK_CHECKSUM");
+    const int checksum = ck && atoi(ck);
+#ifdef ENET_LOOPBACK_DEFERRED
+    *rc = enet_rc_deferred_attach(h, checksum);
+    if (*rc != 0) { fprintf(stderr, "enet_rc_deferred_attach = %d\n", *rc); exit(3); }
+#else
     *rc = enet_host_compress_with_range_coder(h);
     if (*rc != 0) { fprintf(stderr, "enet_host_compress_with_range_coder = %d\n", *rc); exit(3); }
-    const char *ck = getenv("ENET_LOOPBACK_CHECKSUM");
-    if (ck && atoi(ck)) h->checksum = enet_crc32;
+    if (checksum) h->checksum = enet_crc32;
+#endif
     const char *dp = getenv("ENET_LOOPBACK_DUMP");
     if (dp) {
         if (!g_dump) g_dump = fopen(dp, "w");
@@ -152,9 +165,94 @@ static void pump(Side *s)
     }
 }
 
+static void print_stats(const char *name, ENetHost *h)
+{
+#ifdef ENET_LOOPBACK_DEFERRED
+    enet_rc_deferred_stats st;
+    enet_rc_deferred_get_stats(h, &st);
+    printf("\"%s\": {\"send_batches\": %llu, \"send_datagrams\": %llu, \"send_compressed\": %llu, "
+           "\"recv_batches\": %llu, \"recv_datagrams\": %llu, \"recv_dropped\": %llu}", name,
+           (unsigned long long) st.send_batches, (unsigned long long) st.send_datagrams,
+           (unsigned long long) st.send_compressed, (unsigned long long) st.recv_batches,
+           (unsigned long long) st.recv_datagrams, (unsigned long long) st.recv_dropped);
+#else
+    (void) h;
+    printf("\"%s\": null", name);
+#endif
+}
+
+/* fan PORT COUNT K: a server host and a client host in this process, K peers
+ * between them; every client peer keeps a window of packets in flight and
+ * checks the echoes.  With K peers, one send pass of either host assembles up
+ * to K datagrams -- what a deferred host turns into one GPU batch. */
+typedef struct { uint32_t sent, got, bad; int connected; } Lane;
+
+static int run_fan(const ENetAddress *addr, uint32_t count, uint32_t k)
+{
+    int rc = 0;
+    ENetHost *sv = mk_host(addr, k, &rc), *cl = mk_host(NULL, k, &rc);
+    Lane *ln = (Lane *) calloc(k, sizeof *ln);
+    for (uint32_t i = 0; i < k; ++i) {
+        ENetPeer *p = enet_host_connect(cl, addr, 2, i);
+        if (!p) return 4;
+        p->data = &ln[i];
+    }
+    uint32_t done = 0, echoed = 0;
+    uint64_t raw = 0;
+    double t0 = now(), deadline = t0 + 60.0;
+    while (now() < deadline && done < k) {
+        ENetEvent ev;
+        while (enet_host_service(sv, &ev, 0) > 0) {
+            if (ev.type != ENET_EVENT_TYPE_RECEIVE) continue;
+            enet_peer_send(ev.peer, 0, enet_packet_create(ev.packet->data, ev.packet->dataLength,
+                                                          ENET_PACKET_FLAG_RELIABLE));
+            ++echoed;
+            enet_packet_destroy(ev.packet);
+        }
+        while (enet_host_service(cl, &ev, 0) > 0) {
+            Lane *l = (Lane *) ev.peer->data;
+            if (ev.type == ENET_EVENT_TYPE_CONNECT) l->connected = 1;
+            if (ev.type != ENET_EVENT_TYPE_RECEIVE) continue;
+            uint8_t want[1400];
+            size_t n = make_payload((uint32_t) (l - ln) * count + l->got, want);
+            if (ev.packet->dataLength != n || memcmp(ev.packet->data, want, n) != 0) ++l->bad;
+            if (++l->got == count) ++done;
+            enet_packet_destroy(ev.packet);
+        }
+        for (uint32_t i = 0; i < k; ++i) {
+            Lane *l = &ln[i];
+            while (l->connected && l->sent < count && l->sent < l->got + 8) {
+                uint8_t buf[1400];
+                size_t n = make_payload(i * count + l->sent, buf);
+                enet_peer_send(&cl->peers[i], 0, enet_packet_create(buf, n, ENET_PACKET_FLAG_RELIABLE));
+                raw += n;
+                ++l->sent;
+            }
+        }
+        enet_host_flush(cl);
+        enet_host_flush(sv);
+    }
+    uint32_t got = 0, bad = 0;
+    for (uint32_t i = 0; i < k; ++i) { got += ln[i].got; bad += ln[i].bad; }
+    const int ok = done == k && bad == 0;
+    printf("{\"role\": \"fan\", \"coder\": \"%s\", \"peers\": %u, \"packets\": %u, \"received\": %u, "
+           "\"echoed\": %u, \"mismatches\": %u, \"payload_bytes\": %llu, \"seconds\": %.3f, ",
+           enet_rc_version ? enet_rc_version() : "reference compress.c", k, k * count, got, echoed, bad,
+           (unsigned long long) raw, now() - t0);
+    print_stats("server", sv);
+    printf(", ");
+    print_stats("client", cl);
+    printf(", \"ok\": %s}\n", ok ? "true" : "false");
+    fflush(stdout);
+    enet_host_destroy(cl);
+    enet_host_destroy(sv);
+    free(ln);
+    return ok ? 0 : 1;
+}
+
 int main(int argc, char **argv)
 {
-    if (argc < 4) { fprintf(stderr, "usage: %s both|server|client PORT COUNT\n", argv[0]); return 2; }
+    if (argc < 4) { fprintf(stderr, "usage: %s both|server|client|fan PORT COUNT [PEERS]\n", argv[0]); return 2; }
     const char *role = argv[1];
     const int both = !strcmp(role, "both"), server = both || !strcmp(role, "server"),
               client = both || !strcmp(role, "client");
@@ -163,14 +261,19 @@ int main(int argc, char **argv)
     ENetAddress addr;
     enet_address_set_host(&addr, "127.0.0.1");
     addr.port = (enet_uint16) atoi(argv[2]);
+    if (!strcmp(role, "fan")) {
+        const int r = run_fan(&addr, count, argc > 4 ? (uint32_t) strtoul(argv[4], NULL, 10) : 16);
+        enet_deinitialize();
+        return r;
+    }
 
     Side sv, cl;
     memset(&sv, 0, sizeof sv);
     memset(&cl, 0, sizeof cl);
     int rc = 0;
-    if (server) { sv.host = mk_host(&addr, &rc); sv.count = count; }
+    if (server) { sv.host = mk_host(&addr, 4, &rc); sv.count = count; }
     if (client) {
-        cl.host = mk_host(NULL, &rc);
+        cl.host = mk_host(NULL, 4, &rc);
         cl.is_client = 1;
         cl.count = count;
         cl.peer = enet_host_connect(cl.host, &addr, 2, 0);
