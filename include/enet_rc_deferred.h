@@ -30,6 +30,10 @@
  *
  * Sockets of hosts that are not attached pass straight through to unix.c.
  *
+ * Threading follows ENet's: one host is serviced by one thread.  Attach and
+ * detach hosts from one thread (the host table is not locked).  A batch that
+ * fails on the GPU is lost like a dropped UDP datagram (the call returns -1).
+ *
  * Requires enet/enet.h to be included first (ENetHost, ENetBuffer).
  */
 #ifndef ENET_RC_DEFERRED_H
