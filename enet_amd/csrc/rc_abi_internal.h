@@ -41,7 +41,12 @@ typedef struct {
     uint32_t  lane_active;  /* lane kernels: packets per wavefront (64, 32 or 16) */
     uint32_t *order;        /* [n_cap] processing order (packets binned by length), lane kernels */
     uint32_t *bins;         /* [RC_LEN_BINS + 1] length-bin counters + uniform flag */
+    uint32_t  cus;          /* compute units of the device */
+    uint32_t  small_max;    /* lane3 contexts: batches of up to this many packets (and no more than
+                               fit on the chip at once) run on the wave kernel; RC_SMALL_AUTO = no cap */
 } rc_workspace_dev;
+
+#define RC_SMALL_AUTO 0xFFFFFFFFu
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */
 #define RC_KERNEL_LANE 0u   /* one packet per lane, model v2 (rc_lane.hip) */

@@ -155,6 +155,14 @@ void *enet_range_coder_create(void)
         const char *a = getenv("ENET_RC_LANES");
         c->ws.lane_active = 64;
         if (a && (atoi(a) == 32 || atoi(a) == 16)) c->ws.lane_active = (uint32_t) atoi(a);
+        /* ENET_RC_SMALL_BATCH=n caps the batches routed to the wave kernel
+         * (0: never); unset = every batch that fits on the chip at once */
+        const char *sb = getenv("ENET_RC_SMALL_BATCH");
+        c->ws.small_max = sb ? (uint32_t) strtoul(sb, NULL, 10) : RC_SMALL_AUTO;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
+            cus = 256;
+        c->ws.cus = (uint32_t) cus;
         const char *sl = getenv("ENET_RC_SLOTS");
         c->max_slots = MAX_LANE_SLOTS;
         if (sl && atol(sl) >= 256 && atol(sl) <= (1l << 22)) c->max_slots = (uint32_t) atol(sl);

@@ -27,6 +27,8 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "rc_abi_internal.h"
 
@@ -1051,7 +1053,15 @@ extern "C" const char* rc_hip_fast_kernel_name(int decompress, uint32_t kernel)
     return decompress ? "rc_decompress_lane3" : "rc_compress_lane3";
 }
 
-constexpr uint32_t kSmallBatch = 64;   // packets: up to this many, one wavefront each
+constexpr uint32_t kLdsPerCu = 160 * 1024;   // gfx950
+
+// LDS per wavefront of the wave kernels.  The decoder's model grows with the
+// bytes it produces, not the bytes it reads (max_len bounds the input), so it
+// always gets the largest arena.
+uint32_t wave_lds(bool decompress, uint32_t max_len)
+{
+    return decompress ? kMaxLds : lds_bytes_for(max_len);
+}
 
 static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
 {
@@ -1060,17 +1070,28 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     if (b->n > ws->n_cap) return static_cast<int>(hipErrorInvalidValue);
     hipError_t err = hipMemsetAsync(ws->counters, 0, 4 * sizeof(uint32_t), st);
     if (err != hipSuccess) return static_cast<int>(err);
-    // Small batches (the per-datagram drop-in calls among them) go to the
-    // wavefront-per-packet kernel: a lone packet's byte chain runs there with
-    // its model in LDS, ~1.5-2x sooner than on one lane of the lane kernels.
-    const bool small = b->n <= kSmallBatch && ws->kernel == RC_KERNEL_LANE3;
+    const uint32_t max_len = b->max_len ? b->max_len : 4096;
+    // Batches that fit on the chip in one wave per packet (the per-datagram
+    // drop-in calls and a live host's send / receive passes among them) go to
+    // the wavefront-per-packet kernel: a packet's byte chain runs there with
+    // its model in LDS, 1.4-2.9x sooner than on one lane of the lane kernels
+    // (tools/smallbatch.py).  Larger batches are throughput work: lanes.
+    const uint32_t lds_w = wave_lds(decompress, max_len);
+    const uint32_t resident = ws->cus * (kLdsPerCu / lds_w ? kLdsPerCu / lds_w : 1u);
+    // (not min(): on the host it resolves to the int overload, and small_max
+    // RC_SMALL_AUTO would read as -1)
+    const bool small = ws->kernel == RC_KERNEL_LANE3 && b->n <= resident && b->n <= ws->small_max;
+    static const bool debug = getenv("ENET_RC_DEBUG") != nullptr;
+    if (debug)
+        fprintf(stderr, "enet_rc: %s n=%u max_len=%u cus=%u lds=%u resident=%u small_max=%u -> %s\n",
+                decompress ? "decompress" : "compress", b->n, max_len, ws->cus, lds_w, resident,
+                ws->small_max, small || ws->kernel == RC_KERNEL_WAVE ? "wave" : "lanes");
     if (ws->kernel != RC_KERNEL_WAVE && !small) {
         const int rc = rc_hip_lane_launch(decompress ? 1 : 0, b, ws, stream);
         if (rc != 0) return rc;
     } else {
-        uint32_t max_len = b->max_len ? b->max_len : 4096;
         uint32_t stage = stage_bytes_for(max_len);
-        uint32_t lds = lds_bytes_for(max_len);
+        uint32_t lds = lds_w;
         if (stage + kInStage + 4096 > lds) {        // absurd max_len: everything goes exact
             stage = 16; lds = 16384;
         }
