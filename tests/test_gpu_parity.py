@@ -235,13 +235,15 @@ def test_wave_kernel_fixtures(wave_coder):
 
 
 def test_small_batches_vs_oracle(coder):
-    """Batches of <= 64 packets (the per-datagram calls among them) run on the
-    wavefront-per-packet kernel (rc_kernels.hip launch): bit-exact, all sizes."""
+    """Batches that fit on the chip at one wavefront per packet (the
+    per-datagram calls among them) run on the wavefront-per-packet kernel
+    (rc_kernels.hip launch): bit-exact, all sizes, several wavefronts per CU
+    (n > 256 CUs), and both sides of the decoder's 512-packet limit."""
     from oracle.pyoracle import Coder
     port = Coder("port")
     rng = np.random.default_rng(31)
-    for n in (1, 7, 64):
-        pk = [rng.integers(0, int(rng.choice([2, 17, 256])), size=int(rng.integers(1, 4097)),
+    for n, top in ((1, 4097), (7, 4097), (64, 4097), (300, 1401), (512, 1401), (513, 1401)):
+        pk = [rng.integers(0, int(rng.choice([2, 17, 256])), size=int(rng.integers(1, top)),
                            dtype=np.uint8).tobytes() for _ in range(n)]
         caps = [2 * len(p) + 64 for p in pk]
         res = _run(coder, False, pk, caps)
