@@ -50,6 +50,17 @@ constexpr uint32_t kOutStage = 64;            // 64-byte output staging
 constexpr uint32_t kInStage = 128;            // input staging, stage_bytes long
 constexpr uint32_t kNoBlock = 0xFFFFu;
 
+// Phase timing of the wave compress kernel (tools/waveprof.hip only): shader
+// clock cycles per phase, summed over packets.
+#ifdef RC_WAVE_PROF
+__device__ unsigned long long g_wave_prof[8];
+#define PROF_T(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define PROF_T(t)
+#define PROF_ADD(acc, a, b)
+#endif
+
 // ------------------------------------------------------------- wave helpers
 
 DEV uint32_t lane() { return __lane_id(); }
@@ -491,7 +502,11 @@ void rc_compress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes,
     uint32_t order = 0, b1 = 0, c2 = 0;
     bool ok = true;
 
+#ifdef RC_WAVE_PROF
+    uint64_t p2 = 0, p1 = 0, p0 = 0, pa = 0;
+#endif
     for (uint32_t i = 0; i < len; ++i) {
+        PROF_T(ta);
         const uint32_t v = s[kInStage + i];
         uint32_t under, cnt, nxt = 0;
         bool have_nxt = false, done = false;
@@ -506,6 +521,8 @@ void rc_compress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes,
             else if (esc0 > 0 && esc0 < tot0) ok = enc_code(s, e, o, 0, esc0, tot0);
             if (!ok) break;
         }
+        PROF_T(tb);
+        PROF_ADD(p2, ta, tb);
         if (!done && order >= 1) {                         // order-1 context
             Ctx c; o1_get(m, b1, c);
             const uint32_t esc0 = c.esc, tot0 = c.tot;
@@ -517,6 +534,8 @@ void rc_compress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes,
             else if (esc0 > 0 && esc0 < tot0) ok = enc_code(s, e, o, 0, esc0, tot0);
             if (!ok) break;
         }
+        PROF_T(tc);
+        PROF_ADD(p1, tb, tc);
         if (!done) {                                       // root, compress.c:318-329
             root_lookup(m, v, under, cnt);
             const uint32_t tot0 = m.rtot;
@@ -527,6 +546,8 @@ void rc_compress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes,
             m.rtot = (m.rtot + kRootDelta) & 0xFFFF;
             if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || m.rtot > kTotalLimit) root_rescale(m);
         }
+        PROF_T(td);
+        PROF_ADD(p0, tc, td);
         // advance, compress.c:331-336
         if (order >= 1) {
             if (!have_nxt) {
@@ -539,7 +560,18 @@ void rc_compress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes,
         if (order < 2) ++order;
         b1 = v;
         if (m.nodes >= kMaxNodes) { model_reset(s, m); order = 0; }
+        PROF_T(te);
+        PROF_ADD(pa, td, te);
     }
+#ifdef RC_WAVE_PROF
+    if (lane() == 0) {
+        atomicAdd(&g_wave_prof[0], (unsigned long long) p2);
+        atomicAdd(&g_wave_prof[1], (unsigned long long) p1);
+        atomicAdd(&g_wave_prof[2], (unsigned long long) p0);
+        atomicAdd(&g_wave_prof[3], (unsigned long long) pa);
+        atomicAdd(&g_wave_prof[4], (unsigned long long) len);
+    }
+#endif
 
     if (m.overflow) { flag_exact(ws, pkt); return; }
     if (ok) {                                              // flush, compress.c:139-146
