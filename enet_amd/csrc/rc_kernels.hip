@@ -505,9 +505,13 @@ void rc_compress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes,
 #ifdef RC_WAVE_PROF
     uint64_t p2 = 0, p1 = 0, p0 = 0, pa = 0;
 #endif
+    uint32_t inw = 0;                                      // input bytes i & ~63 .. +63, one per lane
     for (uint32_t i = 0; i < len; ++i) {
         PROF_T(ta);
-        const uint32_t v = s[kInStage + i];
+        // (a readlane instead of an LDS round trip per byte; the read past
+        // len stays inside the arena that follows the staging buffer)
+        if ((i & 63) == 0) inw = s[kInStage + i + lane()];
+        const uint32_t v = lane_val(inw, i & 63);
         uint32_t under, cnt, nxt = 0;
         bool have_nxt = false, done = false;
 
