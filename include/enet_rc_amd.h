@@ -46,7 +46,16 @@ typedef struct _ENetAddress { enet_uint32 host; enet_uint16 port; } ENetAddress;
  * Replaces compress.c:48-56.  Creates a coder context bound to the current HIP
  * device (its own stream + device workspace).  NULL on failure (no device,
  * out of memory).  Like the reference, one context is not thread-safe;
- * distinct contexts are independent. */
+ * distinct contexts are independent.
+ *
+ * Read once here from the environment (all optional):
+ *   ENET_RC_KERNEL=wave|lane2   force the wavefront-per-packet kernels, or the
+ *                               v2 lane kernels (default: v3 lane kernels)
+ *   ENET_RC_SMALL_BATCH=n       batches of up to n packets (and no more than
+ *                               fit on the chip at one wavefront each) run on
+ *                               the wavefront-per-packet kernels; 0 = never;
+ *                               unset = every batch that fits
+ *   ENET_RC_DEBUG=1             log pool sizes and kernel routing to stderr */
 void *enet_range_coder_create(void);
 
 /* Replaces compress.c:58-66.  NULL is ignored. */
