@@ -25,6 +25,8 @@ typedef struct {
     uint32_t       *out_len;
     uint32_t        n;
     uint32_t        max_len;   /* upper bound of in_len[] used to size LDS; longer packets take the exact path */
+    uint32_t        max_out;   /* upper bound of out_cap[] when the caller knows it, else 0; sizes the
+                                  wave decoder's LDS arena (a model that outgrows it takes the exact path) */
 } rc_batch_dev;
 
 /* Device workspace owned by a coder context. */

@@ -197,7 +197,7 @@ void enet_range_coder_destroy(void *context)
 }
 
 static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
-                      const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                      const uint32_t *in_len, size_t n, uint32_t max_len, uint32_t max_out, uint8_t *out,
                       const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
                       void *stream)
 {
@@ -212,6 +212,7 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;
     b.n = (uint32_t) n;
     b.max_len = max_len;
+    b.max_out = max_out;
     /* stream is a hipStream_t; NULL is HIP's default (null) stream */
     return decompress ? rc_hip_decompress(&b, &c->ws, stream) : rc_hip_compress(&b, &c->ws, stream);
 }
@@ -221,7 +222,7 @@ int enet_rc_compress_batch_device(void *context, const uint8_t *in, const uint64
                                   uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                                   uint32_t *out_len, void *stream)
 {
-    return run_device((rc_ctx *) context, 0, in, in_off, in_len, n, max_len, out, out_off,
+    return run_device((rc_ctx *) context, 0, in, in_off, in_len, n, max_len, 0, out, out_off,
                       out_cap, out_len, stream);
 }
 
@@ -230,7 +231,7 @@ int enet_rc_decompress_batch_device(void *context, const uint8_t *in, const uint
                                     uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                                     uint32_t *out_len, void *stream)
 {
-    return run_device((rc_ctx *) context, 1, in, in_off, in_len, n, max_len, out, out_off,
+    return run_device((rc_ctx *) context, 1, in, in_off, in_len, n, max_len, 0, out, out_off,
                       out_cap, out_len, stream);
 }
 
@@ -334,13 +335,14 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     if (!c) return (int) hipErrorInvalidValue;
     if (n == 0) return 0;
     uint64_t in_bytes = 0, out_bytes = 0;
-    uint32_t max_len = 0;
+    uint32_t max_len = 0, max_cap = 0;
     for (size_t i = 0; i < n; ++i) {
         uint64_t e = in_off[i] + in_len[i];
         if (e > in_bytes) in_bytes = e;
         uint64_t f = out_off[i] + out_cap[i];
         if (f > out_bytes) out_bytes = f;
         if (in_len[i] > max_len) max_len = in_len[i];
+        if (out_cap[i] > max_cap) max_cap = out_cap[i];
     }
     size_t a_in = 0;
     size_t a_ioff = (a_in + in_bytes + 15) & ~(size_t) 15;
@@ -370,7 +372,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         if (err != hipSuccess) return (int) err;
     }
     int rc = run_device(c, decompress, d + a_in, (const uint64_t *) (d + a_ioff),
-                        (const uint32_t *) (d + a_ilen), n, max_len, d + a_out,
+                        (const uint32_t *) (d + a_ilen), n, max_len, max_cap, d + a_out,
                         (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_ocap),
                         (uint32_t *) (d + a_olen), (void *) c->stream);
     if (rc != 0) return rc;
@@ -496,7 +498,7 @@ static int run_dgram(rc_ctx *c, int decode, const uint8_t *in, const uint64_t *i
     g.checksum = checksum ? 1u : 0u;
     int rc = rc_hip_dgram_launch(decode ? RC_DGRAM_DEC_PREP : RC_DGRAM_ENC_PREP, &g, stream);
     if (rc) return rc;
-    rc = run_device(c, decode, in, g.p_off, g.p_len, n, DG_MTU, out, g.q_off, g.q_cap, g.c_len, stream);
+    rc = run_device(c, decode, in, g.p_off, g.p_len, n, DG_MTU, 0, out, g.q_off, g.q_cap, g.c_len, stream);
     if (rc) return rc;
     rc = rc_hip_dgram_launch(decode ? RC_DGRAM_DEC_STAGE : RC_DGRAM_ENC_STAGE, &g, stream);
     if (rc) return rc;

@@ -1092,11 +1092,16 @@ extern "C" const char* rc_hip_fast_kernel_name(int decompress, uint32_t kernel)
 constexpr uint32_t kLdsPerCu = 160 * 1024;   // gfx950
 
 // LDS per wavefront of the wave kernels.  The decoder's model grows with the
-// bytes it produces, not the bytes it reads (max_len bounds the input), so it
-// always gets the largest arena.
-uint32_t wave_lds(bool decompress, uint32_t max_len)
+// bytes it produces, not the bytes it reads (max_len bounds the input): its
+// arena is sized by the output bound when the caller knows one (max_out, the
+// host-pointer batches), else it takes the largest arena.
+uint32_t wave_lds(bool decompress, uint32_t max_len, uint32_t max_out)
 {
-    return decompress ? kMaxLds : lds_bytes_for(max_len);
+    if (!decompress) return lds_bytes_for(max_len);
+    if (max_out == 0) return kMaxLds;
+    uint64_t total = kInStage + stage_bytes_for(max_len) + 22ull * max_out + 2048;
+    if (total > kMaxLds) total = kMaxLds;
+    return static_cast<uint32_t>(total & ~15ull);
 }
 
 static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
@@ -1112,7 +1117,7 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     // the wavefront-per-packet kernel: a packet's byte chain runs there with
     // its model in LDS, 1.4-2.9x sooner than on one lane of the lane kernels
     // (tools/smallbatch.py).  Larger batches are throughput work: lanes.
-    const uint32_t lds_w = wave_lds(decompress, max_len);
+    const uint32_t lds_w = wave_lds(decompress, max_len, b->max_out);
     const uint32_t resident = ws->cus * (kLdsPerCu / lds_w ? kLdsPerCu / lds_w : 1u);
     // (not min(): on the host it resolves to the int overload, and small_max
     // RC_SMALL_AUTO would read as -1)

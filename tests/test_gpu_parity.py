@@ -280,6 +280,44 @@ def test_host_pointer_batches_large(coder):
     assert np.array_equal(dout[: d.size], d)
 
 
+def test_host_pointer_decoder_sized_by_out_cap(coder):
+    """Host-pointer decompress batches pass max(out_cap) down (rc_host.c
+    run_host), so the wave decoder sizes its LDS arena by the output bound
+    and batches of 513-1280 packets of <= 1400 B now fit on the chip at one
+    wavefront per packet (rc_kernels.hip wave_lds).  Bit-exact against the
+    oracle on both sides of the old 512-packet limit, with tight caps (a
+    model outgrowing the smaller arena must take the exact path)."""
+    import ctypes as C
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(77)
+    lib = coder.lib
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    for n in (513, 1000, 1280):
+        pk = [rng.integers(0, int(rng.choice([2, 17, 256])), size=int(rng.integers(1, 1401)),
+                           dtype=np.uint8).tobytes() for _ in range(n)]
+        ln = np.array([len(x) for x in pk], np.uint32)
+        o = np.zeros(n, np.uint64)
+        o[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+        d = np.frombuffer(b"".join(pk), np.uint8).copy()
+        cap = (2 * ln.astype(np.int64) + 64).astype(np.uint32)
+        coff = np.zeros(n, np.uint64)
+        coff[1:] = np.cumsum(cap[:-1].astype(np.uint64))
+        cout = np.zeros(int(coff[-1] + cap[-1]) + 16, np.uint8)
+        clen = np.zeros(n, np.uint32)
+        assert lib.enet_rc_compress_batch_host(coder.ctx, p(d), p(o), p(ln), n, p(cout), p(coff), p(cap),
+                                               p(clen)) == 0
+        for i in range(n):
+            got = cout[int(coff[i]): int(coff[i]) + int(clen[i])].tobytes()
+            assert (int(clen[i]), got) == port.compress(pk[i], out_limit=int(cap[i])), f"n={n} packet {i}"
+        dout = np.zeros(d.size + 16, np.uint8)
+        dlen = np.zeros(n, np.uint32)
+        assert lib.enet_rc_decompress_batch_host(coder.ctx, p(cout), p(coff), p(clen), n, p(dout), p(o), p(ln),
+                                                 p(dlen)) == 0
+        assert np.array_equal(dlen, ln), f"n={n}"
+        assert np.array_equal(dout[: d.size], d), f"n={n}"
+
+
 def test_long_packets_batch_vs_oracle(coder):
     """2048 packets of 1900-4096 B (random, low-entropy, runs): compress.c's
     model reset at 4094 nodes happens inside the lane kernels (rc_lane3.hip
