@@ -96,7 +96,15 @@ class RangeCoder:
         self._batch(self.lib.enet_rc_compress_batch_device, inp, in_off, in_len, max_len, out, out_off,
                     out_cap, out_len, stream)
 
-    def decompress_batch(self, inp, in_off, in_len, out, out_off, out_cap, out_len, max_len=0, stream=None):
+    def decompress_batch(self, inp, in_off, in_len, out, out_off, out_cap, out_len, max_len=0, stream=None,
+                         max_out=0):
+        """max_out: an upper bound of out_cap[] (0 = unknown); with it, small
+        batches decode with a right-sized model (enet_rc_decompress_batch_device_bounded)."""
+        if max_out:
+            fn = self.lib.enet_rc_decompress_batch_device_bounded
+            self._batch(lambda *a: fn(*a[:-1], max_out, a[-1]), inp, in_off, in_len, max_len, out, out_off,
+                        out_cap, out_len, stream)
+            return
         self._batch(self.lib.enet_rc_decompress_batch_device, inp, in_off, in_len, max_len, out, out_off,
                     out_cap, out_len, stream)
 

@@ -47,7 +47,8 @@ def _load() -> C.CDLL:
     for name, args in (("enet_rc_compress_batch_device", batch_dev),
                        ("enet_rc_decompress_batch_device", batch_dev),
                        ("enet_rc_compress_batch_host", batch_host),
-                       ("enet_rc_decompress_batch_host", batch_host)):
+                       ("enet_rc_decompress_batch_host", batch_host),
+                       ("enet_rc_decompress_batch_device_bounded", batch_dev[:-1] + [u32, vp])):
         f = getattr(lib, name)
         f.restype = C.c_int
         f.argtypes = args

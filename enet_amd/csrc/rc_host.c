@@ -235,6 +235,15 @@ int enet_rc_decompress_batch_device(void *context, const uint8_t *in, const uint
                       out_cap, out_len, stream);
 }
 
+int enet_rc_decompress_batch_device_bounded(void *context, const uint8_t *in, const uint64_t *in_off,
+                                            const uint32_t *in_len, size_t n, uint32_t max_len,
+                                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                                            uint32_t *out_len, uint32_t max_out, void *stream)
+{
+    return run_device((rc_ctx *) context, 1, in, in_off, in_len, n, max_len, max_out, out, out_off,
+                      out_cap, out_len, stream);
+}
+
 /* Host-memory batch: [in | in_off | in_len | out_off | out_cap | out_len | out]
  * packed into one pinned buffer, one H2D, kernels, one D2H of out_len+out. */
 /* ---- host-side copies on several threads (the staging memcpy in and the

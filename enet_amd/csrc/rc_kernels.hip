@@ -1118,7 +1118,12 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     // its model in LDS, 1.4-2.9x sooner than on one lane of the lane kernels
     // (tools/smallbatch.py).  Larger batches are throughput work: lanes.
     const uint32_t lds_w = wave_lds(decompress, max_len, b->max_out);
-    const uint32_t resident = ws->cus * (kLdsPerCu / lds_w ? kLdsPerCu / lds_w : 1u);
+    // The decoder caps at 4 wavefronts per CU: with a right-sized model 5 fit,
+    // but 1280 random packets then decode slower than on the lanes (5.9 vs
+    // 3.9 ms, profiles/r1h_smallbatch.log).
+    uint32_t per_cu = kLdsPerCu / lds_w ? kLdsPerCu / lds_w : 1u;
+    if (decompress && per_cu > 4u) per_cu = 4u;
+    const uint32_t resident = ws->cus * per_cu;
     // (not min(): on the host it resolves to the int overload, and small_max
     // RC_SMALL_AUTO would read as -1)
     const bool small = ws->kernel == RC_KERNEL_LANE3 && b->n <= resident && b->n <= ws->small_max;

@@ -99,6 +99,17 @@ int enet_rc_decompress_batch_device(void *context, const uint8_t *in, const uint
                                     const uint32_t *in_len, size_t n, uint32_t max_len,
                                     uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
                                     uint32_t *out_len, void *stream);
+/* As enet_rc_decompress_batch_device, plus max_out >= every out_cap[i] (0 =
+ * unknown).  The bound sizes the model of the wavefront-per-packet decoder
+ * that small batches run on, so twice as many packets decode at one wavefront
+ * per packet (1024 instead of 512 at max_out 1200).  A smaller max_out than some
+ * out_cap[i] is not an error: a packet whose model outgrows it takes the exact
+ * path.  No reference counterpart (the reference decompresses one datagram
+ * per call, compress.c:506). */
+int enet_rc_decompress_batch_device_bounded(void *context, const uint8_t *in, const uint64_t *in_off,
+                                            const uint32_t *in_len, size_t n, uint32_t max_len,
+                                            uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                                            uint32_t *out_len, uint32_t max_out, void *stream);
 
 /* Same with HOST pointers: copies in through pinned staging, runs, copies
  * out, and returns when the results are in host memory. */

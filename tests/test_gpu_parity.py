@@ -49,7 +49,7 @@ def _pack(packets):
     return d, o, l
 
 
-def _run(coder, decompress, packets, caps, max_len=None):
+def _run(coder, decompress, packets, caps, max_len=None, max_out=0):
     d, o, l = _pack(packets)
     caps = np.asarray(caps, dtype=np.int64)
     out_off = np.zeros(len(caps), np.int64)
@@ -60,7 +60,7 @@ def _run(coder, decompress, packets, caps, max_len=None):
             _dev(out_off, torch.int64), _dev(caps, torch.int32), out_len)
     ml = int(l.max()) if max_len is None and len(l) else (max_len or 0)
     if decompress:
-        coder.decompress_batch(*args, max_len=ml)
+        coder.decompress_batch(*args, max_len=ml, max_out=max_out)
     else:
         coder.compress_batch(*args, max_len=ml)
     torch.cuda.synchronize()
@@ -280,10 +280,28 @@ def test_host_pointer_batches_large(coder):
     assert np.array_equal(dout[: d.size], d)
 
 
+def test_device_decoder_bounded_vs_oracle(coder):
+    """enet_rc_decompress_batch_device_bounded: the caller's output bound sizes
+    the wave decoder's model, so 513-1024-packet batches decode one wavefront
+    per packet; bit-exact, including a bound below some caps (those packets
+    outgrow the smaller model and take the exact path)."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(91)
+    for n, bound in ((513, 1400), (1000, 1400), (1280, 1200), (600, 200)):
+        pk = [rng.integers(0, int(rng.choice([2, 17, 256])), size=int(rng.integers(1, 1401)),
+                           dtype=np.uint8).tobytes() for _ in range(n)]
+        caps = [2 * len(p) + 64 for p in pk]
+        res = _run(coder, False, pk, caps)
+        assert res == [port.compress(p, out_limit=c) for p, c in zip(pk, caps)]
+        back = _run(coder, True, [r[1] for r in res], [len(p) for p in pk], max_out=bound)
+        assert back == [(len(p), p) for p in pk], f"n={n} bound={bound}"
+
+
 def test_host_pointer_decoder_sized_by_out_cap(coder):
     """Host-pointer decompress batches pass max(out_cap) down (rc_host.c
     run_host), so the wave decoder sizes its LDS arena by the output bound
-    and batches of 513-1280 packets of <= 1400 B now fit on the chip at one
+    and batches of 513-1024 packets of <= 1400 B now fit on the chip at one
     wavefront per packet (rc_kernels.hip wave_lds).  Bit-exact against the
     oracle on both sides of the old 512-packet limit, with tight caps (a
     model outgrowing the smaller arena must take the exact path)."""
