@@ -223,11 +223,18 @@ def compress_batch(coder: RangeCoder, inp, in_off, in_len, max_len: int, out_cap
     return out, out_off, out_cap, out_len
 
 
-def decompress_batch(coder: RangeCoder, inp, in_off, in_len, out_cap, max_len: int = 0):
+def decompress_batch(coder: RangeCoder, inp, in_off, in_len, out_cap, max_len: int = 0,
+                     max_out: Optional[int] = None):
+    """Allocates outputs of out_cap[i] bytes per packet and decompresses.
+    ``max_out`` bounds out_cap[] (default: its maximum), so small batches get
+    the right-sized decoder (enet_rc_decompress_batch_device_bounded).
+    Returns ``(out, out_off, out_len)`` device tensors."""
     import torch
     out_off = _caps_offsets(out_cap)
     total = int(out_off[-1].item() + out_cap[-1].item()) if out_cap.numel() else 0
     out = torch.empty(max(total, 1), dtype=torch.uint8, device=inp.device)
     out_len = torch.empty_like(in_len)
-    coder.decompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, max_len)
+    if max_out is None:
+        max_out = max(int(out_cap.max().item()), 0) if out_cap.numel() else 0
+    coder.decompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, max_len, max_out=max_out)
     return out, out_off, out_len

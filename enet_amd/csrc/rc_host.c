@@ -468,8 +468,6 @@ static int dgram_reserve(rc_ctx *c, size_t n, int scratch)
     if (scratch && n * DG_MTU > c->dg_scratch_cap) {
         hipDeviceSynchronize();
         if (c->dg_scratch) hipFree(c->dg_scratch);
-    if (c->d_pack) hipFree(c->d_pack);
-    if (c->d_bsum) hipFree(c->d_bsum);
         c->dg_scratch = NULL; c->dg_scratch_cap = 0;
         if (hipMalloc((void **) &c->dg_scratch, n * DG_MTU) != hipSuccess) return -1;
         c->dg_scratch_cap = n * DG_MTU;

@@ -1065,11 +1065,20 @@ constexpr uint32_t kMaxLds = 65536;
 
 uint32_t stage_bytes_for(uint32_t max_len) { return ((max_len + 8 + 15) / 16) * 16; }
 
+constexpr uint32_t kMinArena = 4096;
+
+uint64_t arena_bytes_for(uint32_t model_bytes_bound)
+{
+    const uint64_t a = 22ull * model_bytes_bound + 2048;
+    return a < kMinArena ? kMinArena : a;
+}
+
 uint32_t lds_bytes_for(uint32_t max_len)
 {
     // arena: <= 18 B of model per input byte in the worst case (o2 header 8 +
-    // o2 entry 4 + o1 entry 6) plus power-of-two slack.
-    uint64_t arena = 22ull * max_len + 2048;
+    // o2 entry 4 + o1 entry 6) plus power-of-two slack; never below the 4 KB
+    // the launcher requires of a usable arena.
+    uint64_t arena = arena_bytes_for(max_len);
     uint64_t total = kInStage + stage_bytes_for(max_len) + arena;
     if (total > kMaxLds) total = kMaxLds;
     return static_cast<uint32_t>(total & ~15ull);
@@ -1099,7 +1108,7 @@ uint32_t wave_lds(bool decompress, uint32_t max_len, uint32_t max_out)
 {
     if (!decompress) return lds_bytes_for(max_len);
     if (max_out == 0) return kMaxLds;
-    uint64_t total = kInStage + stage_bytes_for(max_len) + 22ull * max_out + 2048;
+    uint64_t total = kInStage + stage_bytes_for(max_len) + arena_bytes_for(max_out);
     if (total > kMaxLds) total = kMaxLds;
     return static_cast<uint32_t>(total & ~15ull);
 }
@@ -1138,7 +1147,7 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     } else {
         uint32_t stage = stage_bytes_for(max_len);
         uint32_t lds = lds_w;
-        if (stage + kInStage + 4096 > lds) {        // absurd max_len: everything goes exact
+        if (stage + kInStage + kMinArena > lds) {   // absurd max_len: everything goes exact
             stage = 16; lds = 16384;
         }
         if (decompress)

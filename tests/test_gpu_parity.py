@@ -365,3 +365,73 @@ def test_long_packets_batch_vs_oracle(coder):
     assert fnv_digest(blob, goff, gl) == fnv_digest(out, oo, ol)
     back = _run(coder, True, [r[1] for r in res], [len(p) for p in pk])
     assert all(b == (len(p), p) for b, p in zip(back, pk))
+
+
+def test_device_decoder_small_bounds(coder):
+    """Small output bounds (game-state-sized packets, bound 64, bound 1, and the
+    largest bound 0xFFFFFFFF): the wave decoder's arena has a floor of 4 KB, so
+    a small bound never routes valid streams to the 256-thread exact path
+    (rc_kernels.hip arena_bytes_for).  Bit-exact, and no exact-path packets
+    where every stream fits its model."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(64)
+    for n, lo, hi, bound in ((1024, 16, 65, 64), (256, 1, 2, 1), (300, 1, 400, 0xFFFFFFFF), (1024, 48, 49, 48)):
+        pk = [rng.integers(0, int(rng.choice([2, 17, 256])), size=int(rng.integers(lo, hi)),
+                           dtype=np.uint8).tobytes() for _ in range(n)]
+        caps = [2 * len(p) + 64 for p in pk]
+        res = _run(coder, False, pk, caps)
+        assert res == [port.compress(p, out_limit=c) for p, c in zip(pk, caps)]
+        back = _run(coder, True, [r[1] for r in res], [len(p) for p in pk], max_out=bound)
+        assert back == [(len(p), p) for p in pk], f"n={n} bound={bound}"
+        assert coder.last_exact_count() == 0, f"n={n} bound={bound}: valid streams took the exact path"
+
+
+def test_small_packets_compress_not_exact(coder):
+    """Compress batches of short packets (max_len < 94) stay on the fast
+    kernels: the arena floor keeps them off the exact path."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(48)
+    pk = [rng.integers(0, 256, size=int(rng.integers(1, 65)), dtype=np.uint8).tobytes() for _ in range(1024)]
+    caps = [2 * len(p) + 64 for p in pk]
+    res = _run(coder, False, pk, caps)
+    assert res == [port.compress(p, out_limit=c) for p, c in zip(pk, caps)]
+    assert coder.last_exact_count() == 0
+
+
+def test_host_batches_around_checksummed_datagrams(coder):
+    """One context: a large host batch (device-side packing buffers), then a
+    checksummed datagram encode with a larger n (grows the datagram scratch),
+    then a large host batch again, all bit-exact.  Guards the ownership of the
+    packing buffers (rc_host.c pack_reserve / dgram_reserve)."""
+    import ctypes as C
+    from oracle.pyoracle import compress_batch as ocompress, datagram_encode, fnv_digest, Coder
+    lib = coder.lib
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    d, o, l = synth.mixed_batch(3000)            # > 1 MiB out: the packing path
+    n = len(l)
+    ln = l.astype(np.uint32)
+    cap = (2 * ln.astype(np.int64) + 64).astype(np.uint32)
+    coff = np.zeros(n, np.uint64)
+    coff[1:] = np.cumsum(cap[:-1].astype(np.uint64))
+    want, wo, wcap, wl = ocompress(d, o, l, "port")
+
+    def host_round():
+        cout = np.zeros(int(coff[-1] + cap[-1]) + 16, np.uint8)
+        clen = np.zeros(n, np.uint32)
+        assert lib.enet_rc_compress_batch_host(coder.ctx, p(d), p(o), p(ln), n, p(cout), p(coff), p(cap),
+                                               p(clen)) == 0
+        assert np.array_equal(clen, wl)
+        assert fnv_digest(cout, coff, clen) == fnv_digest(want, wo, wl)
+
+    host_round()
+    port = Coder("port")
+    rng = np.random.default_rng(3)
+    dg = [b"\x80\x01\x00\x02" + bytes(4) + rng.integers(0, 3, size=int(rng.integers(1, 1200)),
+                                                          dtype=np.uint8).tobytes() for _ in range(4000)]
+    seeds = [int(s) for s in rng.integers(0, 2**32, size=len(dg))]
+    enc = coder.datagrams(False, dg, checksum=True, seeds=seeds)
+    for i in range(0, len(dg), 97):
+        assert enc[i] == datagram_encode(dg[i], True, seeds[i], port)
+    host_round()
