@@ -32,7 +32,8 @@ typedef struct {
 /* Device workspace owned by a coder context. */
 typedef struct {
     uint32_t *flag_list;    /* [n_cap] packets routed to the exact path */
-    uint32_t *counters;     /* [4]: 0 = flagged count, 1 = work queue head (fast), 2 = exact queue head */
+    uint32_t *counters;     /* [4]: 0 = flagged count, 1 = work queue head (fast), 2 = exact queue head,
+                               3 = packets the two-pass encoder leaves to the lane kernels */
     void     *exact_pool;   /* exact_slots * RC_EXACT_POOL_BYTES */
     uint32_t  exact_slots;
     uint32_t  n_cap;
@@ -46,6 +47,13 @@ typedef struct {
     uint32_t  cus;          /* compute units of the device */
     uint32_t  small_max;    /* lane3 contexts: batches of up to this many packets (and no more than
                                fit on the chip at once) run on the wave kernel; RC_SMALL_AUTO = no cap */
+    /* two-pass encoder (rc_enc2.hip): record stream and the packets it leaves to the lane kernels */
+    void     *enc2_stream;  /* NULL: the encoder is off (ENET_RC_ENC2=0) or not allocated yet */
+    uint64_t  enc2_cap;     /* bytes */
+    uint32_t *enc2_list;    /* [n_cap] */
+    /* lane kernels: when set, run only the sub_count[0] packets of sub_list */
+    const uint32_t *sub_list;
+    const uint32_t *sub_count;
 } rc_workspace_dev;
 
 #define RC_SMALL_AUTO 0xFFFFFFFFu
@@ -60,6 +68,13 @@ typedef struct {
 /* Launchers (rc_kernels.hip).  Return 0 or a hipError_t value. Stream-ordered, no host sync. */
 int rc_hip_compress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
 int rc_hip_decompress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
+
+/* Two-pass encoder (rc_enc2.hip): record-stream bytes per packet of up to
+ * max_len bytes, and the launcher (both passes, chunked by ws->enc2_cap;
+ * packets off its fast path are listed in ws->enc2_list, count in
+ * ws->counters[3]). */
+uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len);
+int rc_hip_enc2_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
 uint32_t rc_hip_lane_region_bytes(uint32_t max_len);    /* model v2 */

@@ -1,0 +1,384 @@
+// rc_enc2.hip -- two-pass range-coder encoder (compress.c:246-342), bit-exact.
+//
+// compress.c's order-1 and order-2 statistics are functions of the packet's
+// own bytes, never of the coder's output.  The lane kernels (rc_lane3.hip)
+// still rebuild that model byte by byte in HBM, one random record access per
+// byte; this encoder derives it from the packet instead, and keeps only the
+// root context (order 0) and the range coder serial:
+//
+//   pass 1, rc_enc2_scan: one 256-thread workgroup per packet, in LDS.
+//     Positions 1..N-1 are bucketed by their previous byte x[i-1].  Both
+//     sub-contexts of position i -- order 1 = (x[i-1]), order 2 =
+//     (x[i-2], x[i-1]) -- hold only positions of i's bucket, so thread b
+//     walks bucket b in position order and derives every order-1/order-2
+//     coding interval from counts over the position's bucket predecessors
+//     (compress.c:159-199, :286-316):
+//        escapes = 5 * dist, total = escapes + 2 * t,
+//        count = 2 * same, under = 2 * less
+//     (t earlier visits of the context, dist of them with a new symbol,
+//     same of them with this symbol, less with a smaller one).  A position
+//     visits order 1 only if order 2 lacked its byte, and the root only if
+//     order 1 lacked it too.  Output: one 8-B record per position, written
+//     straight to the packet's slot of the record stream (no LDS staging).
+//   pass 2, rc_enc2_code: one lane per packet.  The root context in LDS
+//     (rc_lane_common.h) and the range coder, over the records.  The records
+//     also carry the packet's bytes, so a lane reads one uniform stream:
+//     every lane consumes one record per step, its loads are the same for all
+//     lanes (issued three chunks ahead), and the output window is stored
+//     every step (to a dummy slot when nothing is pending).  With the same
+//     memory operations on every path, the compiler never has to wait for
+//     all outstanding stores before using a record (vmcnt is in order).
+//
+// tests/proto/twopass.py restates both passes and the record format in
+// Python (checked against the oracle on the CPU, tests/test_twopass_model.py).
+//
+// Fast path: 1 <= N <= 1919 (no model reset, compress.c:148-157) and no
+// bucket over 64 positions (every statistic <= 63, so no count reaches the
+// rescale threshold, compress.c:313).  Other packets are listed for the lane
+// kernels, which run after the two passes on that list only.
+//
+// Record of position i: two words (w0, w1)
+//   w0 bits 0-2 type, 3-8 tA, 9-14 dA, 16-27 ext
+//   w1 bits 0-23 second (type 5), 24-31 the byte x[i]
+//   type 0  no sub-context codes (root)
+//        1  order 1 escape, (tA, dA) = (t1, dist1)                  (root)
+//        2  order 1 hit (t1, dist1), ext = same1 | less1 << 6
+//        3  order 2 escape (t2, dist2)                              (root)
+//        4  order 2 escape (t2, dist2), ext = t1 | dist1 << 6       (root)
+//        5  order 2 escape (t2, dist2), second = t1 | dist1 << 6 |
+//           same1 << 12 | less1 << 18 (order 1 hit)
+//        6  order 2 hit (t2, dist2), ext = same2 | less2 << 6
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rc_abi_internal.h"
+#include "rc_udiv.h"
+#include "rc_lane_common.h"
+
+namespace {
+
+constexpr uint32_t kE2MaxLen = 1919;          // compress.c:148-157: no reset below 1920 B
+constexpr uint32_t kE2Bucket = 64;            // statistics <= 63
+constexpr uint32_t kScanThreads = 256;        // one thread per bucket
+constexpr uint32_t kSkipFallback = 0xFFFFFFFFu;   // first word of a slot: lane kernels
+constexpr uint32_t kSkipDone = 0xFFFFFFFEu;       // empty packet, out_len already 0
+
+struct E2Params {
+    uint8_t*        stream;     // record stream, one slot per packet of the chunk
+    uint64_t        slot_bytes;
+    uint32_t        lo, hi;     // chunk: batch indices [lo, hi)
+    const uint32_t* order;      // batch index -> packet (length-binned), or null
+    const uint32_t* bins;       // bins[RC_LEN_BINS] != 0: order not built (uniform batch)
+    uint32_t*       list;       // packets for the lane kernels
+    uint32_t*       count;
+};
+
+DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
+{
+    return (e.order && !e.bins[RC_LEN_BINS]) ? e.order[idx] : idx;
+}
+
+// ------------------------------------------------------------------ pass 1
+
+struct ScanLds {
+    uint8_t  x[2048];                 // packet bytes at x[mis + i]
+    uint32_t cnt[256];                // bucket sizes, then fill pointers
+    uint32_t start[260];              // bucket starts, start[256] = N - 1
+    uint32_t e[2048];                 // elements in bucket order (below)
+    uint32_t wsum[8];
+};
+
+// element word: pos (0-10) | v (11-18) | a | 256 (19-27, 0 for position 1) |
+//               found2 (28) | visits order 1 (29) | found1 (30)
+constexpr uint32_t kF2 = 1u << 28, kV1 = 1u << 29, kF1 = 1u << 30;
+
+DEV uint32_t wave_incl_scan(uint32_t x)
+{
+    const int l = static_cast<int>(threadIdx.x & 63);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        x += l >= d ? y : 0u;
+    }
+    return x;
+}
+
+// exclusive prefix over the workgroup's threads; total of all; two barriers
+DEV uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, uint32_t& total)
+{
+    const uint32_t inc = wave_incl_scan(x), w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanThreads / 64; ++k) {
+        base += k < w ? wsum[k] : 0u;
+        all += wsum[k];
+    }
+    __syncthreads();
+    total = all;
+    return base + inc - x;
+}
+
+DEV void fallback(const E2Params& e, uint32_t* slot, uint32_t pkt)
+{
+    slot[0] = kSkipFallback;
+    e.list[atomicAdd(e.count, 1u)] = pkt;
+}
+
+// one predecessor u of an element (v, akey): SWAR accumulators
+// t | same << 8 | less << 16 | dist << 24 of order 2 and order 1
+DEV void pair(uint32_t u, uint32_t v, uint32_t akey, bool in, uint32_t& acc2, uint32_t& acc1)
+{
+    const uint32_t uv = (u >> 11) & 255;
+    const uint32_t base = 1u | (uv == v ? 0x100u : 0u) | (uv < v ? 0x10000u : 0u);
+    const bool m2 = in && ((u >> 19) & 511) == akey;
+    const bool m1 = in && (u & kV1) != 0;
+    acc2 += m2 ? (base | ((u & kF2) ? 0u : 0x1000000u)) : 0u;
+    acc1 += m1 ? (base | ((u & kF1) ? 0u : 0x1000000u)) : 0u;
+}
+
+// position j of bucket [bs, ...): its statistics over the predecessors
+// [bs, j) (final: their flags are set), its flags, and its record
+DEV void scan_position(ScanLds& s, uint32_t bs, uint32_t j, const uint8_t* x, uint2* rec)
+{
+    const uint32_t w = s.e[j];
+    const uint32_t pos = w & 2047, v = (w >> 11) & 255;
+    const uint32_t akey = (w & (256u << 19)) ? (w >> 19) & 511 : 1024u;   // never matches at position 1
+    uint32_t acc2 = 0, acc1 = 0;
+    for (uint32_t q = bs & ~3u; q < j; q += 4) {      // 4 predecessors per LDS read
+        const uint4 u = *reinterpret_cast<const uint4*>(&s.e[q]);
+        pair(u.x, v, akey, q >= bs, acc2, acc1);
+        pair(u.y, v, akey, q + 1 >= bs && q + 1 < j, acc2, acc1);
+        pair(u.z, v, akey, q + 2 >= bs && q + 2 < j, acc2, acc1);
+        pair(u.w, v, akey, q + 3 < j, acc2, acc1);
+    }
+    const uint32_t t2 = acc2 & 255, same2 = (acc2 >> 8) & 255, less2 = (acc2 >> 16) & 255, d2 = acc2 >> 24;
+    const bool f2 = same2 != 0;
+    const bool v1 = !f2;                              // compress.c:315: order 1 only after an escape
+    if (!v1) acc1 = 0;
+    const uint32_t t1 = acc1 & 255, same1 = (acc1 >> 8) & 255, less1 = (acc1 >> 16) & 255, d1 = acc1 >> 24;
+    const bool f1 = v1 && same1 != 0;
+    s.e[j] = w | (f2 ? kF2 : 0u) | (v1 ? kV1 : 0u) | (f1 ? kF1 : 0u);
+    uint32_t r, r2 = 0;
+    if (f2) {
+        r = 6u | t2 << 3 | d2 << 9 | (same2 | less2 << 6) << 16;
+    } else if (t2 != 0) {
+        if (t1 == 0) r = 3u | t2 << 3 | d2 << 9;
+        else if (f1) { r = 5u | t2 << 3 | d2 << 9; r2 = t1 | d1 << 6 | same1 << 12 | less1 << 18; }
+        else r = 4u | t2 << 3 | d2 << 9 | (t1 | d1 << 6) << 16;
+    } else if (t1 == 0) {
+        r = 0u;
+    } else if (f1) {
+        r = 2u | t1 << 3 | d1 << 9 | (same1 | less1 << 6) << 16;
+    } else {
+        r = 1u | t1 << 3 | d1 << 9;
+    }
+    rec[pos] = make_uint2(r, r2 | v << 24);
+}
+
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_scan(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) ScanLds s;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
+        const uint32_t pkt = packet_of(e, idx);
+        uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
+        const uint32_t n = b.in_len[pkt];
+        if (n == 0 || n > kE2MaxLen) {                 // compress.c:257 / possible model reset
+            if (t == 0) {
+                if (n == 0) { slot[0] = kSkipDone; b.out_len[pkt] = 0; }
+                else fallback(e, slot, pkt);
+            }
+            continue;
+        }
+        // the packet into LDS: aligned 16-B chunks, x = s.x + misalignment
+        const uintptr_t src = reinterpret_cast<uintptr_t>(b.in + b.in_off[pkt]);
+        const uintptr_t a16 = src & ~static_cast<uintptr_t>(15);
+        const uint32_t mis = static_cast<uint32_t>(src & 15);
+        const uint32_t chunks = (mis + n + 15) >> 4;
+        for (uint32_t c = t; c < chunks; c += kScanThreads)
+            *reinterpret_cast<uint4*>(s.x + 16 * c) = gload16(a16 + 16 * c);
+        s.cnt[t] = 0;
+        __syncthreads();
+        const uint8_t* x = s.x + mis;
+        for (uint32_t i = 1 + t; i < n; i += kScanThreads) atomicAdd(&s.cnt[x[i - 1]], 1u);
+        __syncthreads();
+        const uint32_t c = s.cnt[t];
+        if (__syncthreads_or(c > kE2Bucket)) {
+            if (t == 0) fallback(e, slot, pkt);
+            continue;
+        }
+        uint32_t total;
+        const uint32_t ex = block_excl_scan(c, s.wsum, total);
+        s.start[t] = ex;
+        s.cnt[t] = ex;
+        if (t == 0) s.start[256] = total;
+        __syncthreads();
+        for (uint32_t i = 1 + t; i < n; i += kScanThreads) {
+            const uint32_t k = atomicAdd(&s.cnt[x[i - 1]], 1u);
+            s.e[k] = i | static_cast<uint32_t>(x[i]) << 11 | (i >= 2 ? (x[i - 2] | 256u) << 19 : 0u);
+        }
+        __syncthreads();
+        // bucket t: position order (the atomics placed it nearly sorted), then
+        // its positions one by one
+        uint2* rec = reinterpret_cast<uint2*>(slot);
+        const uint32_t bs = s.start[t], be = s.start[t + 1];
+        for (uint32_t j = bs + 1; j < be; ++j) {
+            const uint32_t w = s.e[j];
+            uint32_t q = j;
+            while (q > bs && (s.e[q - 1] & 2047) > (w & 2047)) { s.e[q] = s.e[q - 1]; --q; }
+            s.e[q] = w;
+        }
+        for (uint32_t j = bs; j < be; ++j) scan_position(s, bs, j, x, rec);
+        if (t == 0) rec[0] = make_uint2(0u, static_cast<uint32_t>(x[0]) << 24);   // position 0: root only
+        __syncthreads();                              // LDS reuse by the next packet
+    }
+}
+
+// ------------------------------------------------------------------ pass 2
+
+// compress.c:139-146 window store at the top of a step, issued on every path:
+// a pending window goes to its place, otherwise the same 16 B go to a dummy
+// slot of the lane (the first chunk of its record slot, already consumed).
+DEV void sink_flush_always(ByteSink& o, uintptr_t dummy)
+{
+    const bool edge = o.pend && o.wpaddr < o.lo;
+    const uintptr_t a = (o.pend && !edge) ? o.wpaddr : dummy;
+    const v4u32 d = {o.wp.x, o.wp.y, o.wp.z, o.wp.w};
+    *GPTR(v4u32, a) = d;
+    if (rare_lane(edge)) {
+        if (edge) sink_bytes(o.wpaddr, o.wp, 0, 16, o.lo);
+    }
+    o.pend = false;
+}
+
+// interval of a sub-context code from (t, dist[, same, less]): compress.c:301-308
+DEV void sub_interval(uint32_t t, uint32_t d, uint32_t same, uint32_t less, bool hit, uint32_t& under,
+                      uint32_t& count, uint32_t& total)
+{
+    const uint32_t esc = 5 * d;
+    total = esc + 2 * t;
+    under = hit ? esc + 2 * less : 0u;
+    count = hit ? 2 * same : esc;
+}
+
+struct CodeState {
+    uint32_t low, range, rtot;
+    bool ok;
+};
+
+// one position: its sub-context codes, then the root (compress.c:286-337)
+DEV void code_step(CodeState& k, ByteSink& o, uint8_t* root, uint32_t w0, uint32_t w1, bool en,
+                   uintptr_t dummy)
+{
+    sink_flush_always(o, dummy);
+    en = en && k.ok;
+    const uint32_t typ = w0 & 7, ext = w0 >> 16, v = w1 >> 24;
+    // first sub-context code: order 2 (types 3-6) or order 1 (types 1, 2)
+    uint32_t un, ct, tt;
+    sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
+    enc_code(k.low, k.range, un, ct, tt, o, en && typ != 0, k.ok);
+    // order 1 after an order-2 escape (types 4, 5)
+    const uint32_t fb = typ == 5 ? w1 : ext;
+    sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un, ct, tt);
+    enc_code(k.low, k.range, un, ct, tt, o, en && (typ == 4 || typ == 5), k.ok);
+    // root, compress.c:318-329
+    const bool en0 = en && (typ <= 1 || typ == 3 || typ == 4);
+    uint32_t under0, cnt0;
+    root_lookup(root, v, under0, cnt0);
+    if (en0) root_add(root, v, cnt0);
+    enc_code(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, o, en0, k.ok);
+    k.rtot = en0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
+    const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
+    if (any_lane(rs0)) { if (rs0) k.rtot = root_rescale(root); }
+}
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void rc_enc2_code(rc_batch_dev b, E2Params e)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t idx = e.lo + blockIdx.x * 256 + threadIdx.x;
+    if (idx >= e.hi) return;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(e.stream) + static_cast<size_t>(idx - e.lo) * e.slot_bytes;
+    uint4 c0 = gload16(base);
+    if (c0.x >= kSkipDone) return;                    // lane kernels / empty
+    uint4 c1 = gload16(base + 16), c2 = gload16(base + 32);
+    const uint32_t pkt = packet_of(e, idx);
+    const uint32_t len = b.in_len[pkt];
+    uint8_t* root = smem + threadIdx.x * kRootStride;
+    ByteSink o;
+    sink_init(o, b.out + b.out_off[pkt], b.out_cap[pkt]);
+    root_clear(root);
+    CodeState k;
+    k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
+    __builtin_amdgcn_s_waitcnt(0);                    // settle the first chunks before the loop
+    // Six positions per iteration from three chunk registers; each register
+    // is reloaded right after its two positions are coded, with the chunk
+    // three ahead, and is next read two register-steps later.  (Rotating one
+    // set of registers instead would copy a load's result within the
+    // iteration that issued it, i.e. wait for it.)
+    uintptr_t a = base + 48;
+    for (uint32_t i = 0; any_lane(i < len && k.ok); i += 6, a += 48) {
+        code_step(k, o, root, c0.x, c0.y, i < len, base);
+        code_step(k, o, root, c0.z, c0.w, i + 1 < len, base);
+        c0 = gload16(a);
+        code_step(k, o, root, c1.x, c1.y, i + 2 < len, base);
+        code_step(k, o, root, c1.z, c1.w, i + 3 < len, base);
+        c1 = gload16(a + 16);
+        code_step(k, o, root, c2.x, c2.y, i + 4 < len, base);
+        code_step(k, o, root, c2.z, c2.w, i + 5 < len, base);
+        c2 = gload16(a + 32);
+    }
+    // flush, compress.c:139-146
+    bool ok = k.ok;
+    uint32_t low = k.low;
+    while (any_lane(ok && low != 0)) {
+        const bool more = ok && low != 0;
+        const bool full = more && o.n >= o.cap;
+        ok = ok && !full;
+        sink_put(o, low >> 24, 1, more && !full);
+        low = (more && !full) ? low << 8 : low;
+    }
+    sink_finish(o, ok);
+    b.out_len[pkt] = ok ? o.n : 0u;
+}
+
+}  // namespace
+
+// bytes of one packet's record slot for packets of up to max_len bytes
+extern "C" uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len)
+{
+    const uint64_t l = max_len < kE2MaxLen ? max_len : kE2MaxLen;
+    return ((8 * l + 15) & ~15ull) + 96;              // 8 B per position, + the chunks read ahead
+}
+
+// Both passes over the batch, in chunks that fit the record stream; packets
+// off the fast path end up in ws->enc2_list / counters[3] for the lane kernels.
+extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t slot = rc_hip_enc2_slot_bytes(b->max_len ? b->max_len : 4096);
+    uint64_t per = ws->enc2_cap / slot;
+    if (per == 0) return static_cast<int>(hipErrorInvalidValue);
+    E2Params e;
+    e.stream = static_cast<uint8_t*>(ws->enc2_stream);
+    e.slot_bytes = slot;
+    e.order = ws->order;
+    e.bins = ws->bins;
+    e.list = ws->enc2_list;
+    e.count = ws->counters + 3;
+    const uint32_t scan_blocks_max = ws->cus * 8;
+    for (uint64_t lo = 0; lo < b->n; lo += per) {
+        const uint64_t hi = lo + per < b->n ? lo + per : b->n;
+        e.lo = static_cast<uint32_t>(lo);
+        e.hi = static_cast<uint32_t>(hi);
+        const uint32_t cnt = static_cast<uint32_t>(hi - lo);
+        hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
+                           0, st, *b, e);
+        hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 255) / 256), dim3(256), 256 * kRootStride, st, *b, e);
+    }
+    return static_cast<int>(hipGetLastError());
+}

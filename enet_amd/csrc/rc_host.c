@@ -42,6 +42,7 @@ typedef struct {
     size_t h_stage_cap;
     uint32_t last_exact;
     uint32_t max_slots;             /* lanes with a model region (ENET_RC_SLOTS) */
+    int enc2_on;                    /* compress batches on the two-pass encoder (ENET_RC_ENC2=0: off) */
     uint32_t *crc_tables;           /* device: slice-by-16 + shift tables (rc_crc32.hip) */
     /* datagram framing workspace (rc_dgram.hip): per-datagram arrays + checksum scratch */
     uint8_t *dg_arrays;
@@ -63,16 +64,19 @@ static int ws_reserve(rc_ctx *c, size_t n)
     if (n <= c->ws.n_cap) return 0;
     size_t cap = c->ws.n_cap ? c->ws.n_cap : 1024;
     while (cap < n) cap *= 2;
-    uint32_t *fl = NULL, *ord = NULL;
+    uint32_t *fl = NULL, *ord = NULL, *el = NULL;
     if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) return -1;
     if (hipMalloc((void **) &ord, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(fl); return -1; }
+    if (hipMalloc((void **) &el, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(fl); hipFree(ord); return -1; }
     if (c->ws.flag_list) {
         hipDeviceSynchronize();
         hipFree(c->ws.flag_list);
         hipFree(c->ws.order);
+        hipFree(c->ws.enc2_list);
     }
     c->ws.flag_list = fl;
     c->ws.order = ord;
+    c->ws.enc2_list = el;
     c->ws.n_cap = (uint32_t) cap;
     return 0;
 }
@@ -105,6 +109,25 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     c->ws.lane_region = region;
     if (getenv("ENET_RC_DEBUG"))
         fprintf(stderr, "enet_rc: lane pool %p, %zu slots x %u B\n", c->ws.lane_pool, slots, region);
+    return 0;
+}
+
+/* Record stream of the two-pass encoder (rc_enc2.hip): one slot per packet,
+ * at most ENC2_STREAM_MAX bytes (larger batches run in chunks). */
+#define ENC2_STREAM_MAX (1ull << 30)
+
+static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
+{
+    if (!c->enc2_on || c->ws.kernel != RC_KERNEL_LANE3) return 0;
+    const uint64_t slot = rc_hip_enc2_slot_bytes(max_len ? max_len : 4096);
+    uint64_t want = (uint64_t) n * slot;
+    if (want > ENC2_STREAM_MAX) want = ENC2_STREAM_MAX > slot ? ENC2_STREAM_MAX : slot;
+    if (want <= c->ws.enc2_cap) return 0;
+    hipDeviceSynchronize();
+    if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
+    c->ws.enc2_stream = NULL; c->ws.enc2_cap = 0;
+    if (hipMalloc(&c->ws.enc2_stream, want) != hipSuccess) return -1;
+    c->ws.enc2_cap = want;
     return 0;
 }
 
@@ -163,6 +186,8 @@ void *enet_range_coder_create(void)
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
             cus = 256;
         c->ws.cus = (uint32_t) cus;
+        const char *e2 = getenv("ENET_RC_ENC2");
+        c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
         const char *sl = getenv("ENET_RC_SLOTS");
         c->max_slots = MAX_LANE_SLOTS;
         if (sl && atol(sl) >= 256 && atol(sl) <= (1l << 22)) c->max_slots = (uint32_t) atol(sl);
@@ -182,6 +207,8 @@ void enet_range_coder_destroy(void *context)
     if (c->ws.flag_list) hipFree(c->ws.flag_list);
     if (c->ws.counters) hipFree(c->ws.counters);
     if (c->ws.order) hipFree(c->ws.order);
+    if (c->ws.enc2_list) hipFree(c->ws.enc2_list);
+    if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
     if (c->ws.bins) hipFree(c->ws.bins);
     if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
@@ -207,6 +234,7 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
     if (ws_reserve(c, n) != 0) return (int) hipErrorOutOfMemory;
     if (c->ws.kernel != RC_KERNEL_WAVE && lanes_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
+    if (!decompress && enc2_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
     rc_batch_dev b;
     b.in = in; b.in_off = in_off; b.in_len = in_len;
     b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;

@@ -835,6 +835,14 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
         hipLaunchKernelGGL(rc_len_scatter, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins, ws->order);
         w.order = ws->order;
     }
+    if (ws->kernel == RC_KERNEL_LANE3 && !decompress && ws->enc2_stream) {
+        // the two-pass encoder takes what it can (rc_enc2.hip); the lanes run
+        // only the packets it lists
+        const int rc = rc_hip_enc2_launch(b, &w, stream);
+        if (rc != 0) return rc;
+        w.sub_list = ws->enc2_list;
+        w.sub_count = ws->counters + 3;
+    }
     if (ws->kernel == RC_KERNEL_LANE3) return rc_hip_lane3_launch(decompress, b, &w, blocks, stream);
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(256), lds, st, *b, w);

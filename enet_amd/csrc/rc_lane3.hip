@@ -942,8 +942,9 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
-    for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
-        const uint32_t pkt = order ? order[i] : i;
+    const uint32_t count = ws.sub_count ? *ws.sub_count : b.n;   // a sub-list: the two-pass encoder's leftovers
+    for (uint32_t i = slot; i < count; i += gridDim.x * per_block) {
+        const uint32_t pkt = ws.sub_list ? ws.sub_list[i] : (order ? order[i] : i);
         if (DECOMP) decompress_one3(b, ws, pkt, reg, root);
         else compress_one3(b, ws, pkt, reg, root, mtab);
     }
