@@ -51,6 +51,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "rc_abi_internal.h"
 #include "rc_udiv.h"
@@ -60,7 +61,7 @@ namespace {
 
 constexpr uint32_t kE2MaxLen = 1919;          // compress.c:148-157: no reset below 1920 B
 constexpr uint32_t kE2Bucket = 64;            // statistics <= 63
-constexpr uint32_t kScanThreads = 256;        // one thread per bucket
+constexpr uint32_t kScanThreads = 64;         // one wavefront per packet, four buckets per lane
 constexpr uint32_t kSkipFallback = 0xFFFFFFFFu;   // first word of a slot: lane kernels
 constexpr uint32_t kSkipDone = 0xFFFFFFFEu;       // empty packet, out_len already 0
 
@@ -72,6 +73,7 @@ struct E2Params {
     const uint32_t* bins;       // bins[RC_LEN_BINS] != 0: order not built (uniform batch)
     uint32_t*       list;       // packets for the lane kernels
     uint32_t*       count;
+    uint32_t        act;        // pass 2: packets per wavefront (64 or 32)
 };
 
 DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
@@ -84,8 +86,10 @@ DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 struct ScanLds {
     uint8_t  x[2048];                 // packet bytes at x[mis + i]
     uint32_t cnt[256];                // bucket sizes, then fill pointers
-    uint32_t start[260];              // bucket starts, start[256] = N - 1
-    uint32_t e[2048];                 // elements in bucket order (below)
+    uint32_t start[260];              // bucket starts (4-aligned)
+    uint32_t e[2048 + 768];           // elements in bucket order (below), buckets 4-aligned
+    uint32_t bysize[65];              // bucket-size histogram, then rank offsets
+    uint8_t  owner[256];              // thread -> bucket, largest buckets first
     uint32_t wsum[8];
 };
 
@@ -102,23 +106,6 @@ DEV uint32_t wave_incl_scan(uint32_t x)
         x += l >= d ? y : 0u;
     }
     return x;
-}
-
-// exclusive prefix over the workgroup's threads; total of all; two barriers
-DEV uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, uint32_t& total)
-{
-    const uint32_t inc = wave_incl_scan(x), w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 63) wsum[w] = inc;
-    __syncthreads();
-    uint32_t base = 0, all = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kScanThreads / 64; ++k) {
-        base += k < w ? wsum[k] : 0u;
-        all += wsum[k];
-    }
-    __syncthreads();
-    total = all;
-    return base + inc - x;
 }
 
 DEV void fallback(const E2Params& e, uint32_t* slot, uint32_t pkt)
@@ -140,18 +127,32 @@ DEV void pair(uint32_t u, uint32_t v, uint32_t akey, bool in, uint32_t& acc2, ui
 }
 
 // position j of bucket [bs, ...): its statistics over the predecessors
-// [bs, j) (final: their flags are set), its flags, and its record
+// [bs, j) (final: their flags are set), its flags, and its record.  Bucket
+// starts are 4-aligned, so each LDS read brings four predecessors.
 DEV void scan_position(ScanLds& s, uint32_t bs, uint32_t j, const uint8_t* x, uint2* rec)
 {
     const uint32_t w = s.e[j];
     const uint32_t pos = w & 2047, v = (w >> 11) & 255;
     const uint32_t akey = (w & (256u << 19)) ? (w >> 19) & 511 : 1024u;   // never matches at position 1
     uint32_t acc2 = 0, acc1 = 0;
-    for (uint32_t q = bs & ~3u; q < j; q += 4) {      // 4 predecessors per LDS read
+    uint32_t q = bs;
+    for (; q + 8 <= j; q += 8) {                      // two reads in flight
         const uint4 u = *reinterpret_cast<const uint4*>(&s.e[q]);
-        pair(u.x, v, akey, q >= bs, acc2, acc1);
-        pair(u.y, v, akey, q + 1 >= bs && q + 1 < j, acc2, acc1);
-        pair(u.z, v, akey, q + 2 >= bs && q + 2 < j, acc2, acc1);
+        const uint4 z = *reinterpret_cast<const uint4*>(&s.e[q + 4]);
+        pair(u.x, v, akey, true, acc2, acc1);
+        pair(u.y, v, akey, true, acc2, acc1);
+        pair(u.z, v, akey, true, acc2, acc1);
+        pair(u.w, v, akey, true, acc2, acc1);
+        pair(z.x, v, akey, true, acc2, acc1);
+        pair(z.y, v, akey, true, acc2, acc1);
+        pair(z.z, v, akey, true, acc2, acc1);
+        pair(z.w, v, akey, true, acc2, acc1);
+    }
+    for (; q < j; q += 4) {
+        const uint4 u = *reinterpret_cast<const uint4*>(&s.e[q]);
+        pair(u.x, v, akey, true, acc2, acc1);
+        pair(u.y, v, akey, q + 1 < j, acc2, acc1);
+        pair(u.z, v, akey, q + 2 < j, acc2, acc1);
         pair(u.w, v, akey, q + 3 < j, acc2, acc1);
     }
     const uint32_t t2 = acc2 & 255, same2 = (acc2 >> 8) & 255, less2 = (acc2 >> 16) & 255, d2 = acc2 >> 24;
@@ -178,6 +179,20 @@ DEV void scan_position(ScanLds& s, uint32_t bs, uint32_t j, const uint8_t* x, ui
     rec[pos] = make_uint2(r, r2 | v << 24);
 }
 
+// bucket b: position order (the atomics placed it nearly sorted), then its
+// positions one by one
+DEV void scan_bucket(ScanLds& s, uint32_t b, const uint8_t* x, uint2* rec)
+{
+    const uint32_t bs = s.start[b], be = s.cnt[b];
+    for (uint32_t j = bs + 1; j < be; ++j) {
+        const uint32_t w = s.e[j];
+        uint32_t q = j;
+        while (q > bs && (s.e[q - 1] & 2047) > (w & 2047)) { s.e[q] = s.e[q - 1]; --q; }
+        s.e[q] = w;
+    }
+    for (uint32_t j = bs; j < be; ++j) scan_position(s, bs, j, x, rec);
+}
+
 extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_scan(rc_batch_dev b, E2Params e)
 {
@@ -201,38 +216,54 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint32_t chunks = (mis + n + 15) >> 4;
         for (uint32_t c = t; c < chunks; c += kScanThreads)
             *reinterpret_cast<uint4*>(s.x + 16 * c) = gload16(a16 + 16 * c);
-        s.cnt[t] = 0;
+        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
+        if (t < 17) *reinterpret_cast<uint4*>(&s.bysize[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
         const uint8_t* x = s.x + mis;
         for (uint32_t i = 1 + t; i < n; i += kScanThreads) atomicAdd(&s.cnt[x[i - 1]], 1u);
         __syncthreads();
-        const uint32_t c = s.cnt[t];
-        if (__syncthreads_or(c > kE2Bucket)) {
+        // lane t owns buckets 4t .. 4t+3: sizes, 4-aligned starts
+        const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
+        const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
+        if (__syncthreads_or(mx > kE2Bucket)) {
             if (t == 0) fallback(e, slot, pkt);
             continue;
         }
-        uint32_t total;
-        const uint32_t ex = block_excl_scan(c, s.wsum, total);
-        s.start[t] = ex;
-        s.cnt[t] = ex;
-        if (t == 0) s.start[256] = total;
+        const uint32_t a0 = (c4.x + 3) & ~3u, a1 = (c4.y + 3) & ~3u, a2 = (c4.z + 3) & ~3u, a3 = (c4.w + 3) & ~3u;
+        const uint32_t mine = a0 + a1 + a2 + a3;
+        const uint32_t st = wave_incl_scan(mine) - mine;
+        const uint4 s4 = make_uint4(st, st + a0, st + a0 + a1, st + a0 + a1 + a2);
+        *reinterpret_cast<uint4*>(&s.start[4 * t]) = s4;
+        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
+        atomicAdd(&s.bysize[c4.x], 1u);
+        atomicAdd(&s.bysize[c4.y], 1u);
+        atomicAdd(&s.bysize[c4.z], 1u);
+        atomicAdd(&s.bysize[c4.w], 1u);
         __syncthreads();
         for (uint32_t i = 1 + t; i < n; i += kScanThreads) {
             const uint32_t k = atomicAdd(&s.cnt[x[i - 1]], 1u);
             s.e[k] = i | static_cast<uint32_t>(x[i]) << 11 | (i >= 2 ? (x[i - 2] | 256u) << 19 : 0u);
         }
-        __syncthreads();
-        // bucket t: position order (the atomics placed it nearly sorted), then
-        // its positions one by one
-        uint2* rec = reinterpret_cast<uint2*>(slot);
-        const uint32_t bs = s.start[t], be = s.start[t + 1];
-        for (uint32_t j = bs + 1; j < be; ++j) {
-            const uint32_t w = s.e[j];
-            uint32_t q = j;
-            while (q > bs && (s.e[q - 1] & 2047) > (w & 2047)) { s.e[q] = s.e[q - 1]; --q; }
-            s.e[q] = w;
+        // buckets ranked by size, largest first
+        if (t == 0) {
+            uint32_t acc = 0;
+            for (int k = kE2Bucket; k >= 0; --k) { const uint32_t m = s.bysize[k]; s.bysize[k] = acc; acc += m; }
         }
-        for (uint32_t j = bs; j < be; ++j) scan_position(s, bs, j, x, rec);
+        __syncthreads();
+        s.owner[atomicAdd(&s.bysize[c4.x], 1u)] = static_cast<uint8_t>(4 * t);
+        s.owner[atomicAdd(&s.bysize[c4.y], 1u)] = static_cast<uint8_t>(4 * t + 1);
+        s.owner[atomicAdd(&s.bysize[c4.z], 1u)] = static_cast<uint8_t>(4 * t + 2);
+        s.owner[atomicAdd(&s.bysize[c4.w], 1u)] = static_cast<uint8_t>(4 * t + 3);
+        __syncthreads();
+        // lane t takes the buckets ranked t, 127 - t, 128 + t, 255 - t: every
+        // lane gets about the same work (a wavefront lasts as long as its
+        // busiest lane)
+        uint2* rec = reinterpret_cast<uint2*>(slot);
+#pragma unroll 1
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t rank = (r & 1) ? 128 * ((r >> 1) + 1) - 1 - t : 128 * (r >> 1) + t;
+            scan_bucket(s, s.owner[rank], x, rec);
+        }
         if (t == 0) rec[0] = make_uint2(0u, static_cast<uint32_t>(x[0]) << 24);   // position 0: root only
         __syncthreads();                              // LDS reuse by the next packet
     }
@@ -240,19 +271,98 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 
 // ------------------------------------------------------------------ pass 2
 
-// compress.c:139-146 window store at the top of a step, issued on every path:
-// a pending window goes to its place, otherwise the same 16 B go to a dummy
-// slot of the lane (the first chunk of its record slot, already consumed).
-DEV void sink_flush_always(ByteSink& o, uintptr_t dummy)
+// ---- output: a 64-B ring per lane in LDS.  Byte A of the packet's output
+// (A an absolute address) lives at ring[A & 63], so every aligned 16-B chunk
+// of the output is an aligned 16-B slot of the ring.  A code appends its
+// settled bytes with three byte writes (bytes past the count are rewritten by
+// the next code before their chunk completes); a chunk that completes during
+// a step is read back then and stored at the end of the next step, by a
+// store issued on every path (to a dummy slot when no chunk is due).
+struct Ring {
+    uint8_t* r;
+    uintptr_t lo;               // output start
+    uint32_t n, cap;            // bytes produced, capacity (compress.c:114-119)
+    uint4 ch;                   // completed chunk awaiting its store
+    uintptr_t ca;               // its address, or the dummy slot
+};
+
+DEV void ring_put(Ring& o, uint32_t low, uint32_t k, bool put)
 {
-    const bool edge = o.pend && o.wpaddr < o.lo;
-    const uintptr_t a = (o.pend && !edge) ? o.wpaddr : dummy;
-    const v4u32 d = {o.wp.x, o.wp.y, o.wp.z, o.wp.w};
-    *GPTR(v4u32, a) = d;
-    if (rare_lane(edge)) {
-        if (edge) sink_bytes(o.wpaddr, o.wp, 0, 16, o.lo);
+    if (put) {
+        const uint32_t p = static_cast<uint32_t>(o.lo) + o.n;
+        o.r[p & 63] = static_cast<uint8_t>(low >> 24);
+        o.r[(p + 1) & 63] = static_cast<uint8_t>(low >> 16);
+        o.r[(p + 2) & 63] = static_cast<uint8_t>(low >> 8);
+        o.n += k;
     }
-    o.pend = false;
+}
+
+// the chunk store of the previous step (always issued; the dummy slot is the
+// lane's first record chunk, consumed before the loop)
+DEV void ring_store(Ring& o)
+{
+    const v4u32 d = {o.ch.x, o.ch.y, o.ch.z, o.ch.w};
+    *GPTR(v4u32, o.ca) = d;
+}
+
+// after a step's codes: a chunk completed since n0 is read back for storing
+DEV void ring_chunk(Ring& o, uint32_t n0, uintptr_t dummy)
+{
+    const uintptr_t e0 = o.lo + n0, e1 = o.lo + o.n;
+    const bool done = (e0 >> 4) != (e1 >> 4);         // codes add <= 12 bytes: at most one chunk
+    const uintptr_t c = (e1 & ~static_cast<uintptr_t>(15)) - 16;
+    o.ch = *reinterpret_cast<const uint4*>(o.r + (c & 63));
+    const bool edge = done && c < o.lo;               // the first chunk starts before the output
+    o.ca = (done && !edge) ? c : dummy;
+    if (rare_lane(edge)) {
+        if (edge) sink_bytes(c, o.ch, 0, 16, o.lo);
+    }
+}
+
+// the last, partial chunk
+DEV void ring_finish(Ring& o, bool en)
+{
+    if (rare_lane(en)) {
+        if (en) {
+            const uintptr_t e1 = o.lo + o.n, c = e1 & ~static_cast<uintptr_t>(15);
+            if (e1 > c) {
+                const uint4 w = *reinterpret_cast<const uint4*>(o.r + (c & 63));
+                sink_bytes(c, w, 0, static_cast<uint32_t>(e1 - c), o.lo);
+            }
+        }
+    }
+}
+
+// compress.c:121-137 where `en`; clears `ok` when the output is full
+DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total, Ring& o,
+              bool en, bool& ok)
+{
+    en = en && ok;
+    if (!any_lane(en)) return;
+    const uint32_t r = udiv16(range, en ? total : 1u);
+    low = en ? low + under * r : low;
+    range = en ? r * count : range;
+    const uint32_t k = en ? settled_bytes(low, range) : 0u;
+    const bool full = o.n + k > o.cap;
+    ok = ok && !full;
+    const bool put = en && !full;
+    ring_put(o, low, k, put);
+    low = put ? low << (8 * k) : low;
+    range = put ? range << (8 * k) : range;
+    bool more = put && range < kBot;
+    while (rare_lane(more)) {
+        const bool carry = (low ^ (low + range)) >= kTop;
+        const bool stop = carry && range >= kBot;
+        more = more && !stop;
+        if (!any_lane(more)) break;
+        range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
+        const bool f = more && o.n >= o.cap;
+        ok = ok && !f;
+        more = more && !f;
+        ring_put(o, low, 1, more);
+        range = more ? range << 8 : range;
+        low = more ? low << 8 : low;
+    }
 }
 
 // interval of a sub-context code from (t, dist[, same, less]): compress.c:301-308
@@ -271,36 +381,42 @@ struct CodeState {
 };
 
 // one position: its sub-context codes, then the root (compress.c:286-337)
-DEV void code_step(CodeState& k, ByteSink& o, uint8_t* root, uint32_t w0, uint32_t w1, bool en,
-                   uintptr_t dummy)
+DEV void code_step(CodeState& k, Ring& o, uint8_t* root, uint32_t w0, uint32_t w1, bool en, uintptr_t dummy)
 {
-    sink_flush_always(o, dummy);
     en = en && k.ok;
+    const uint32_t n0 = o.n;
     const uint32_t typ = w0 & 7, ext = w0 >> 16, v = w1 >> 24;
     // first sub-context code: order 2 (types 3-6) or order 1 (types 1, 2)
     uint32_t un, ct, tt;
     sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
-    enc_code(k.low, k.range, un, ct, tt, o, en && typ != 0, k.ok);
+    code(k.low, k.range, un, ct, tt, o, en && typ != 0, k.ok);
     // order 1 after an order-2 escape (types 4, 5)
     const uint32_t fb = typ == 5 ? w1 : ext;
     sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un, ct, tt);
-    enc_code(k.low, k.range, un, ct, tt, o, en && (typ == 4 || typ == 5), k.ok);
+    code(k.low, k.range, un, ct, tt, o, en && (typ == 4 || typ == 5), k.ok);
     // root, compress.c:318-329
     const bool en0 = en && (typ <= 1 || typ == 3 || typ == 4);
     uint32_t under0, cnt0;
     root_lookup(root, v, under0, cnt0);
     if (en0) root_add(root, v, cnt0);
-    enc_code(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, o, en0, k.ok);
+    code(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, o, en0, k.ok);
     k.rtot = en0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
     const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
     if (any_lane(rs0)) { if (rs0) k.rtot = root_rescale(root); }
+    ring_store(o);                                    // the chunk read back a step ago
+    ring_chunk(o, n0, dummy);
 }
+
+constexpr uint32_t kRing = 64;
+constexpr uint32_t kCodeLds = kRootStride + kRing;    // per lane
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void rc_enc2_code(rc_batch_dev b, E2Params e)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t idx = e.lo + blockIdx.x * 256 + threadIdx.x;
+    const uint32_t l = threadIdx.x & 63;
+    if (l >= e.act) return;
+    const uint32_t idx = e.lo + blockIdx.x * 4 * e.act + (threadIdx.x >> 6) * e.act + l;
     if (idx >= e.hi) return;
     const uintptr_t base = reinterpret_cast<uintptr_t>(e.stream) + static_cast<size_t>(idx - e.lo) * e.slot_bytes;
     uint4 c0 = gload16(base);
@@ -308,9 +424,14 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     uint4 c1 = gload16(base + 16), c2 = gload16(base + 32);
     const uint32_t pkt = packet_of(e, idx);
     const uint32_t len = b.in_len[pkt];
-    uint8_t* root = smem + threadIdx.x * kRootStride;
-    ByteSink o;
-    sink_init(o, b.out + b.out_off[pkt], b.out_cap[pkt]);
+    uint8_t* root = smem + threadIdx.x * kCodeLds;
+    Ring o;
+    o.r = root + kRootStride;
+    o.lo = reinterpret_cast<uintptr_t>(b.out + b.out_off[pkt]);
+    o.n = 0;
+    o.cap = b.out_cap[pkt];
+    o.ch = make_uint4(0u, 0u, 0u, 0u);
+    o.ca = base;
     root_clear(root);
     CodeState k;
     k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
@@ -332,6 +453,8 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
         code_step(k, o, root, c2.z, c2.w, i + 5 < len, base);
         c2 = gload16(a + 32);
     }
+    ring_store(o);
+    ring_chunk(o, o.n, base);                         // (nothing new: the next store goes to the dummy)
     // flush, compress.c:139-146
     bool ok = k.ok;
     uint32_t low = k.low;
@@ -339,10 +462,13 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
         const bool more = ok && low != 0;
         const bool full = more && o.n >= o.cap;
         ok = ok && !full;
-        sink_put(o, low >> 24, 1, more && !full);
+        const uint32_t n0 = o.n;
+        ring_put(o, low, 1, more && !full);
         low = (more && !full) ? low << 8 : low;
+        ring_chunk(o, n0, base);
+        ring_store(o);
     }
-    sink_finish(o, ok);
+    ring_finish(o, ok);
     b.out_len[pkt] = ok ? o.n : 0u;
 }
 
@@ -370,7 +496,9 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     e.bins = ws->bins;
     e.list = ws->enc2_list;
     e.count = ws->counters + 3;
-    const uint32_t scan_blocks_max = ws->cus * 8;
+    const uint32_t scan_blocks_max = ws->cus * 16;
+    static const char* lanes = getenv("ENET_RC_ENC2_LANES");      // experiment: 32 packets per wavefront
+    e.act = (lanes && atoi(lanes) == 32) ? 32u : 64u;
     for (uint64_t lo = 0; lo < b->n; lo += per) {
         const uint64_t hi = lo + per < b->n ? lo + per : b->n;
         e.lo = static_cast<uint32_t>(lo);
@@ -378,7 +506,8 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         const uint32_t cnt = static_cast<uint32_t>(hi - lo);
         hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
                            0, st, *b, e);
-        hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 255) / 256), dim3(256), 256 * kRootStride, st, *b, e);
+        hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 4 * e.act - 1) / (4 * e.act)), dim3(256), 256 * kCodeLds, st,
+                           *b, e);
     }
     return static_cast<int>(hipGetLastError());
 }
