@@ -57,6 +57,20 @@
 #include "rc_udiv.h"
 #include "rc_lane_common.h"
 
+// Diagnostic build only (-DE2_PROF, tools/enc2_prof.py): per-phase cycles of
+// the scan pass, summed over wavefronts.  The product build has no stamps.
+#ifdef E2_PROF
+__device__ unsigned long long g_e2prof[16];
+#define E2P_DECL unsigned long long e2p_t = __builtin_amdgcn_s_memtime(), e2p_acc[8] = {0};
+#define E2P(k) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+                 e2p_acc[k] += t_ - e2p_t; e2p_t = t_; __builtin_amdgcn_sched_barrier(0); }
+#define E2P_FLUSH { if (threadIdx.x == 0) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_e2prof[k_], e2p_acc[k_]); }
+#else
+#define E2P_DECL
+#define E2P(k)
+#define E2P_FLUSH
+#endif
+
 namespace {
 
 constexpr uint32_t kE2MaxLen = 1919;          // compress.c:148-157: no reset below 1920 B
@@ -86,16 +100,20 @@ DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 struct ScanLds {
     uint8_t  x[2048];                 // packet bytes at x[mis + i]
     uint32_t cnt[256];                // bucket sizes, then fill pointers
-    uint32_t start[260];              // bucket starts (4-aligned)
-    uint32_t e[2048 + 768];           // elements in bucket order (below), buckets 4-aligned
-    uint32_t bysize[65];              // bucket-size histogram, then rank offsets
-    uint8_t  owner[256];              // thread -> bucket, largest buckets first
-    uint32_t wsum[8];
+    uint32_t start[256];              // bucket starts (4-aligned)
+    union {
+        uint32_t seen[2048];          // bigrams (x[i-1], x[i]) seen, 64 Ki bits
+        uint32_t e[2048 + 768];       // elements in bucket order (below), buckets 4-aligned
+    };
+    uint32_t rep[32];                 // 1 Ki-bit filter of the bigrams seen twice (hashed)
+    uint8_t  excb[256];               // bucket holds an exceptional position
+    uint8_t  xlist[256];              // those buckets
 };
 
 // element word: pos (0-10) | v (11-18) | a | 256 (19-27, 0 for position 1) |
-//               found2 (28) | visits order 1 (29) | found1 (30)
-constexpr uint32_t kF2 = 1u << 28, kV1 = 1u << 29, kF1 = 1u << 30;
+//               found2 (28) | does not visit order 1 (29) | found1 (30) |
+//               exceptional (31).  A plain position has flags 0.
+constexpr uint32_t kF2 = 1u << 28, kNV1 = 1u << 29, kF1 = 1u << 30, kExc = 1u << 31;
 
 DEV uint32_t wave_incl_scan(uint32_t x)
 {
@@ -114,6 +132,8 @@ DEV void fallback(const E2Params& e, uint32_t* slot, uint32_t pkt)
     e.list[atomicAdd(e.count, 1u)] = pkt;
 }
 
+DEV uint32_t rep_hash(uint32_t bigram) { return (bigram * 0x9E3779B1u) >> 22; }   // 10 bits
+
 // one predecessor u of an element (v, akey): SWAR accumulators
 // t | same << 8 | less << 16 | dist << 24 of order 2 and order 1
 DEV void pair(uint32_t u, uint32_t v, uint32_t akey, bool in, uint32_t& acc2, uint32_t& acc1)
@@ -121,47 +141,16 @@ DEV void pair(uint32_t u, uint32_t v, uint32_t akey, bool in, uint32_t& acc2, ui
     const uint32_t uv = (u >> 11) & 255;
     const uint32_t base = 1u | (uv == v ? 0x100u : 0u) | (uv < v ? 0x10000u : 0u);
     const bool m2 = in && ((u >> 19) & 511) == akey;
-    const bool m1 = in && (u & kV1) != 0;
+    const bool m1 = in && (u & kNV1) == 0;
     acc2 += m2 ? (base | ((u & kF2) ? 0u : 0x1000000u)) : 0u;
     acc1 += m1 ? (base | ((u & kF1) ? 0u : 0x1000000u)) : 0u;
 }
 
-// position j of bucket [bs, ...): its statistics over the predecessors
-// [bs, j) (final: their flags are set), its flags, and its record.  Bucket
-// starts are 4-aligned, so each LDS read brings four predecessors.
-DEV void scan_position(ScanLds& s, uint32_t bs, uint32_t j, const uint8_t* x, uint2* rec)
+// record of position pos from its statistics (see the format above)
+DEV uint2 make_record(uint32_t acc2, uint32_t acc1, bool f2, bool f1, uint32_t v)
 {
-    const uint32_t w = s.e[j];
-    const uint32_t pos = w & 2047, v = (w >> 11) & 255;
-    const uint32_t akey = (w & (256u << 19)) ? (w >> 19) & 511 : 1024u;   // never matches at position 1
-    uint32_t acc2 = 0, acc1 = 0;
-    uint32_t q = bs;
-    for (; q + 8 <= j; q += 8) {                      // two reads in flight
-        const uint4 u = *reinterpret_cast<const uint4*>(&s.e[q]);
-        const uint4 z = *reinterpret_cast<const uint4*>(&s.e[q + 4]);
-        pair(u.x, v, akey, true, acc2, acc1);
-        pair(u.y, v, akey, true, acc2, acc1);
-        pair(u.z, v, akey, true, acc2, acc1);
-        pair(u.w, v, akey, true, acc2, acc1);
-        pair(z.x, v, akey, true, acc2, acc1);
-        pair(z.y, v, akey, true, acc2, acc1);
-        pair(z.z, v, akey, true, acc2, acc1);
-        pair(z.w, v, akey, true, acc2, acc1);
-    }
-    for (; q < j; q += 4) {
-        const uint4 u = *reinterpret_cast<const uint4*>(&s.e[q]);
-        pair(u.x, v, akey, true, acc2, acc1);
-        pair(u.y, v, akey, q + 1 < j, acc2, acc1);
-        pair(u.z, v, akey, q + 2 < j, acc2, acc1);
-        pair(u.w, v, akey, q + 3 < j, acc2, acc1);
-    }
     const uint32_t t2 = acc2 & 255, same2 = (acc2 >> 8) & 255, less2 = (acc2 >> 16) & 255, d2 = acc2 >> 24;
-    const bool f2 = same2 != 0;
-    const bool v1 = !f2;                              // compress.c:315: order 1 only after an escape
-    if (!v1) acc1 = 0;
     const uint32_t t1 = acc1 & 255, same1 = (acc1 >> 8) & 255, less1 = (acc1 >> 16) & 255, d1 = acc1 >> 24;
-    const bool f1 = v1 && same1 != 0;
-    s.e[j] = w | (f2 ? kF2 : 0u) | (v1 ? kV1 : 0u) | (f1 ? kF1 : 0u);
     uint32_t r, r2 = 0;
     if (f2) {
         r = 6u | t2 << 3 | d2 << 9 | (same2 | less2 << 6) << 16;
@@ -176,21 +165,77 @@ DEV void scan_position(ScanLds& s, uint32_t bs, uint32_t j, const uint8_t* x, ui
     } else {
         r = 1u | t1 << 3 | d1 << 9;
     }
-    rec[pos] = make_uint2(r, r2 | v << 24);
+    return make_uint2(r, r2 | v << 24);
 }
 
-// bucket b: position order (the atomics placed it nearly sorted), then its
-// positions one by one
-DEV void scan_bucket(ScanLds& s, uint32_t b, const uint8_t* x, uint2* rec)
+// exceptional position j of bucket [bs, ...): statistics over all its
+// predecessors [bs, j) (their flags are final), its flags, its record
+__device__ __attribute__((noinline)) uint32_t scan_exceptional(ScanLds& s, uint32_t bs, uint32_t j, uint32_t w,
+                                                               uint2* rec)
 {
-    const uint32_t bs = s.start[b], be = s.cnt[b];
+    const uint32_t pos = w & 2047, v = (w >> 11) & 255;
+    const uint32_t akey = (w & (256u << 19)) ? (w >> 19) & 511 : 1024u;   // never matches at position 1
+    uint32_t acc2 = 0, acc1 = 0;
+    for (uint32_t q = bs; q < j; q += 4) {            // bucket starts are 4-aligned
+        const uint4 u = *reinterpret_cast<const uint4*>(&s.e[q]);
+        pair(u.x, v, akey, true, acc2, acc1);
+        pair(u.y, v, akey, q + 1 < j, acc2, acc1);
+        pair(u.z, v, akey, q + 2 < j, acc2, acc1);
+        pair(u.w, v, akey, q + 3 < j, acc2, acc1);
+    }
+    const bool f2 = ((acc2 >> 8) & 255) != 0;
+    if (f2) acc1 = 0;                                 // compress.c:315: order 1 only after an escape
+    const bool f1 = !f2 && ((acc1 >> 8) & 255) != 0;
+    rec[pos] = make_record(acc2, acc1, f2, f1, v);
+    const uint32_t fl = (f2 ? kF2 | kNV1 : 0u) | (f1 ? kF1 : 0u);
+    s.e[j] = w | fl;
+    return fl;
+}
+
+// insertion sort of a bucket by position (diagnostic safety net: the scatter
+// keeps position order when LDS atomics apply in lane order, as on gfx950)
+DEV void sort_bucket(ScanLds& s, uint32_t bs, uint32_t be)
+{
     for (uint32_t j = bs + 1; j < be; ++j) {
         const uint32_t w = s.e[j];
         uint32_t q = j;
         while (q > bs && (s.e[q - 1] & 2047) > (w & 2047)) { s.e[q] = s.e[q - 1]; --q; }
         s.e[q] = w;
     }
-    for (uint32_t j = bs; j < be; ++j) scan_position(s, bs, j, x, rec);
+}
+
+// Bucket b in position order.  A plain position (neither of its bigrams
+// (x[i-2], x[i-1]) and (x[i-1], x[i]) occurs twice in the packet) has no
+// order-2 context seen before (t2 = 0) and a new order-1 symbol, so its
+// record needs only how many predecessors visited order 1 (t1) and how many
+// of those were order-1 hits (dist1 = t1 - hits): counters kept along the
+// walk.  Exceptional positions get the full count over their predecessors.
+// A bucket holding exceptional positions, in position order: each
+// exceptional position needs the flags of the earlier ones; a plain one
+// codes t1 = j - (earlier order-2 hits), dist1 = t1 - (earlier order-1 hits),
+// hits that occur only at exceptional positions.  Returns false if the
+// bucket is not in position order (nothing is final then).
+DEV bool walk_full(ScanLds& s, uint32_t bs, uint32_t k, uint2* rec)
+{
+    uint32_t nf2 = 0, nh1 = 0, prev = 0;
+    bool sorted = true;
+    uint4 u = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll 1
+    for (uint32_t j = 0; j < k; ++j) {
+        if ((j & 3) == 0) u = *reinterpret_cast<const uint4*>(&s.e[bs + j]);
+        const uint32_t w = pick4(j & 3, u);
+        sorted = sorted && (w & 2047) > prev;
+        prev = w & 2047;
+        if (w & kExc) {
+            const uint32_t fl = scan_exceptional(s, bs, bs + j, w, rec);
+            nf2 += (fl & kF2) ? 1u : 0u;
+            nh1 += (fl & kF1) ? 1u : 0u;
+        } else {
+            const uint32_t t1 = j - nf2, d1 = t1 - nh1;
+            rec[w & 2047] = make_uint2(t1 ? (1u | t1 << 3 | d1 << 9) : 0u, ((w >> 11) & 255) << 24);
+        }
+    }
+    return sorted;
 }
 
 extern "C" __global__ __launch_bounds__(kScanThreads)
@@ -198,6 +243,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 {
     __shared__ __attribute__((aligned(16))) ScanLds s;
     const uint32_t t = threadIdx.x;
+    E2P_DECL
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const uint32_t pkt = packet_of(e, idx);
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
@@ -216,12 +262,39 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint32_t chunks = (mis + n + 15) >> 4;
         for (uint32_t c = t; c < chunks; c += kScanThreads)
             *reinterpret_cast<uint4*>(s.x + 16 * c) = gload16(a16 + 16 * c);
-        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
-        if (t < 17) *reinterpret_cast<uint4*>(&s.bysize[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = z;
+        if (t < 8) *reinterpret_cast<uint4*>(&s.rep[4 * t]) = z;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(&s.seen[4 * (t + 64 * k)]) = z;
         __syncthreads();
+        E2P(0)
         const uint8_t* x = s.x + mis;
-        for (uint32_t i = 1 + t; i < n; i += kScanThreads) atomicAdd(&s.cnt[x[i - 1]], 1u);
+        // bucket sizes, and the bigrams that occur twice
+        for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
+            uint32_t key[4], old[4];
+#pragma unroll
+            for (uint32_t m = 0; m < 4; ++m) {
+                const uint32_t ii = i + m * kScanThreads;
+                key[m] = ii < n ? static_cast<uint32_t>(x[ii - 1]) << 8 | x[ii] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (uint32_t m = 0; m < 4; ++m) {
+                old[m] = 0;
+                if (key[m] != 0xFFFFFFFFu) {
+                    atomicAdd(&s.cnt[key[m] >> 8], 1u);
+                    old[m] = atomicOr(&s.seen[key[m] >> 5], 1u << (key[m] & 31));
+                }
+            }
+#pragma unroll
+            for (uint32_t m = 0; m < 4; ++m)
+                if (key[m] != 0xFFFFFFFFu && (old[m] & (1u << (key[m] & 31)))) {
+                    const uint32_t h = rep_hash(key[m]);
+                    atomicOr(&s.rep[h >> 5], 1u << (h & 31));
+                }
+        }
         __syncthreads();
+        E2P(1)
         // lane t owns buckets 4t .. 4t+3: sizes, 4-aligned starts
         const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
         const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
@@ -235,38 +308,94 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint4 s4 = make_uint4(st, st + a0, st + a0 + a1, st + a0 + a1 + a2);
         *reinterpret_cast<uint4*>(&s.start[4 * t]) = s4;
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
-        atomicAdd(&s.bysize[c4.x], 1u);
-        atomicAdd(&s.bysize[c4.y], 1u);
-        atomicAdd(&s.bysize[c4.z], 1u);
-        atomicAdd(&s.bysize[c4.w], 1u);
         __syncthreads();
-        for (uint32_t i = 1 + t; i < n; i += kScanThreads) {
-            const uint32_t k = atomicAdd(&s.cnt[x[i - 1]], 1u);
-            s.e[k] = i | static_cast<uint32_t>(x[i]) << 11 | (i >= 2 ? (x[i - 2] | 256u) << 19 : 0u);
+        E2P(2)
+        if (t < 16) *reinterpret_cast<uint4*>(&s.excb[16 * t]) = z;
+        __syncthreads();
+        for (uint32_t i = 1 + t; i < n; i += 2 * kScanThreads) {
+            uint32_t w[2], k[2], bb[2];
+#pragma unroll
+            for (uint32_t m = 0; m < 2; ++m) {
+                const uint32_t ii = i + m * kScanThreads;
+                bb[m] = 0xFFFFFFFFu;
+                if (ii < n) {
+                    const uint32_t p = x[ii - 1], v = x[ii], a = ii >= 2 ? x[ii - 2] : 0u;
+                    const uint32_t h1 = rep_hash(p << 8 | v), h2 = rep_hash(a << 8 | p);
+                    const bool exc = ((s.rep[h1 >> 5] >> (h1 & 31)) & 1) ||
+                                     (ii >= 2 && ((s.rep[h2 >> 5] >> (h2 & 31)) & 1));
+                    w[m] = ii | v << 11 | (ii >= 2 ? (a | 256u) << 19 : 0u) | (exc ? kExc : 0u);
+                    bb[m] = p;
+                    if (exc) s.excb[p] = 1;
+                }
+            }
+#pragma unroll
+            for (uint32_t m = 0; m < 2; ++m) k[m] = bb[m] != 0xFFFFFFFFu ? atomicAdd(&s.cnt[bb[m]], 1u) : 0u;
+#pragma unroll
+            for (uint32_t m = 0; m < 2; ++m)
+                if (bb[m] != 0xFFFFFFFFu) s.e[k[m]] = w[m];
         }
-        // buckets ranked by size, largest first
-        if (t == 0) {
-            uint32_t acc = 0;
-            for (int k = kE2Bucket; k >= 0; --k) { const uint32_t m = s.bysize[k]; s.bysize[k] = acc; acc += m; }
-        }
+        const uint32_t x0 = x[0];
         __syncthreads();
-        s.owner[atomicAdd(&s.bysize[c4.x], 1u)] = static_cast<uint8_t>(4 * t);
-        s.owner[atomicAdd(&s.bysize[c4.y], 1u)] = static_cast<uint8_t>(4 * t + 1);
-        s.owner[atomicAdd(&s.bysize[c4.z], 1u)] = static_cast<uint8_t>(4 * t + 2);
-        s.owner[atomicAdd(&s.bysize[c4.w], 1u)] = static_cast<uint8_t>(4 * t + 3);
-        __syncthreads();
-        // lane t takes the buckets ranked t, 127 - t, 128 + t, 255 - t: every
-        // lane gets about the same work (a wavefront lasts as long as its
-        // busiest lane)
+        E2P(3)
         uint2* rec = reinterpret_cast<uint2*>(slot);
+        // buckets with exceptional positions: compacted over the lanes, one
+        // per lane, each walked in full
+        {
+            const uint32_t f = *reinterpret_cast<const uint32_t*>(&s.excb[4 * t]);
+            const uint32_t m0 = f & 1, m1 = (f >> 8) & 1, m2 = (f >> 16) & 1, m3 = (f >> 24) & 1;
+            const uint32_t cntx = m0 + m1 + m2 + m3;
+            const uint32_t incl = wave_incl_scan(cntx);
+            uint32_t o = incl - cntx;
+            if (m0) s.xlist[o++] = static_cast<uint8_t>(4 * t);
+            if (m1) s.xlist[o++] = static_cast<uint8_t>(4 * t + 1);
+            if (m2) s.xlist[o++] = static_cast<uint8_t>(4 * t + 2);
+            if (m3) s.xlist[o++] = static_cast<uint8_t>(4 * t + 3);
+            const uint32_t nx = __shfl(incl, 63, 64);
+            __syncthreads();
+#pragma unroll 1
+            for (uint32_t q = t; q < nx; q += kScanThreads) {
+                const uint32_t bk = s.xlist[q];
+                const uint32_t bs = s.start[bk], kk = s.cnt[bk] - bs;
+                if (rare_lane(!walk_full(s, bs, kk, rec))) {   // (not seen on gfx950) sort, walk again
+                    for (uint32_t j = 0; j < kk; ++j) s.e[bs + j] &= ~(kF2 | kNV1 | kF1);
+                    sort_bucket(s, bs, bs + kk);
+                    walk_full(s, bs, kk, rec);
+                }
+            }
+        }
+        E2P(4)
+        // every other bucket: its positions in order, t1 = dist1 = j
+        __syncthreads();
 #pragma unroll 1
         for (uint32_t r = 0; r < 4; ++r) {
-            const uint32_t rank = (r & 1) ? 128 * ((r >> 1) + 1) - 1 - t : 128 * (r >> 1) + t;
-            scan_bucket(s, s.owner[rank], x, rec);
+            const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
+            if (s.excb[4 * t + r]) continue;
+            uint32_t prev = 0;
+            bool sorted = true;
+            uint4 u = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll 1
+            for (uint32_t j = 0; j < kk; ++j) {
+                if ((j & 3) == 0) u = *reinterpret_cast<const uint4*>(&s.e[bs + j]);
+                const uint32_t w = pick4(j & 3, u);
+                sorted = sorted && (w & 2047) > prev;
+                prev = w & 2047;
+                rec[w & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w >> 11) & 255) << 24);
+            }
+            if (rare_lane(!sorted)) {                 // (not seen on gfx950) sort, write again
+                if (!sorted) {
+                    sort_bucket(s, bs, bs + kk);
+                    for (uint32_t j = 0; j < kk; ++j) {
+                        const uint32_t w = s.e[bs + j];
+                        rec[w & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w >> 11) & 255) << 24);
+                    }
+                }
+            }
         }
-        if (t == 0) rec[0] = make_uint2(0u, static_cast<uint32_t>(x[0]) << 24);   // position 0: root only
+        if (t == 0) rec[0] = make_uint2(0u, x0 << 24);  // position 0: root only
         __syncthreads();                              // LDS reuse by the next packet
+        E2P(5)
     }
+    E2P_FLUSH
 }
 
 // ------------------------------------------------------------------ pass 2
@@ -473,6 +602,19 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
 }
 
 }  // namespace
+
+#ifdef E2_PROF
+extern "C" int rc_enc2_prof_read(unsigned long long* out, int reset)
+{
+    hipError_t err = hipDeviceSynchronize();
+    if (err == hipSuccess) err = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_e2prof), sizeof(unsigned long long) * 16);
+    if (err == hipSuccess && reset) {
+        static const unsigned long long zero[16] = {0};
+        err = hipMemcpyToSymbol(HIP_SYMBOL(g_e2prof), zero, sizeof zero);
+    }
+    return static_cast<int>(err);
+}
+#endif
 
 // bytes of one packet's record slot for packets of up to max_len bytes
 extern "C" uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len)

@@ -1,0 +1,34 @@
+"""Per-phase cycles of the two-pass encoder's scan pass (diagnostic build,
+make -C enet_amd/csrc e2prof).  Runs one C2 compress batch and prints the
+shader cycles each phase took, summed over wavefronts, per packet."""
+import ctypes as C
+import os
+import sys
+
+os.environ["ENET_RC_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "enet_amd", "lib",
+                                         "libenet_rc_amd_e2prof.so")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch  # noqa: E402
+from enet_amd import RangeCoder, compress_batch, synth, get_lib  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+lib = get_lib()
+lib.rc_enc2_prof_read.restype = C.c_int
+lib.rc_enc2_prof_read.argtypes = [C.c_void_p, C.c_int]
+d, o, l = synth.random_batch(n, 1200)
+din = torch.from_numpy(d).cuda()
+doff = torch.from_numpy(o.astype("int64")).cuda()
+dlen = torch.from_numpy(l.astype("int32")).cuda()
+buf = (C.c_ulonglong * 16)()
+with RangeCoder() as rc:
+    compress_batch(rc, din, doff, dlen, max_len=1200)
+    torch.cuda.synchronize()
+    lib.rc_enc2_prof_read(buf, 1)
+    compress_batch(rc, din, doff, dlen, max_len=1200)
+    torch.cuda.synchronize()
+    lib.rc_enc2_prof_read(buf, 1)
+names = ["load+zero", "hist+bigrams", "sizes", "scatter", "exceptional", "plain+end", "-", "-"]
+tot = sum(buf[k] for k in range(8))
+for k, nm in enumerate(names):
+    print(f"{nm:14s} {buf[k] / n:10.0f} cycles/packet  {100.0 * buf[k] / max(tot, 1):5.1f} %")
+print(f"{'total':14s} {tot / n:10.0f} cycles/packet")
