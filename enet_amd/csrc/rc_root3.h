@@ -1,0 +1,137 @@
+// rc_root3.h -- the order-0 (root) context of one lane: counts in LDS, the
+// cumulative group boundaries in registers (compress.c:159-199, :318-329,
+// :570-596, :90-112).  Shared by the lane kernels (rc_lane3.hip) and the
+// bucket-history decoder (rc_dec4.hip).  Include after rc_lane_common.h.
+#pragma once
+
+namespace {
+
+// ------------------------------------------------------------ order 0
+// Per lane: counts[256] (u8) in LDS; the 16 group boundaries in registers,
+// D[t] = 16 (t + 1) + the counts of symbols < 16 (t + 1) -- the cumulative
+// frequency including every symbol's minimum 1 (compress.c:159-199) -- as
+// packed u16 pairs d[i] = D[2i] | D[2i + 1] << 16.  The root total is
+// 1 + D[15].  The encoder also keeps a copy of D in LDS after the counts, so
+// that a lookup is three independent LDS reads (the symbol's 16-B group, D of
+// the groups below, the prefix mask of its position in the group from a
+// block-wide table) and no register selects; an update writes one byte (and
+// the encoder's copy of D).  The decoder finds the group with packed compares
+// on the registers (no LDS reads).
+constexpr uint32_t kRootStride3 = 304;   // counts[256], D[16] (u16), pad
+constexpr uint32_t kRootD = 256;
+
+struct Root { uint32_t d[8]; };
+
+// the block-wide table of prefix masks: entry j has bytes 0..j-1 set
+DEV void root3_mask_init(uint8_t* tab, uint32_t j)
+{
+    uint32_t w[4];
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+        const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
+        w[d] = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+    }
+    reinterpret_cast<uint4*>(tab)[j] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <bool COPY>
+DEV void root3_store_d(uint8_t* r, const Root& R)
+{
+    if (COPY) {
+        uint4* p = reinterpret_cast<uint4*>(r + kRootD);
+        p[0] = make_uint4(R.d[0], R.d[1], R.d[2], R.d[3]);
+        p[1] = make_uint4(R.d[4], R.d[5], R.d[6], R.d[7]);
+    }
+}
+
+template <bool COPY>
+DEV void root3_clear(uint8_t* r, Root& R)
+{
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) reinterpret_cast<uint4*>(r)[i] = z;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) R.d[i] = (32 * i + 16) | ((32 * i + 32) << 16);
+    root3_store_d<COPY>(r, R);
+}
+
+// under = cumulative frequency below v, cnt = count[v] (compress.c:159-199, minimum 1)
+DEV void root3_lookup(const uint8_t* r, const uint8_t* mtab, uint32_t v, uint32_t& under, uint32_t& cnt)
+{
+    const uint32_t g = v >> 4, j = v & 15;
+    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    const uint4 m = *reinterpret_cast<const uint4*>(mtab + 16 * j);
+    const uint32_t dprev = reinterpret_cast<const uint16_t*>(r + kRootD)[static_cast<int>(g) - 1];   // (g = 0: unused)
+    cnt = r[v];
+    const uint32_t within = sad(q.w & m.w, sad(q.z & m.z, sad(q.y & m.y, sad(q.x & m.x, 0u))));
+    under = (g ? dprev : 0u) + j + within;
+}
+
+template <bool COPY>
+DEV void root3_add(uint8_t* r, Root& R, uint32_t v, uint32_t cnt)
+{
+    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
+    cum_add(R.d, v >> 4, kRootDelta);
+    root3_store_d<COPY>(r, R);
+}
+
+// Decoder: the symbol whose interval holds code (code < root total - 1):
+// g = #{t : D[t] <= code} by packed saturating compares, then halving on byte
+// sums inside group g.  Returns v; under = its cumulative frequency, cnt = count[v].
+DEV uint32_t root3_search(const uint8_t* r, const Root& R, uint32_t code, uint32_t& under, uint32_t& cnt)
+{
+    const uint32_t x1 = (code + 1) * 0x00010001u;
+    uint32_t acc = 0, pm = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t b = pk_min(pk_subsat(x1, R.d[i]), 0x00010001u);   // 1 where D <= code
+        acc = pk_add(acc, b);
+        pm = pk_max(pm, pk_mul(R.d[i], b));
+    }
+    const uint32_t g = (acc & 0xFFFF) + (acc >> 16);
+    const uint32_t prev = max(pm & 0xFFFF, pm >> 16);                 // D[g - 1], 0 for g = 0
+    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    uint32_t base = prev, j = 0;
+    uint32_t s = sad(q.x, sad(q.y, 8u));
+    bool hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 8u : 0u;
+    const uint32_t d0 = hi ? q.z : q.x, d1 = hi ? q.w : q.y;
+    s = sad(d0, 4u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 4u : 0u;
+    uint32_t w = hi ? d1 : d0;
+    s = sad(w & 0xFFFFu, 2u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 2u : 0u;
+    w = hi ? (w >> 16) : w;
+    s = (w & 0xFFu) + 1u;
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 1u : 0u;
+    w = hi ? (w >> 8) : w;
+    under = base;
+    cnt = w & 0xFFu;
+    return 16 * g + j;
+}
+
+// compress.c:90-112 for the root: halve the counts, rebuild D; returns the new total
+template <bool COPY>
+DEV uint32_t root3_rescale(uint8_t* r, Root& R)
+{
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < 16; ++g) {
+        uint4 q = reinterpret_cast<uint4*>(r)[g];
+        q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
+        q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
+        q.z -= (q.z >> 1) & 0x7F7F7F7Fu;
+        q.w -= (q.w >> 1) & 0x7F7F7F7Fu;
+        reinterpret_cast<uint4*>(r)[g] = q;
+        sum = sad(q.w, sad(q.z, sad(q.y, sad(q.x, sum))));
+        const uint32_t dg = sum + 16 * (g + 1);
+        if (g & 1) R.d[g >> 1] |= dg << 16; else R.d[g >> 1] = dg;
+    }
+    root3_store_d<COPY>(r, R);
+    return (sum + 1 + 256) & 0xFFFF;
+}
+
+}  // namespace

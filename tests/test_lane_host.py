@@ -21,7 +21,7 @@ def lane(request):
     so = SO if request.param == "v2" else SO.replace("liblanehost", "liblanehost3")
     csrc = os.path.join(ROOT, "enet_amd", "csrc")
     src = [os.path.join(ROOT, "tests", "proto", "lane_host.cpp")] + \
-        [os.path.join(csrc, f) for f in ("rc_lane.hip", "rc_lane3.hip", "rc_lane_common.h")]
+        [os.path.join(csrc, f) for f in ("rc_lane.hip", "rc_lane3.hip", "rc_lane_common.h", "rc_root3.h")]
     if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in src):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared"] +
                               (["-DLANE3"] if request.param == "v3" else []) +
