@@ -200,6 +200,11 @@ class RangeCoder:
     def last_exact_count(self) -> int:
         return int(self.lib.enet_rc_last_exact_count(self.ctx))
 
+    def last_lane_count(self) -> int:
+        """Packets of the last batch the first pass (two-pass encoder or
+        bucket-history decoder) left to the lane kernels."""
+        return int(self.lib.enet_rc_last_lane_count(self.ctx))
+
 
 def _caps_offsets(caps):
     import torch

@@ -73,6 +73,8 @@ def _load() -> C.CDLL:
     lib.enet_rc_crc32.argtypes = [C.POINTER(ENetBuffer), sz]
     lib.enet_rc_last_exact_count.restype = u32
     lib.enet_rc_last_exact_count.argtypes = [vp]
+    lib.enet_rc_last_lane_count.restype = u32
+    lib.enet_rc_last_lane_count.argtypes = [vp]
     lib.enet_rc_version.restype = C.c_char_p
     lib.enet_rc_version.argtypes = []
     lib.rc_hip_lds_bytes.restype = u32

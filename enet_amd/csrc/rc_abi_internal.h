@@ -33,7 +33,8 @@ typedef struct {
 typedef struct {
     uint32_t *flag_list;    /* [n_cap] packets routed to the exact path */
     uint32_t *counters;     /* [4]: 0 = flagged count, 1 = work queue head (fast), 2 = exact queue head,
-                               3 = packets the two-pass encoder leaves to the lane kernels */
+                               3 = packets the two-pass encoder (compress) or the bucket-history
+                               decoder (decompress) leaves to the lane kernels */
     void     *exact_pool;   /* exact_slots * RC_EXACT_POOL_BYTES */
     uint32_t  exact_slots;
     uint32_t  n_cap;
@@ -51,6 +52,9 @@ typedef struct {
     void     *enc2_stream;  /* NULL: the encoder is off (ENET_RC_ENC2=0) or not allocated yet */
     uint64_t  enc2_cap;     /* bytes */
     uint32_t *enc2_list;    /* [n_cap] */
+    /* bucket-history decoder (rc_dec4.hip) in front of the v3 lane decoder; the packets it
+       leaves go to enc2_list / counters[3] (ENET_RC_DEC4=1: on) */
+    uint32_t  dec4;
     /* lane kernels: when set, run only the sub_count[0] packets of sub_list */
     const uint32_t *sub_list;
     const uint32_t *sub_count;
@@ -75,6 +79,11 @@ int rc_hip_decompress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *s
  * ws->counters[3]). */
 uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len);
 int rc_hip_enc2_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
+
+/* Bucket-history decoder (rc_dec4.hip): one packet per lane over the lane
+ * regions; packets off its fast path are listed in ws->enc2_list, count in
+ * ws->counters[3]. */
+int rc_hip_dec4_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
 uint32_t rc_hip_lane_region_bytes(uint32_t max_len);    /* model v2 */

@@ -1,0 +1,355 @@
+// rc_dec4.hip -- bucket-history range decoder (compress.c:498-627), bit-exact.
+//
+// One packet per lane, like the lane kernels (rc_lane3.hip), with a leaner
+// model.  compress.c's order-1 context of position i is (x[i-1]) and its
+// order-2 context is (x[i-2], x[i-1]); both hold only positions j with
+// x[j-1] = x[i-1].  So the decoder keeps, per packet, one 64-B record per
+// previous byte p ("bucket p") listing the positions decoded so far with
+// x[j-1] = p, each as an element (a = x[j-2], v = x[j], flags), and derives
+// every sub-context statistic from it (compress.c:159-199, :536-615):
+//
+//   order 2 (a, p): the elements with that a; t2 of them, dist2 of them new
+//       to the context when added:  escapes 5 * dist2, total escapes + 2 * t2
+//   order 1 (p): the elements not decoded at order 2 (the ones that visited
+//       order 1, compress.c:598-615); t1 of them, dist1 new to it:
+//       escapes 5 * dist1, total escapes + 2 * t1
+//   a symbol u of a context counts 2 per element with v = u, its cumulative
+//   count is 2 per element with v < u: the code r = READ - escapes selects
+//   the element of rank floor(r / 2) in value order.
+//
+// Elements are kept sorted by value (stable), so the selection is a prefix
+// count over a byte mask.  Appending the decoded position to its bucket is
+// every update the reference makes; nothing else is stored.  The root (order
+// 0) is the lane kernels' LDS table (rc_root3.h).
+//
+// Per byte: one record read (the bucket of the byte just decoded, issued as
+// soon as it is known) and one record write.  The flags record whether a
+// symbol was new (compress.c:306-310 / :606-610) -- a property of the history,
+// not of the decode path: a corrupt stream can escape from a context that
+// holds the symbol, and the reference's patch then finds it there.
+// tests/proto/histdec.py restates the algebra (CPU test against the oracle).
+//
+// Fast path: no bucket over kCap4 elements (no sub-context count or total
+// can then reach compress.c's rescale thresholds), no model reset (fewer
+// than 4094 nodes, compress.c:148-157), root codes within symbol 255.  A lane
+// that leaves it lists its packet (ws.enc2_list, count ws.counters[3]) and
+// the lane kernels decode that packet from the start.
+
+#ifndef RC_LANE_HOST_TEST
+#include <hip/hip_runtime.h>
+#else
+#include "lane_host_shim.h"   // tests/proto: host build of the per-lane logic (test only)
+#endif
+#include <stdint.h>
+
+#include "rc_abi_internal.h"
+#include "rc_udiv.h"
+#include "rc_lane_common.h"
+#include "rc_root3.h"
+
+namespace {
+
+constexpr uint32_t kCap4 = 20;              // elements per bucket record
+constexpr uint32_t kRec4 = 64;
+constexpr uint32_t kNodeLimit4 = 4096 - 2;  // compress.c:148-157
+
+// element flags (one byte per element)
+constexpr uint32_t kHit2 = 1, kNew2 = 2, kNew1 = 4, kHasA = 8;
+
+// bucket record (16 dwords): w0 = tag | k << 16 | nh2 << 21 | nn1 << 26
+// (k elements, nh2 of them decoded at order 2, nn1 new to order 1);
+// a[20] w1..5, v[20] w6..10 (ascending, stable), f[20] w11..15.  A tag other
+// than the lane's epoch reads as an empty bucket.
+struct Bucket { uint32_t h; uint32_t a[5], v[5], f[5]; };
+struct Raw4 { uint4 q0, q1, q2, q3; };
+
+DEV uint32_t bk_k(uint32_t h) { return (h >> 16) & 31; }
+
+DEV void raw4_load(const uint8_t* reg, uint32_t off, Raw4& w)
+{
+    const uint4* p = reinterpret_cast<const uint4*>(reg + off);
+    w.q0 = p[0]; w.q1 = p[1]; w.q2 = p[2]; w.q3 = p[3];
+}
+
+DEV void bk_from(const Raw4& w, uint32_t epoch, Bucket& B)
+{
+    B.h = (w.q0.x & 0xFFFFu) == epoch ? w.q0.x : epoch;   // (the arrays only count below k)
+    B.a[0] = w.q0.y; B.a[1] = w.q0.z; B.a[2] = w.q0.w; B.a[3] = w.q1.x; B.a[4] = w.q1.y;
+    B.v[0] = w.q1.z; B.v[1] = w.q1.w; B.v[2] = w.q2.x; B.v[3] = w.q2.y; B.v[4] = w.q2.z;
+    B.f[0] = w.q2.w; B.f[1] = w.q3.x; B.f[2] = w.q3.y; B.f[3] = w.q3.z; B.f[4] = w.q3.w;
+}
+
+DEV void bk_store(uint8_t* reg, uint32_t off, const Bucket& B)
+{
+    uint4* p = reinterpret_cast<uint4*>(reg + off);
+    p[0] = make_uint4(B.h, B.a[0], B.a[1], B.a[2]);
+    p[1] = make_uint4(B.a[3], B.a[4], B.v[0], B.v[1]);
+    p[2] = make_uint4(B.v[2], B.v[3], B.v[4], B.f[0]);
+    p[3] = make_uint4(B.f[1], B.f[2], B.f[3], B.f[4]);
+}
+
+// 0x01 in each byte where x and y agree
+DEV uint32_t eq01(uint32_t x, uint32_t y)
+{
+    const uint32_t z = x ^ y;
+    const uint32_t t = ((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z;
+    return (~t >> 7) & 0x01010101u;
+}
+
+// ny for swar_ge: 0x01 in each byte >= u (u <= 256)
+DEV uint32_t ny_of(uint32_t u) { return 0x01000100u - u * 0x00010001u; }
+
+// the two sub-contexts of a position, as byte masks over the bucket's elements
+struct Groups {
+    uint32_t g2[5], g1[5];      // 0x01 per member: order 2 (a, p), order 1 (p)
+    uint32_t t2, d2, t1, d1;    // members, members added as new symbols
+};
+
+DEV void bk_groups(const Bucket& B, uint32_t acur, bool o2, Groups& s)
+{
+    const uint32_t k = bk_k(B.h);
+    const uint32_t ap = acur * 0x01010101u;
+    s.t2 = 0; s.d2 = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 5; ++d) {
+        const uint32_t vm = below_mask(static_cast<int>(k), static_cast<int>(d)) & 0x01010101u;
+        const uint32_t g2 = o2 ? (eq01(B.a[d], ap) & (B.f[d] >> 3) & vm) : 0u;
+        s.g2[d] = g2;
+        s.t2 = sad(g2, s.t2);
+        s.d2 = sad(g2 & (B.f[d] >> 1), s.d2);
+        s.g1[d] = vm & ~B.f[d];
+    }
+    s.t1 = k - ((B.h >> 21) & 31);
+    s.d1 = (B.h >> 26) & 31;
+}
+
+// position (0..19) of the member of rank r (0-based) of the byte set g:
+// the number of positions whose inclusive member count is <= r
+DEV uint32_t bk_select(const uint32_t* g, uint32_t r)
+{
+    uint32_t base = 0, j = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 5; ++d) {
+        uint32_t inc = g[d] + (g[d] << 8);
+        inc += inc << 16;                                   // inclusive prefix count per byte (<= 4)
+        const int t = static_cast<int>(r) - static_cast<int>(base);
+        const uint32_t tt = t < 0 ? 0u : (t > 3 ? 3u : static_cast<uint32_t>(t));
+        const uint32_t above = sad(swar_ge(inc, ny_of(tt + 1)), 0u);
+        j += t < 0 ? 0u : (t > 3 ? 4u : 4u - above);
+        base += inc >> 24;
+    }
+    return j;
+}
+
+// byte j of a 20-byte array (a masked OR: a select chain on a lane-varying
+// index compiles to a dynamically indexed scratch load)
+DEV uint32_t byte_at(const uint32_t* x, uint32_t j)
+{
+    const uint32_t d = j >> 2;
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 5; ++e) w |= x[e] & (0u - static_cast<uint32_t>(d == e));
+    return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
+// members of g below u, and equal to u
+DEV void bk_interval(const Bucket& B, const uint32_t* g, uint32_t u, uint32_t& less, uint32_t& same)
+{
+    const uint32_t ny = ny_of(u), up = u * 0x01010101u;
+    less = 0; same = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 5; ++d) {
+        less = sad((swar_ge(B.v[d], ny) ^ 0x01010101u) & g[d], less);
+        same = sad(eq01(B.v[d], up) & g[d], same);
+    }
+}
+
+// compress.c:536-568 in one sub-context: READ, then an escape (false) or the
+// member the code selects (true; v, with its interval decoded).  fail: the
+// code is past the context's symbols (compress.c:416).
+DEV bool sub_decode(const Bucket& B, const uint32_t* g, uint32_t t, uint32_t dd, uint32_t& low, uint32_t& code,
+                    uint32_t& range, ByteSrc& in, uint32_t& v, bool& fail)
+{
+    const uint32_t esc = kSubEscDelta * dd, tot = esc + kSubDelta * t;
+    const uint32_t cd = dec_read(range, low, code, tot, true);
+    if (cd < esc) {
+        dec_code(low, code, range, 0, esc, in, true);
+        return false;
+    }
+    const uint32_t r = cd - esc;
+    if (r >= kSubDelta * t) { fail = true; return false; }
+    v = byte_at(B.v, bk_select(g, r >> 1));
+    uint32_t less, same;
+    bk_interval(B, g, v, less, same);
+    dec_code(low, code, range, esc + kSubDelta * less, kSubDelta * same, in, true);
+    return true;
+}
+
+// the element (a, v, f) joins the bucket in value order (after equal values)
+DEV void bk_insert(Bucket& B, uint32_t a, uint32_t v, uint32_t f, bool en)
+{
+    const uint32_t k = bk_k(B.h);
+    const uint32_t ny = ny_of(v + 1);
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 5; ++d) {
+        const uint32_t vm = below_mask(static_cast<int>(k), static_cast<int>(d)) & 0x01010101u;
+        pos = sad((swar_ge(B.v[d], ny) ^ 0x01010101u) & vm, pos);
+    }
+    const int pp = static_cast<int>(pos);
+    const uint32_t ar = a * 0x01010101u, vr = v * 0x01010101u, fr = f * 0x01010101u;
+    uint32_t pa = 0, pv = 0, pf = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 5; ++d) {
+        // bytes below pos stay, byte pos is new, bytes above move up one
+        const uint32_t keep = en ? below_mask(pp, static_cast<int>(d)) : 0xFFFFFFFFu;
+        const uint32_t im = en ? byte_mask(pp, static_cast<int>(d)) : 0u;
+        const uint32_t ca = B.a[d], cv = B.v[d], cf = B.f[d];
+        B.a[d] = (ca & keep) | (align8(ca, pa, 3) & ~keep & ~im) | (ar & im);
+        B.v[d] = (cv & keep) | (align8(cv, pv, 3) & ~keep & ~im) | (vr & im);
+        B.f[d] = (cf & keep) | (align8(cf, pf, 3) & ~keep & ~im) | (fr & im);
+        pa = ca; pv = cv; pf = cf;
+    }
+    B.h += en ? ((1u << 16) + ((f & kHit2) ? (1u << 21) : 0u) + ((f & kNew1) ? (1u << 26) : 0u)) : 0u;
+}
+
+DEV void bail(const rc_workspace_dev& ws, uint32_t pkt)
+{
+    const uint32_t slot = atomicAdd(&ws.counters[3], 1u);
+    ws.enc2_list[slot] = pkt;
+}
+
+DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg,
+                         uint8_t* root)
+{
+    const uint32_t len = bt.in_len[pkt];
+    const uint32_t cap = bt.out_cap[pkt];
+    if (len == 0) { bt.out_len[pkt] = 0; return; }                   // compress.c:513
+    ByteSink o;
+    sink_init(o, bt.out + bt.out_off[pkt], cap);
+    ByteSrc in;
+    src_init(in, bt.in + bt.in_off[pkt], len);
+    const uint32_t epoch = next_epoch(reg, *reinterpret_cast<const uint32_t*>(reg)) & 0xFFFF;
+    Root R;
+    root3_clear<false>(root, R);
+    uint32_t rtot = 1 + 256;
+    uint32_t low = 0, range = ~0u;
+    uint32_t code = static_cast<uint32_t>(in.la >> 32);            // compress.c:344-350 (0 past the end)
+    in.la <<= 32;
+    in.na -= 4;
+    src_refill(in, true);
+
+    Bucket B;                       // bucket p of this step
+    B.h = epoch;
+#pragma unroll
+    for (uint32_t d = 0; d < 5; ++d) { B.a[d] = 0u; B.v[d] = 0u; B.f[d] = 0u; }
+    Raw4 rw;                        // the next step's bucket, in flight
+    uint32_t fwd = 1;               // (a word: a bool would be an SGPR lane mask)
+    uint32_t order = 0, a = 0, p = 0, nodes = 1;
+    bool fail = false, off = false;
+
+    for (;;) {
+        if (!fwd) bk_from(rw, epoch, B);
+        sink_flush(o);
+        src_fill(in, true);
+        Groups s;
+        bk_groups(B, a, order >= 2, s);
+        int at = -1;
+        uint32_t v = 0;
+        bool new0 = false;
+        // order 2, then order 1: visited when the context holds elements
+        // (escapes 0 < 5 * dist < total, compress.c:536-544)
+        if (order >= 2 && s.t2 > 0) {
+            if (sub_decode(B, s.g2, s.t2, s.d2, low, code, range, in, v, fail)) at = 2;
+            if (fail) break;
+        }
+        if (at < 0 && order >= 1 && s.t1 > 0) {
+            if (sub_decode(B, s.g1, s.t1, s.d1, low, code, range, in, v, fail)) at = 1;
+            if (fail) break;
+        }
+        // root, compress.c:570-596
+        if (at < 0) {
+            const uint32_t cd = dec_read(range, low, code, rtot, true);
+            if (cd < 1) { dec_code(low, code, range, 0, 1, in, true); break; }   // end of stream
+            if (cd - 1 >= rtot - 1) { off = true; break; }                 // past symbol 255
+            uint32_t under, cnt;
+            v = root3_search(root, R, cd - 1, under, cnt);
+            new0 = cnt == 0;
+            root3_add<false>(root, R, v, cnt);
+            dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
+            rtot = (rtot + kRootDelta) & 0xFFFF;
+            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
+            at = 0;
+        }
+        // the next step's bucket: this one when v == p (updated below), else a
+        // load issued now so that its latency overlaps the rest of the step.
+        // The step's memory operations are unconditional (the scratch record
+        // for lanes that need none; see rc_lane3.hip lane_prefetch).
+        const bool nfwd = order >= 1 && v == p;
+        raw4_load(reg, nfwd ? kDummyRec : kO1Base + v * kRec4, rw);
+        fail = o.n >= o.cap;                                         // compress.c:617
+        // the element joins bucket p (compress.c:598-615: every visited
+        // context gains v); nodes as compress.c creates them
+        const uint32_t vp = v * 0x01010101u;
+        uint32_t h2 = 0, h1 = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < 5; ++d) {
+            const uint32_t e = eq01(B.v[d], vp);
+            h2 |= e & s.g2[d];
+            h1 |= e & s.g1[d];
+        }
+        const bool n2 = order >= 2 && h2 == 0;
+        const bool n1 = order >= 1 && at != 2 && h1 == 0;
+        nodes += (new0 ? 1u : 0u) + (n2 ? 1u : 0u) + (n1 ? 1u : 0u);
+        const bool full = order >= 1 && bk_k(B.h) >= kCap4;
+        const uint32_t f = (at == 2 ? kHit2 : 0u) | (n2 ? kNew2 : 0u) | (n1 ? kNew1 : 0u) | (order >= 2 ? kHasA : 0u);
+        bk_insert(B, a, v, f, order >= 1 && !full);
+        // (the step's last memory operation)
+        bk_store(reg, order >= 1 ? kO1Base + p * kRec4 : kDummyRec, B);
+        off = full || nodes >= kNodeLimit4;
+        if (fail || off) break;
+        sink_put(o, v, 1, true);
+        src_adv(in);
+        fwd = nfwd ? 1u : 0u;
+        a = p;
+        p = v;
+        order += order < 2 ? 1u : 0u;
+    }
+    if (off && !fail) { bail(ws, pkt); return; }
+    sink_finish(o, !fail);
+    bt.out_len[pkt] = fail ? 0u : o.n;
+}
+
+}  // namespace
+
+#ifndef RC_LANE_HOST_TEST
+// one wave per SIMD by design (a packet per lane, 65536 lanes fill the chip)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void rc_decompress_dec4(rc_batch_dev b, rc_workspace_dev ws)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t act = ws.lane_active;
+    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l >= act) return;
+    const uint32_t local = wave * act + l;
+    uint8_t* root = smem + local * kRootStride3;
+    const uint32_t per_block = 4 * act;
+    const uint32_t slot = blockIdx.x * per_block + local;
+    uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
+    const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
+    for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
+        const uint32_t pkt = order ? order[i] : i;
+        decompress_one4(b, ws, pkt, reg, root);
+    }
+}
+
+// The decoder over the batch; packets off its fast path are listed in
+// ws->enc2_list, count in ws->counters[3], for the lane kernels.
+extern "C" int rc_hip_dec4_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t blocks, void* stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStride3;
+    hipLaunchKernelGGL(rc_decompress_dec4, dim3(blocks), dim3(256), lds, st, *b, *ws);
+    return static_cast<int>(hipGetLastError());
+}
+#endif  // RC_LANE_HOST_TEST

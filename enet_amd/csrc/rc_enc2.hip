@@ -56,6 +56,7 @@
 #include "rc_abi_internal.h"
 #include "rc_udiv.h"
 #include "rc_lane_common.h"
+#include "rc_root3.h"
 
 // Diagnostic build only (-DE2_PROF, tools/enc2_prof.py): per-phase cycles of
 // the scan pass, summed over wavefronts.  The product build has no stamps.
@@ -507,14 +508,20 @@ DEV void sub_interval(uint32_t t, uint32_t d, uint32_t same, uint32_t less, bool
 struct CodeState {
     uint32_t low, range, rtot;
     bool ok;
+    Root R;                     // the root's group boundaries (rc_root3.h)
 };
 
 // one position: its sub-context codes, then the root (compress.c:286-337)
-DEV void code_step(CodeState& k, Ring& o, uint8_t* root, uint32_t w0, uint32_t w1, bool en, uintptr_t dummy)
+DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, uint32_t w0, uint32_t w1, bool en,
+                   uintptr_t dummy)
 {
     en = en && k.ok;
     const uint32_t n0 = o.n;
     const uint32_t typ = w0 & 7, ext = w0 >> 16, v = w1 >> 24;
+    // the root lookup needs only v: three independent LDS reads whose latency
+    // overlaps the sub-context codes
+    uint32_t under0, cnt0;
+    root3_lookup(root, mtab, v, under0, cnt0);
     // first sub-context code: order 2 (types 3-6) or order 1 (types 1, 2)
     uint32_t un, ct, tt;
     sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
@@ -525,24 +532,26 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, uint32_t w0, uint32_t w
     code(k.low, k.range, un, ct, tt, o, en && (typ == 4 || typ == 5), k.ok);
     // root, compress.c:318-329
     const bool en0 = en && (typ <= 1 || typ == 3 || typ == 4);
-    uint32_t under0, cnt0;
-    root_lookup(root, v, under0, cnt0);
-    if (en0) root_add(root, v, cnt0);
+    if (en0) root3_add<true>(root, k.R, v, cnt0);
     code(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, o, en0, k.ok);
     k.rtot = en0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
     const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
-    if (any_lane(rs0)) { if (rs0) k.rtot = root_rescale(root); }
+    if (any_lane(rs0)) { if (rs0) k.rtot = root3_rescale<true>(root, k.R); }
     ring_store(o);                                    // the chunk read back a step ago
     ring_chunk(o, n0, dummy);
 }
 
 constexpr uint32_t kRing = 64;
-constexpr uint32_t kCodeLds = kRootStride + kRing;    // per lane
+constexpr uint32_t kCodeLds = kRootStride3 + kRing;   // per lane (92 dwords: b128 accesses conflict-free)
+constexpr uint32_t kCodeMtab = 256 * kCodeLds;         // the block's prefix-mask table (rc_root3.h)
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void rc_enc2_code(rc_batch_dev b, E2Params e)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint8_t* mtab = smem + kCodeMtab;
+    if (threadIdx.x < 16) root3_mask_init(smem + kCodeMtab, threadIdx.x);
+    __syncthreads();
     const uint32_t l = threadIdx.x & 63;
     if (l >= e.act) return;
     const uint32_t idx = e.lo + blockIdx.x * 4 * e.act + (threadIdx.x >> 6) * e.act + l;
@@ -555,14 +564,14 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     const uint32_t len = b.in_len[pkt];
     uint8_t* root = smem + threadIdx.x * kCodeLds;
     Ring o;
-    o.r = root + kRootStride;
+    o.r = root + kRootStride3;
     o.lo = reinterpret_cast<uintptr_t>(b.out + b.out_off[pkt]);
     o.n = 0;
     o.cap = b.out_cap[pkt];
     o.ch = make_uint4(0u, 0u, 0u, 0u);
     o.ca = base;
-    root_clear(root);
     CodeState k;
+    root3_clear<true>(root, k.R);
     k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
     __builtin_amdgcn_s_waitcnt(0);                    // settle the first chunks before the loop
     // Six positions per iteration from three chunk registers; each register
@@ -572,14 +581,14 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     // iteration that issued it, i.e. wait for it.)
     uintptr_t a = base + 48;
     for (uint32_t i = 0; any_lane(i < len && k.ok); i += 6, a += 48) {
-        code_step(k, o, root, c0.x, c0.y, i < len, base);
-        code_step(k, o, root, c0.z, c0.w, i + 1 < len, base);
+        code_step(k, o, root, mtab, c0.x, c0.y, i < len, base);
+        code_step(k, o, root, mtab, c0.z, c0.w, i + 1 < len, base);
         c0 = gload16(a);
-        code_step(k, o, root, c1.x, c1.y, i + 2 < len, base);
-        code_step(k, o, root, c1.z, c1.w, i + 3 < len, base);
+        code_step(k, o, root, mtab, c1.x, c1.y, i + 2 < len, base);
+        code_step(k, o, root, mtab, c1.z, c1.w, i + 3 < len, base);
         c1 = gload16(a + 16);
-        code_step(k, o, root, c2.x, c2.y, i + 4 < len, base);
-        code_step(k, o, root, c2.z, c2.w, i + 5 < len, base);
+        code_step(k, o, root, mtab, c2.x, c2.y, i + 4 < len, base);
+        code_step(k, o, root, mtab, c2.z, c2.w, i + 5 < len, base);
         c2 = gload16(a + 32);
     }
     ring_store(o);
@@ -648,7 +657,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         const uint32_t cnt = static_cast<uint32_t>(hi - lo);
         hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
                            0, st, *b, e);
-        hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 4 * e.act - 1) / (4 * e.act)), dim3(256), 256 * kCodeLds, st,
+        hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 4 * e.act - 1) / (4 * e.act)), dim3(256), kCodeMtab + 256, st,
                            *b, e);
     }
     return static_cast<int>(hipGetLastError());

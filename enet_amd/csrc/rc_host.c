@@ -188,6 +188,8 @@ void *enet_range_coder_create(void)
         c->ws.cus = (uint32_t) cus;
         const char *e2 = getenv("ENET_RC_ENC2");
         c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
+        const char *d4 = getenv("ENET_RC_DEC4");
+        c->ws.dec4 = d4 && strcmp(d4, "1") == 0;      /* experimental: off unless ENET_RC_DEC4=1 */
         const char *sl = getenv("ENET_RC_SLOTS");
         c->max_slots = MAX_LANE_SLOTS;
         if (sl && atol(sl) >= 256 && atol(sl) <= (1l << 22)) c->max_slots = (uint32_t) atol(sl);
@@ -759,6 +761,16 @@ int enet_host_compress_with_range_coder(ENetHost *host)
     compressor.destroy = enet_range_coder_destroy;
     enet_host_compress(host, &compressor);
     return 0;
+}
+
+uint32_t enet_rc_last_lane_count(void *context)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c) return 0;
+    uint32_t v = 0;
+    hipDeviceSynchronize();
+    if (hipMemcpy(&v, c->ws.counters + 3, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return v;
 }
 
 uint32_t enet_rc_last_exact_count(void *context)

@@ -843,6 +843,14 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
         w.sub_list = ws->enc2_list;
         w.sub_count = ws->counters + 3;
     }
+    if (ws->kernel == RC_KERNEL_LANE3 && decompress && ws->dec4) {
+        // the bucket-history decoder takes what it can (rc_dec4.hip); the
+        // lanes decode only the packets it lists
+        const int rc = rc_hip_dec4_launch(b, &w, blocks, stream);
+        if (rc != 0) return rc;
+        w.sub_list = ws->enc2_list;
+        w.sub_count = ws->counters + 3;
+    }
     if (ws->kernel == RC_KERNEL_LANE3) return rc_hip_lane3_launch(decompress, b, &w, blocks, stream);
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane, dim3(blocks), dim3(256), lds, st, *b, w);

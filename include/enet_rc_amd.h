@@ -192,6 +192,9 @@ int enet_rc_socket_send_batch(int socket, const uint8_t *buf, const uint64_t *of
 /* ============================================================ introspection */
 /* Number of packets of the last batch that took the exact (binary-tree) path. */
 uint32_t enet_rc_last_exact_count(void *context);
+/* Number of packets of the last batch that the first pass (the two-pass
+ * encoder, or the bucket-history decoder) left to the lane kernels. */
+uint32_t enet_rc_last_lane_count(void *context);
 /* Library version string. */
 const char *enet_rc_version(void);
 

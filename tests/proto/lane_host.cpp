@@ -4,6 +4,9 @@
 #include <string.h>
 #ifdef LANE3
 #include "../../enet_amd/csrc/rc_lane3.hip"
+#ifdef DEC4
+#include "../../enet_amd/csrc/rc_dec4.hip"
+#endif
 #define REGION_BYTES rc_hip_lane3_region_bytes
 #define COMPRESS_ONE compress_one3
 #define DECOMPRESS_ONE decompress_one3
@@ -34,12 +37,19 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
         memset(region, 0, need);                                   // like the device pool (epoch 0 = unused)
     }
     uint64_t ioff = 0, ooff = 0;
-    uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0};
+    uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0}, bails[2] = {0, 0};
     rc_batch_dev b = { in, &ioff, &len, out, &ooff, &cap, out_len, 1, max_len };
     rc_workspace_dev ws = {};
-    ws.flag_list = flags; ws.counters = counters; ws.lane_region = need; ws.lane_pool = region; ws.lane_active = 64;
+    ws.flag_list = flags; ws.counters = counters; ws.enc2_list = bails; ws.lane_region = need; ws.lane_pool = region; ws.lane_active = 64;
     *out_len = 0xFFFFFFFFu;
+#ifdef DEC4
+    // the bucket-history decoder first; a packet it leaves goes to the lanes (as on the GPU)
+    if (decompress) {
+        decompress_one4(b, ws, 0, region, g_root);
+        if (!counters[3]) return 0;
+    }
+#endif
     if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root);
     else COMPRESS_ONE(b, ws, 0, region, g_root COMPRESS_ARGS);
-    return counters[0] ? 1 : 0;   // 1 = routed to the exact path
+    return counters[0] ? 1 : (counters[3] ? 2 : 0);   // 1 = routed to the exact path, 2 = left by dec4
 }
