@@ -53,7 +53,7 @@ typedef struct {
     uint64_t  enc2_cap;     /* bytes */
     uint32_t *enc2_list;    /* [n_cap] */
     /* bucket-history decoder (rc_dec4.hip) in front of the v3 lane decoder; the packets it
-       leaves go to enc2_list / counters[3] (ENET_RC_DEC4=1: on) */
+       leaves go to enc2_list / counters[3] (ENET_RC_DEC4=0: off) */
     uint32_t  dec4;
     /* lane kernels: when set, run only the sub_count[0] packets of sub_list */
     const uint32_t *sub_list;

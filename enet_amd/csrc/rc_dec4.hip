@@ -17,8 +17,9 @@
 //   count is 2 per element with v < u: the code r = READ - escapes selects
 //   the element of rank floor(r / 2) in value order.
 //
-// Elements are kept sorted by value (stable), so the selection is a prefix
-// count over a byte mask.  Appending the decoded position to its bucket is
+// Elements are kept sorted by value (stable), with bit masks of their flags
+// and of where each run of equal values starts, so the selection is a rank
+// in a bit mask and a symbol's interval two bit scans.  Appending the decoded position to its bucket is
 // every update the reference makes; nothing else is stored.  The root (order
 // 0) is the lane kernels' LDS table (rc_root3.h).
 //
@@ -49,18 +50,23 @@
 
 namespace {
 
-constexpr uint32_t kCap4 = 20;              // elements per bucket record
+constexpr uint32_t kCap4 = 24;              // elements per bucket record
 constexpr uint32_t kRec4 = 64;
 constexpr uint32_t kNodeLimit4 = 4096 - 2;  // compress.c:148-157
 
-// element flags (one byte per element)
-constexpr uint32_t kHit2 = 1, kNew2 = 2, kNew1 = 4, kHasA = 8;
-
-// bucket record (16 dwords): w0 = tag | k << 16 | nh2 << 21 | nn1 << 26
-// (k elements, nh2 of them decoded at order 2, nn1 new to order 1);
-// a[20] w1..5, v[20] w6..10 (ascending, stable), f[20] w11..15.  A tag other
-// than the lane's epoch reads as an empty bucket.
-struct Bucket { uint32_t h; uint32_t a[5], v[5], f[5]; };
+// bucket record (16 dwords):
+//   w0  tag | k << 16 | nh2 << 21 | nn1 << 26  (k elements; nh2 of them decoded
+//       at order 2; nn1 new to order 1 when added)
+//   w1  hit mask: element decoded at order 2           (bit i = element i)
+//   w2  new mask: element new to its order-2 context
+//   w3  run mask: element's value differs from its predecessor's
+//   w4..9   a[24] (the byte before the bucket byte)
+//   w10..15 v[24] (ascending, stable; 0xFF past k)
+// Position 1 has no order-2 context: its element carries hit and new, a
+// combination no other element has (a hit is never new), which keeps it out
+// of every order-2 group and in its order-1 group.  A tag other than the
+// lane's epoch reads as an empty bucket.
+struct Bucket { uint32_t h, hit, nw, run; uint32_t a[6], v[6]; };
 struct Raw4 { uint4 q0, q1, q2, q3; };
 
 DEV uint32_t bk_k(uint32_t h) { return (h >> 16) & 31; }
@@ -71,21 +77,31 @@ DEV void raw4_load(const uint8_t* reg, uint32_t off, Raw4& w)
     w.q0 = p[0]; w.q1 = p[1]; w.q2 = p[2]; w.q3 = p[3];
 }
 
+DEV void bk_empty(Bucket& B, uint32_t epoch)
+{
+    B.h = epoch; B.hit = 0; B.nw = 0; B.run = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 6; ++d) { B.a[d] = 0u; B.v[d] = 0xFFFFFFFFu; }
+}
+
 DEV void bk_from(const Raw4& w, uint32_t epoch, Bucket& B)
 {
-    B.h = (w.q0.x & 0xFFFFu) == epoch ? w.q0.x : epoch;   // (the arrays only count below k)
-    B.a[0] = w.q0.y; B.a[1] = w.q0.z; B.a[2] = w.q0.w; B.a[3] = w.q1.x; B.a[4] = w.q1.y;
-    B.v[0] = w.q1.z; B.v[1] = w.q1.w; B.v[2] = w.q2.x; B.v[3] = w.q2.y; B.v[4] = w.q2.z;
-    B.f[0] = w.q2.w; B.f[1] = w.q3.x; B.f[2] = w.q3.y; B.f[3] = w.q3.z; B.f[4] = w.q3.w;
+    const bool live = (w.q0.x & 0xFFFFu) == epoch;
+    const uint32_t f = live ? 0xFFFFFFFFu : 0u;
+    B.h = live ? w.q0.x : epoch;
+    B.hit = w.q0.y & f; B.nw = w.q0.z & f; B.run = w.q0.w & f;
+    B.a[0] = w.q1.x; B.a[1] = w.q1.y; B.a[2] = w.q1.z; B.a[3] = w.q1.w; B.a[4] = w.q2.x; B.a[5] = w.q2.y;
+    B.v[0] = w.q2.z | ~f; B.v[1] = w.q2.w | ~f; B.v[2] = w.q3.x | ~f;
+    B.v[3] = w.q3.y | ~f; B.v[4] = w.q3.z | ~f; B.v[5] = w.q3.w | ~f;
 }
 
 DEV void bk_store(uint8_t* reg, uint32_t off, const Bucket& B)
 {
     uint4* p = reinterpret_cast<uint4*>(reg + off);
-    p[0] = make_uint4(B.h, B.a[0], B.a[1], B.a[2]);
-    p[1] = make_uint4(B.a[3], B.a[4], B.v[0], B.v[1]);
-    p[2] = make_uint4(B.v[2], B.v[3], B.v[4], B.f[0]);
-    p[3] = make_uint4(B.f[1], B.f[2], B.f[3], B.f[4]);
+    p[0] = make_uint4(B.h, B.hit, B.nw, B.run);
+    p[1] = make_uint4(B.a[0], B.a[1], B.a[2], B.a[3]);
+    p[2] = make_uint4(B.a[4], B.a[5], B.v[0], B.v[1]);
+    p[3] = make_uint4(B.v[2], B.v[3], B.v[4], B.v[5]);
 }
 
 // 0x01 in each byte where x and y agree
@@ -96,78 +112,94 @@ DEV uint32_t eq01(uint32_t x, uint32_t y)
     return (~t >> 7) & 0x01010101u;
 }
 
+// the 0x01 bytes of e as four bits
+DEV uint32_t gather4(uint32_t e) { return (e | (e >> 7) | (e >> 14) | (e >> 21)) & 0xFu; }
+
 // ny for swar_ge: 0x01 in each byte >= u (u <= 256)
 DEV uint32_t ny_of(uint32_t u) { return 0x01000100u - u * 0x00010001u; }
 
-// the two sub-contexts of a position, as byte masks over the bucket's elements
+DEV uint32_t popc(uint32_t x) { return static_cast<uint32_t>(__builtin_popcount(x)); }
+DEV uint32_t low_bits(uint32_t n) { return n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u); }
+
+// the two sub-contexts of a position, as bit masks over the bucket's elements
 struct Groups {
-    uint32_t g2[5], g1[5];      // 0x01 per member: order 2 (a, p), order 1 (p)
+    uint32_t g2, g1;            // members: order 2 (a, p), order 1 (p)
     uint32_t t2, d2, t1, d1;    // members, members added as new symbols
 };
 
-DEV void bk_groups(const Bucket& B, uint32_t acur, bool o2, Groups& s)
+// Dwords of the byte arrays that hold an element, or the insertion point, in
+// any lane of the wave (a wave-uniform count: the rest is skipped).
+DEV uint32_t live_dwords(uint32_t k)
 {
-    const uint32_t k = bk_k(B.h);
-    const uint32_t ap = acur * 0x01010101u;
-    s.t2 = 0; s.d2 = 0;
+    uint32_t nd = 1;
 #pragma unroll
-    for (uint32_t d = 0; d < 5; ++d) {
-        const uint32_t vm = below_mask(static_cast<int>(k), static_cast<int>(d)) & 0x01010101u;
-        const uint32_t g2 = o2 ? (eq01(B.a[d], ap) & (B.f[d] >> 3) & vm) : 0u;
-        s.g2[d] = g2;
-        s.t2 = sad(g2, s.t2);
-        s.d2 = sad(g2 & (B.f[d] >> 1), s.d2);
-        s.g1[d] = vm & ~B.f[d];
-    }
+    for (uint32_t d = 1; d < 6; ++d) nd += any_lane(k >= 4 * d) ? 1u : 0u;
+    return nd;
+}
+
+DEV void bk_groups(const Bucket& B, uint32_t nd, uint32_t acur, bool o2, Groups& s)
+{
+    const uint32_t k = bk_k(B.h), km = low_bits(k);
+    const uint32_t ap = acur * 0x01010101u;
+    uint32_t am = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 6; ++d)
+        if (d < nd) am |= gather4(eq01(B.a[d], ap)) << (4 * d);
+    s.g2 = o2 ? (am & km & ~(B.hit & B.nw)) : 0u;
+    s.g1 = (~B.hit | B.nw) & km;
+    s.t2 = popc(s.g2);
+    s.d2 = popc(s.g2 & B.nw);
     s.t1 = k - ((B.h >> 21) & 31);
     s.d1 = (B.h >> 26) & 31;
 }
 
-// position (0..19) of the member of rank r (0-based) of the byte set g:
-// the number of positions whose inclusive member count is <= r
-DEV uint32_t bk_select(const uint32_t* g, uint32_t r)
+// index of the member of rank r (0-based) of the bit set g: the largest j
+// with fewer than r + 1 members below j
+DEV uint32_t select_bit(uint32_t g, uint32_t r)
 {
-    uint32_t base = 0, j = 0;
+    uint32_t j = 0;
 #pragma unroll
-    for (uint32_t d = 0; d < 5; ++d) {
-        uint32_t inc = g[d] + (g[d] << 8);
-        inc += inc << 16;                                   // inclusive prefix count per byte (<= 4)
-        const int t = static_cast<int>(r) - static_cast<int>(base);
-        const uint32_t tt = t < 0 ? 0u : (t > 3 ? 3u : static_cast<uint32_t>(t));
-        const uint32_t above = sad(swar_ge(inc, ny_of(tt + 1)), 0u);
-        j += t < 0 ? 0u : (t > 3 ? 4u : 4u - above);
-        base += inc >> 24;
+    for (uint32_t step = 16; step >= 1; step >>= 1) {
+        const uint32_t jj = j + step;
+        j = popc(g & low_bits(jj)) <= r ? jj : j;
     }
     return j;
 }
 
-// byte j of a 20-byte array (a masked OR: a select chain on a lane-varying
+// byte j of a 24-byte array (a masked OR: a select chain on a lane-varying
 // index compiles to a dynamically indexed scratch load)
 DEV uint32_t byte_at(const uint32_t* x, uint32_t j)
 {
     const uint32_t d = j >> 2;
     uint32_t w = 0;
 #pragma unroll
-    for (uint32_t e = 0; e < 5; ++e) w |= x[e] & (0u - static_cast<uint32_t>(d == e));
+    for (uint32_t e = 0; e < 6; ++e) w |= x[e] & (0u - static_cast<uint32_t>(d == e));
     return (w >> (8 * (j & 3))) & 0xFFu;
 }
 
-// members of g below u, and equal to u
-DEV void bk_interval(const Bucket& B, const uint32_t* g, uint32_t u, uint32_t& less, uint32_t& same)
+// elements with a value below u, and at most u (the bucket is sorted: the
+// elements equal to u are [lt, le))
+DEV void bk_rank(const Bucket& B, uint32_t nd, uint32_t u, uint32_t& lt, uint32_t& le)
 {
-    const uint32_t ny = ny_of(u), up = u * 0x01010101u;
-    less = 0; same = 0;
+    const uint32_t n0 = ny_of(u), n1 = ny_of(u + 1);
+    uint32_t ge0 = 0, ge1 = 0;
 #pragma unroll
-    for (uint32_t d = 0; d < 5; ++d) {
-        less = sad((swar_ge(B.v[d], ny) ^ 0x01010101u) & g[d], less);
-        same = sad(eq01(B.v[d], up) & g[d], same);
+    for (uint32_t d = 0; d < 6; ++d) {
+        if (d < nd) {
+            ge0 = sad(swar_ge(B.v[d], n0), ge0);
+            ge1 = sad(swar_ge(B.v[d], n1), ge1);
+        }
     }
+    const uint32_t k = bk_k(B.h);
+    lt = 4 * nd - ge0;                        // (slots past k hold 0xFF: never below u)
+    le = min(4 * nd - ge1, k);                // (... but at most 0xFF: u = 255 counts them)
 }
 
 // compress.c:536-568 in one sub-context: READ, then an escape (false) or the
 // member the code selects (true; v, with its interval decoded).  fail: the
-// code is past the context's symbols (compress.c:416).
-DEV bool sub_decode(const Bucket& B, const uint32_t* g, uint32_t t, uint32_t dd, uint32_t& low, uint32_t& code,
+// code is past the context's symbols (compress.c:416).  The members with the
+// selected value form the run of the run mask that holds it.
+DEV bool sub_decode(const Bucket& B, uint32_t g, uint32_t t, uint32_t dd, uint32_t& low, uint32_t& code,
                     uint32_t& range, ByteSrc& in, uint32_t& v, bool& fail)
 {
     const uint32_t esc = kSubEscDelta * dd, tot = esc + kSubDelta * t;
@@ -178,39 +210,47 @@ DEV bool sub_decode(const Bucket& B, const uint32_t* g, uint32_t t, uint32_t dd,
     }
     const uint32_t r = cd - esc;
     if (r >= kSubDelta * t) { fail = true; return false; }
-    v = byte_at(B.v, bk_select(g, r >> 1));
-    uint32_t less, same;
-    bk_interval(B, g, v, less, same);
+    const uint32_t j = select_bit(g, r >> 1);
+    v = byte_at(B.v, j);
+    const uint32_t upto = low_bits(j + 1);
+    const uint32_t lo = 31u - static_cast<uint32_t>(__builtin_clz(B.run & upto));   // (bit 0 is a run start)
+    const uint32_t above = B.run & ~upto & low_bits(bk_k(B.h));
+    const uint32_t hi = above ? static_cast<uint32_t>(__builtin_ctz(above)) : bk_k(B.h);
+    const uint32_t less = popc(g & low_bits(lo)), same = popc(g & low_bits(hi)) - less;
     dec_code(low, code, range, esc + kSubDelta * less, kSubDelta * same, in, true);
     return true;
 }
 
-// the element (a, v, f) joins the bucket in value order (after equal values)
-DEV void bk_insert(Bucket& B, uint32_t a, uint32_t v, uint32_t f, bool en)
+// bit pos of m gets b, bits above move up one
+DEV uint32_t bit_insert(uint32_t m, uint32_t pos, uint32_t b)
 {
-    const uint32_t k = bk_k(B.h);
-    const uint32_t ny = ny_of(v + 1);
-    uint32_t pos = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 5; ++d) {
-        const uint32_t vm = below_mask(static_cast<int>(k), static_cast<int>(d)) & 0x01010101u;
-        pos = sad((swar_ge(B.v[d], ny) ^ 0x01010101u) & vm, pos);
-    }
+    const uint32_t lo = low_bits(pos);
+    return (m & lo) | ((m & ~lo) << 1) | (b << pos);
+}
+
+// the element (a, v) joins the bucket at pos (after the values <= v)
+DEV void bk_insert(Bucket& B, uint32_t nd, uint32_t pos, uint32_t a, uint32_t v, uint32_t hit, uint32_t nw,
+                   uint32_t run, uint32_t hadd, bool en)
+{
     const int pp = static_cast<int>(pos);
-    const uint32_t ar = a * 0x01010101u, vr = v * 0x01010101u, fr = f * 0x01010101u;
-    uint32_t pa = 0, pv = 0, pf = 0;
+    const uint32_t ar = a * 0x01010101u, vr = v * 0x01010101u;
+    uint32_t pa = 0, pv = 0;
 #pragma unroll
-    for (uint32_t d = 0; d < 5; ++d) {
-        // bytes below pos stay, byte pos is new, bytes above move up one
-        const uint32_t keep = en ? below_mask(pp, static_cast<int>(d)) : 0xFFFFFFFFu;
-        const uint32_t im = en ? byte_mask(pp, static_cast<int>(d)) : 0u;
-        const uint32_t ca = B.a[d], cv = B.v[d], cf = B.f[d];
-        B.a[d] = (ca & keep) | (align8(ca, pa, 3) & ~keep & ~im) | (ar & im);
-        B.v[d] = (cv & keep) | (align8(cv, pv, 3) & ~keep & ~im) | (vr & im);
-        B.f[d] = (cf & keep) | (align8(cf, pf, 3) & ~keep & ~im) | (fr & im);
-        pa = ca; pv = cv; pf = cf;
+    for (uint32_t d = 0; d < 6; ++d) {
+        if (d < nd) {
+            // bytes below pos stay, byte pos is new, bytes above move up one
+            const uint32_t keep = en ? below_mask(pp, static_cast<int>(d)) : 0xFFFFFFFFu;
+            const uint32_t im = en ? byte_mask(pp, static_cast<int>(d)) : 0u;
+            const uint32_t ca = B.a[d], cv = B.v[d];
+            B.a[d] = (ca & keep) | (align8(ca, pa, 3) & ~keep & ~im) | (ar & im);
+            B.v[d] = (cv & keep) | (align8(cv, pv, 3) & ~keep & ~im) | (vr & im);
+            pa = ca; pv = cv;
+        }
     }
-    B.h += en ? ((1u << 16) + ((f & kHit2) ? (1u << 21) : 0u) + ((f & kNew1) ? (1u << 26) : 0u)) : 0u;
+    B.hit = en ? bit_insert(B.hit, pos, hit) : B.hit;
+    B.nw = en ? bit_insert(B.nw, pos, nw) : B.nw;
+    B.run = en ? bit_insert(B.run, pos, run) : B.run;
+    B.h += en ? hadd : 0u;
 }
 
 DEV void bail(const rc_workspace_dev& ws, uint32_t pkt)
@@ -219,8 +259,14 @@ DEV void bail(const rc_workspace_dev& ws, uint32_t pkt)
     ws.enc2_list[slot] = pkt;
 }
 
+// wbail: this wavefront's count of packets left to the lanes (LDS).  Once a
+// quarter of the wavefront has left its packet, the rest follow at once:
+// a batch of low-entropy packets (large buckets) then costs this decoder a
+// few steps instead of the steps until its last lane fills a bucket.
+constexpr uint32_t kWaveBail = 16;
+
 DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg,
-                         uint8_t* root)
+                         uint8_t* root, uint32_t* wbail)
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
@@ -240,9 +286,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     src_refill(in, true);
 
     Bucket B;                       // bucket p of this step
-    B.h = epoch;
-#pragma unroll
-    for (uint32_t d = 0; d < 5; ++d) { B.a[d] = 0u; B.v[d] = 0u; B.f[d] = 0u; }
+    bk_empty(B, epoch);
     Raw4 rw;                        // the next step's bucket, in flight
     uint32_t fwd = 1;               // (a word: a bool would be an SGPR lane mask)
     uint32_t order = 0, a = 0, p = 0, nodes = 1;
@@ -252,8 +296,9 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         if (!fwd) bk_from(rw, epoch, B);
         sink_flush(o);
         src_fill(in, true);
+        const uint32_t nd = live_dwords(bk_k(B.h));
         Groups s;
-        bk_groups(B, a, order >= 2, s);
+        bk_groups(B, nd, a, order >= 2, s);
         int at = -1;
         uint32_t v = 0;
         bool new0 = false;
@@ -290,23 +335,19 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         fail = o.n >= o.cap;                                         // compress.c:617
         // the element joins bucket p (compress.c:598-615: every visited
         // context gains v); nodes as compress.c creates them
-        const uint32_t vp = v * 0x01010101u;
-        uint32_t h2 = 0, h1 = 0;
-#pragma unroll
-        for (uint32_t d = 0; d < 5; ++d) {
-            const uint32_t e = eq01(B.v[d], vp);
-            h2 |= e & s.g2[d];
-            h1 |= e & s.g1[d];
-        }
-        const bool n2 = order >= 2 && h2 == 0;
-        const bool n1 = order >= 1 && at != 2 && h1 == 0;
+        uint32_t lt, le;
+        bk_rank(B, nd, v, lt, le);
+        const uint32_t eqr = low_bits(le) & ~low_bits(lt);
+        const bool n2 = order >= 2 && (s.g2 & eqr) == 0;
+        const bool n1 = order >= 1 && at != 2 && (s.g1 & eqr) == 0;
         nodes += (new0 ? 1u : 0u) + (n2 ? 1u : 0u) + (n1 ? 1u : 0u);
         const bool full = order >= 1 && bk_k(B.h) >= kCap4;
-        const uint32_t f = (at == 2 ? kHit2 : 0u) | (n2 ? kNew2 : 0u) | (n1 ? kNew1 : 0u) | (order >= 2 ? kHasA : 0u);
-        bk_insert(B, a, v, f, order >= 1 && !full);
+        const uint32_t first = order == 1 ? 1u : 0u;                 // position 1: hit and new
+        bk_insert(B, nd, le, a, v, (at == 2 ? 1u : 0u) | first, (n2 ? 1u : 0u) | first, lt == le ? 1u : 0u,
+                  (1u << 16) + (at == 2 ? (1u << 21) : 0u) + (n1 ? (1u << 26) : 0u), order >= 1 && !full);
         // (the step's last memory operation)
         bk_store(reg, order >= 1 ? kO1Base + p * kRec4 : kDummyRec, B);
-        off = full || nodes >= kNodeLimit4;
+        off = full || nodes >= kNodeLimit4 || *wbail >= kWaveBail;
         if (fail || off) break;
         sink_put(o, v, 1, true);
         src_adv(in);
@@ -315,7 +356,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         p = v;
         order += order < 2 ? 1u : 0u;
     }
-    if (off && !fail) { bail(ws, pkt); return; }
+    if (off && !fail) { atomicAdd(wbail, 1u); bail(ws, pkt); return; }
     sink_finish(o, !fail);
     bt.out_len[pkt] = fail ? 0u : o.n;
 }
@@ -332,14 +373,16 @@ void rc_decompress_dec4(rc_batch_dev b, rc_workspace_dev ws)
     const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (l >= act) return;
     const uint32_t local = wave * act + l;
-    uint8_t* root = smem + local * kRootStride3;
+    uint8_t* root = smem + local * kRootStrideDec;
+    uint32_t* wbail = reinterpret_cast<uint32_t*>(smem + 4 * act * kRootStrideDec) + wave;
+    if (l == 0) *wbail = 0u;
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
         const uint32_t pkt = order ? order[i] : i;
-        decompress_one4(b, ws, pkt, reg, root);
+        decompress_one4(b, ws, pkt, reg, root, wbail);
     }
 }
 
@@ -348,7 +391,7 @@ void rc_decompress_dec4(rc_batch_dev b, rc_workspace_dev ws)
 extern "C" int rc_hip_dec4_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStride3;
+    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStrideDec + 16;   // + wbail[4]
     hipLaunchKernelGGL(rc_decompress_dec4, dim3(blocks), dim3(256), lds, st, *b, *ws);
     return static_cast<int>(hipGetLastError());
 }

@@ -401,8 +401,8 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 
 // ------------------------------------------------------------------ pass 2
 
-// ---- output: a 64-B ring per lane in LDS.  Byte A of the packet's output
-// (A an absolute address) lives at ring[A & 63], so every aligned 16-B chunk
+// ---- output: a 32-B ring per lane in LDS.  Byte A of the packet's output
+// (A an absolute address) lives at ring[A & 31], so every aligned 16-B chunk
 // of the output is an aligned 16-B slot of the ring.  A code appends its
 // settled bytes with three byte writes (bytes past the count are rewritten by
 // the next code before their chunk completes); a chunk that completes during
@@ -420,9 +420,9 @@ DEV void ring_put(Ring& o, uint32_t low, uint32_t k, bool put)
 {
     if (put) {
         const uint32_t p = static_cast<uint32_t>(o.lo) + o.n;
-        o.r[p & 63] = static_cast<uint8_t>(low >> 24);
-        o.r[(p + 1) & 63] = static_cast<uint8_t>(low >> 16);
-        o.r[(p + 2) & 63] = static_cast<uint8_t>(low >> 8);
+        o.r[p & 31] = static_cast<uint8_t>(low >> 24);
+        o.r[(p + 1) & 31] = static_cast<uint8_t>(low >> 16);
+        o.r[(p + 2) & 31] = static_cast<uint8_t>(low >> 8);
         o.n += k;
     }
 }
@@ -441,7 +441,7 @@ DEV void ring_chunk(Ring& o, uint32_t n0, uintptr_t dummy)
     const uintptr_t e0 = o.lo + n0, e1 = o.lo + o.n;
     const bool done = (e0 >> 4) != (e1 >> 4);         // codes add <= 12 bytes: at most one chunk
     const uintptr_t c = (e1 & ~static_cast<uintptr_t>(15)) - 16;
-    o.ch = *reinterpret_cast<const uint4*>(o.r + (c & 63));
+    o.ch = *reinterpret_cast<const uint4*>(o.r + (c & 31));
     const bool edge = done && c < o.lo;               // the first chunk starts before the output
     o.ca = (done && !edge) ? c : dummy;
     if (rare_lane(edge)) {
@@ -456,7 +456,7 @@ DEV void ring_finish(Ring& o, bool en)
         if (en) {
             const uintptr_t e1 = o.lo + o.n, c = e1 & ~static_cast<uintptr_t>(15);
             if (e1 > c) {
-                const uint4 w = *reinterpret_cast<const uint4*>(o.r + (c & 63));
+                const uint4 w = *reinterpret_cast<const uint4*>(o.r + (c & 31));
                 sink_bytes(c, w, 0, static_cast<uint32_t>(e1 - c), o.lo);
             }
         }
@@ -541,8 +541,12 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, ui
     ring_chunk(o, n0, dummy);
 }
 
-constexpr uint32_t kRing = 64;
-constexpr uint32_t kCodeLds = kRootStride3 + kRing;   // per lane (92 dwords: b128 accesses conflict-free)
+// Per lane: the root (counts, D copy) at 0, the ring at 288, pad to 336 B
+// (84 dwords: b128 accesses conflict-free).  Two chunks suffice: a step adds
+// at most 12 bytes, so at most one chunk completes per step, and it is read
+// back at the end of that step, before its slot can be written again.
+constexpr uint32_t kRingAt = 288;
+constexpr uint32_t kCodeLds = 336;
 constexpr uint32_t kCodeMtab = 256 * kCodeLds;         // the block's prefix-mask table (rc_root3.h)
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
@@ -564,7 +568,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     const uint32_t len = b.in_len[pkt];
     uint8_t* root = smem + threadIdx.x * kCodeLds;
     Ring o;
-    o.r = root + kRootStride3;
+    o.r = root + kRingAt;
     o.lo = reinterpret_cast<uintptr_t>(b.out + b.out_off[pkt]);
     o.n = 0;
     o.cap = b.out_cap[pkt];

@@ -189,7 +189,7 @@ void *enet_range_coder_create(void)
         const char *e2 = getenv("ENET_RC_ENC2");
         c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
         const char *d4 = getenv("ENET_RC_DEC4");
-        c->ws.dec4 = d4 && strcmp(d4, "1") == 0;      /* experimental: off unless ENET_RC_DEC4=1 */
+        c->ws.dec4 = !(d4 && strcmp(d4, "0") == 0);
         const char *sl = getenv("ENET_RC_SLOTS");
         c->max_slots = MAX_LANE_SLOTS;
         if (sl && atol(sl) >= 256 && atol(sl) <= (1l << 22)) c->max_slots = (uint32_t) atol(sl);

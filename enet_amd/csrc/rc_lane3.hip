@@ -810,7 +810,7 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     }
     if (l >= act) return;
     const uint32_t local = wave * act + l;
-    uint8_t* root = smem + local * kRootStride3;
+    uint8_t* root = smem + local * (DECOMP ? kRootStrideDec : kRootStride3);
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
@@ -835,7 +835,10 @@ extern "C" int rc_hip_lane3_launch(int decompress, const rc_batch_dev* b, const 
                                    uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStride3 + 256;   // + the mask table
+    // the encoder: roots with their D copy + the mask table; the decoder: roots only (LDS
+    // left for a co-resident encoder block, rc_enc2_code)
+    const size_t lds = decompress ? static_cast<size_t>(4 * ws->lane_active) * kRootStrideDec
+                                  : static_cast<size_t>(4 * ws->lane_active) * kRootStride3 + 256;
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane3, dim3(blocks), dim3(256), lds, st, *b, *ws);
     else

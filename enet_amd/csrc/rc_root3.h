@@ -18,6 +18,7 @@ namespace {
 // the encoder's copy of D).  The decoder finds the group with packed compares
 // on the registers (no LDS reads).
 constexpr uint32_t kRootStride3 = 304;   // counts[256], D[16] (u16), pad
+constexpr uint32_t kRootStrideDec = 272; // decoders (no D copy): counts[256], pad (68 dwords: b128 conflict-free)
 constexpr uint32_t kRootD = 256;
 
 struct Root { uint32_t d[8]; };

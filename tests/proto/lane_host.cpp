@@ -45,7 +45,8 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
 #ifdef DEC4
     // the bucket-history decoder first; a packet it leaves goes to the lanes (as on the GPU)
     if (decompress) {
-        decompress_one4(b, ws, 0, region, g_root);
+        uint32_t wbail = 0;
+        decompress_one4(b, ws, 0, region, g_root, &wbail);
         if (!counters[3]) return 0;
     }
 #endif

@@ -17,23 +17,36 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(scope="module", params=["lane3", "lane2"])
+VARIANTS = {
+    # default: two-pass encoder (rc_enc2.hip) and bucket-history decoder
+    # (rc_dec4.hip) in front of the v3 lane kernels (rc_lane3.hip)
+    "lane3": {"ENET_RC_KERNEL": "lane3"},
+    # the v3 lane kernels alone, both directions
+    "lane3-only": {"ENET_RC_KERNEL": "lane3", "ENET_RC_ENC2": "0", "ENET_RC_DEC4": "0"},
+    # model v2 (rc_lane.hip)
+    "lane2": {"ENET_RC_KERNEL": "lane2"},
+}
+
+
+@pytest.fixture(scope="module", params=list(VARIANTS))
 def coder(request):
-    """Every test runs on the default lane kernels (model v3, rc_lane3.hip) and
-    on model v2 (rc_lane.hip), selected when the coder context is created."""
+    """Every test runs on each kernel configuration, selected by environment
+    when the coder context is created."""
     import os
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from enet_amd import RangeCoder
-    old = os.environ.get("ENET_RC_KERNEL")
-    os.environ["ENET_RC_KERNEL"] = request.param
+    env = VARIANTS[request.param]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         c = RangeCoder()
     finally:
-        if old is None:
-            os.environ.pop("ENET_RC_KERNEL", None)
-        else:
-            os.environ["ENET_RC_KERNEL"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     yield c
     c.close()
 
