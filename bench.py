@@ -150,8 +150,7 @@ def main():
     t_dom = t_dec if dom_is_dec else t_comp
     alg = alg_d if dom_is_dec else alg_c
     achieved = alg / t_dom / 1e9
-    kname = ("rc_decompress_" if dom_is_dec else "rc_compress_") + {"lane2": "lane", "wave": "wave"}.get(
-        os.environ.get("ENET_RC_KERNEL", ""), "lane3")
+    kname = dominant_kernel(dom_is_dec)
     traffic, tsrc = measured_traffic(kname, args.workload, n)
     roofline = {
         "kernel": kname,
@@ -466,6 +465,17 @@ def rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank)
             "packets": n * world,
             "note": "rank0 scatters world x shard over RCCL (xGMI), ranks compress, results gathered to rank0; "
                     "separate from the timed region of value"}
+
+
+def dominant_kernel(decompress):
+    """The kernel that does a direction's work in the library's configuration
+    (rc_host.c reads the same environment when a context is created)."""
+    kern = os.environ.get("ENET_RC_KERNEL", "lane3")
+    if kern in ("lane2", "wave"):
+        return ("rc_decompress_" if decompress else "rc_compress_") + {"lane2": "lane", "wave": "wave"}[kern]
+    if decompress:
+        return "rc_decompress_dec4" if os.environ.get("ENET_RC_DEC4", "1") != "0" else "rc_decompress_lane3"
+    return "rc_enc2_code" if os.environ.get("ENET_RC_ENC2", "1") != "0" else "rc_compress_lane3"
 
 
 def measured_traffic(kernel, workload, packets):

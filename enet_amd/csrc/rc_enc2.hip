@@ -89,6 +89,7 @@ struct E2Params {
     uint32_t*       list;       // packets for the lane kernels
     uint32_t*       count;
     uint32_t        act;        // pass 2: packets per wavefront (64 or 32)
+    uint8_t*        dummy;      // pass 2: 1 MB, 16 B per lane, the target of stores with nothing to store
 };
 
 DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
@@ -171,7 +172,7 @@ DEV uint2 make_record(uint32_t acc2, uint32_t acc1, bool f2, bool f1, uint32_t v
 
 // exceptional position j of bucket [bs, ...): statistics over all its
 // predecessors [bs, j) (their flags are final), its flags, its record
-__device__ __attribute__((noinline)) uint32_t scan_exceptional(ScanLds& s, uint32_t bs, uint32_t j, uint32_t w,
+DEV uint32_t scan_exceptional(ScanLds& s, uint32_t bs, uint32_t j, uint32_t w,
                                                                uint2* rec)
 {
     const uint32_t pos = w & 2047, v = (w >> 11) & 255;
@@ -313,6 +314,15 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         E2P(2)
         if (t < 16) *reinterpret_cast<uint4*>(&s.excb[16 * t]) = z;
         __syncthreads();
+        // Scatter into buckets, and each position's record as in a bucket with
+        // no exceptional position: t1 = dist1 = its rank j in the bucket (the
+        // walk below rewrites the buckets that have one).  The rank is the
+        // slot from the LDS atomic, i.e. position order when same-address
+        // atomics of one instruction apply in lane order (gfx950 does,
+        // tools/atomorder.hip); each position checks its predecessor in the
+        // bucket, and any disorder sends the packet down the sorting walk.
+        uint2* rec = reinterpret_cast<uint2*>(slot);
+        bool disorder = false;
         for (uint32_t i = 1 + t; i < n; i += 2 * kScanThreads) {
             uint32_t w[2], k[2], bb[2];
 #pragma unroll
@@ -332,13 +342,22 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 #pragma unroll
             for (uint32_t m = 0; m < 2; ++m) k[m] = bb[m] != 0xFFFFFFFFu ? atomicAdd(&s.cnt[bb[m]], 1u) : 0u;
 #pragma unroll
+            for (uint32_t m = 0; m < 2; ++m) {
+                if (bb[m] != 0xFFFFFFFFu) {
+                    s.e[k[m]] = w[m];
+                    const uint32_t j = k[m] - s.start[bb[m]];
+                    rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
+                }
+            }
+            __syncthreads();
+#pragma unroll
             for (uint32_t m = 0; m < 2; ++m)
-                if (bb[m] != 0xFFFFFFFFu) s.e[k[m]] = w[m];
+                if (bb[m] != 0xFFFFFFFFu && k[m] != s.start[bb[m]])
+                    disorder = disorder || (s.e[k[m] - 1] & 2047) > (w[m] & 2047);
         }
         const uint32_t x0 = x[0];
-        __syncthreads();
+        disorder = __syncthreads_or(disorder);
         E2P(3)
-        uint2* rec = reinterpret_cast<uint2*>(slot);
         // buckets with exceptional positions: compacted over the lanes, one
         // per lane, each walked in full
         {
@@ -365,32 +384,18 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             }
         }
         E2P(4)
-        // every other bucket: its positions in order, t1 = dist1 = j
+        if (rare_lane(disorder)) {                    // (not seen on gfx950) the plain buckets sorted and rewritten
         __syncthreads();
 #pragma unroll 1
         for (uint32_t r = 0; r < 4; ++r) {
             const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
             if (s.excb[4 * t + r]) continue;
-            uint32_t prev = 0;
-            bool sorted = true;
-            uint4 u = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll 1
+            sort_bucket(s, bs, bs + kk);
             for (uint32_t j = 0; j < kk; ++j) {
-                if ((j & 3) == 0) u = *reinterpret_cast<const uint4*>(&s.e[bs + j]);
-                const uint32_t w = pick4(j & 3, u);
-                sorted = sorted && (w & 2047) > prev;
-                prev = w & 2047;
+                const uint32_t w = s.e[bs + j];
                 rec[w & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w >> 11) & 255) << 24);
             }
-            if (rare_lane(!sorted)) {                 // (not seen on gfx950) sort, write again
-                if (!sorted) {
-                    sort_bucket(s, bs, bs + kk);
-                    for (uint32_t j = 0; j < kk; ++j) {
-                        const uint32_t w = s.e[bs + j];
-                        rec[w & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w >> 11) & 255) << 24);
-                    }
-                }
-            }
+        }
         }
         if (t == 0) rec[0] = make_uint2(0u, x0 << 24);  // position 0: root only
         __syncthreads();                              // LDS reuse by the next packet
@@ -564,6 +569,10 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     uint4 c0 = gload16(base);
     if (c0.x >= kSkipDone) return;                    // lane kernels / empty
     uint4 c1 = gload16(base + 16), c2 = gload16(base + 32);
+    // (a wavefront's dummies are 1 KB contiguous: every store is one coalesced
+    // 1-KB write to lines that stay in L2; a dummy per lane in its own line
+    // was written back to HBM every ~7 steps, 0.7 GB per C2 launch)
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(e.dummy) + ((blockIdx.x * 256u + threadIdx.x) & 65535u) * 16u;
     const uint32_t pkt = packet_of(e, idx);
     const uint32_t len = b.in_len[pkt];
     uint8_t* root = smem + threadIdx.x * kCodeLds;
@@ -573,7 +582,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     o.n = 0;
     o.cap = b.out_cap[pkt];
     o.ch = make_uint4(0u, 0u, 0u, 0u);
-    o.ca = base;
+    o.ca = dummy;
     CodeState k;
     root3_clear<true>(root, k.R);
     k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
@@ -585,18 +594,18 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     // iteration that issued it, i.e. wait for it.)
     uintptr_t a = base + 48;
     for (uint32_t i = 0; any_lane(i < len && k.ok); i += 6, a += 48) {
-        code_step(k, o, root, mtab, c0.x, c0.y, i < len, base);
-        code_step(k, o, root, mtab, c0.z, c0.w, i + 1 < len, base);
+        code_step(k, o, root, mtab, c0.x, c0.y, i < len, dummy);
+        code_step(k, o, root, mtab, c0.z, c0.w, i + 1 < len, dummy);
         c0 = gload16(a);
-        code_step(k, o, root, mtab, c1.x, c1.y, i + 2 < len, base);
-        code_step(k, o, root, mtab, c1.z, c1.w, i + 3 < len, base);
+        code_step(k, o, root, mtab, c1.x, c1.y, i + 2 < len, dummy);
+        code_step(k, o, root, mtab, c1.z, c1.w, i + 3 < len, dummy);
         c1 = gload16(a + 16);
-        code_step(k, o, root, mtab, c2.x, c2.y, i + 4 < len, base);
-        code_step(k, o, root, mtab, c2.z, c2.w, i + 5 < len, base);
+        code_step(k, o, root, mtab, c2.x, c2.y, i + 4 < len, dummy);
+        code_step(k, o, root, mtab, c2.z, c2.w, i + 5 < len, dummy);
         c2 = gload16(a + 32);
     }
     ring_store(o);
-    ring_chunk(o, o.n, base);                         // (nothing new: the next store goes to the dummy)
+    ring_chunk(o, o.n, dummy);                        // (nothing new: the next store goes to the dummy)
     // flush, compress.c:139-146
     bool ok = k.ok;
     uint32_t low = k.low;
@@ -607,7 +616,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
         const uint32_t n0 = o.n;
         ring_put(o, low, 1, more && !full);
         low = (more && !full) ? low << 8 : low;
-        ring_chunk(o, n0, base);
+        ring_chunk(o, n0, dummy);
         ring_store(o);
     }
     ring_finish(o, ok);
@@ -647,6 +656,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     E2Params e;
     e.stream = static_cast<uint8_t*>(ws->enc2_stream);
     e.slot_bytes = slot;
+    e.dummy = static_cast<uint8_t*>(ws->enc2_stream) + ws->enc2_cap;   // (allocated past the stream)
     e.order = ws->order;
     e.bins = ws->bins;
     e.list = ws->enc2_list;

@@ -126,7 +126,8 @@ static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     hipDeviceSynchronize();
     if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
     c->ws.enc2_stream = NULL; c->ws.enc2_cap = 0;
-    if (hipMalloc(&c->ws.enc2_stream, want) != hipSuccess) return -1;
+    /* + 1 MB past the stream: the code pass's dummy store targets (rc_enc2.hip) */
+    if (hipMalloc(&c->ws.enc2_stream, want + (1u << 20)) != hipSuccess) return -1;
     c->ws.enc2_cap = want;
     return 0;
 }
