@@ -107,7 +107,8 @@ struct ScanLds {
         uint32_t seen[2048];          // bigrams (x[i-1], x[i]) seen, 64 Ki bits
         uint32_t e[2048 + 768];       // elements in bucket order (below), buckets 4-aligned
     };
-    uint32_t rep[32];                 // 1 Ki-bit filter of the bigrams seen twice (hashed)
+    uint32_t repat[64];               // position i's bigram (x[i-1], x[i]) occurred before i (2048 bits)
+    uint32_t probe;                   // lane-order probe (rc_enc2_scan)
     uint8_t  excb[256];               // bucket holds an exceptional position
     uint8_t  xlist[256];              // those buckets
 };
@@ -134,7 +135,7 @@ DEV void fallback(const E2Params& e, uint32_t* slot, uint32_t pkt)
     e.list[atomicAdd(e.count, 1u)] = pkt;
 }
 
-DEV uint32_t rep_hash(uint32_t bigram) { return (bigram * 0x9E3779B1u) >> 22; }   // 10 bits
+DEV bool bit_at(const uint32_t* m, uint32_t i) { return (m[i >> 5] >> (i & 31)) & 1; }
 
 // one predecessor u of an element (v, akey): SWAR accumulators
 // t | same << 8 | less << 16 | dist << 24 of order 2 and order 1
@@ -246,6 +247,12 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
     __shared__ __attribute__((aligned(16))) ScanLds s;
     const uint32_t t = threadIdx.x;
     E2P_DECL
+    // Do same-address LDS atomics of one instruction apply in lane order (as
+    // on gfx950, tools/atomorder.hip)?  The repeat bits and bucket ranks below
+    // rely on it; without it every position takes the full statistics.
+    if (t == 0) s.probe = 0;
+    __syncthreads();
+    const bool ordered = __syncthreads_and(atomicAdd(&s.probe, 1u) == t);
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const uint32_t pkt = packet_of(e, idx);
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
@@ -266,13 +273,15 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             *reinterpret_cast<uint4*>(s.x + 16 * c) = gload16(a16 + 16 * c);
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = z;
-        if (t < 8) *reinterpret_cast<uint4*>(&s.rep[4 * t]) = z;
+        if (t < 16) *reinterpret_cast<uint4*>(&s.repat[4 * t]) = z;
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(&s.seen[4 * (t + 64 * k)]) = z;
         __syncthreads();
         E2P(0)
         const uint8_t* x = s.x + mis;
-        // bucket sizes, and the bigrams that occur twice
+        // bucket sizes, and the positions whose bigram occurred before (the
+        // old bit of the seen set: position order, when same-address
+        // atomics of one instruction apply in lane order -- `ordered`)
         for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
             uint32_t key[4], old[4];
 #pragma unroll
@@ -291,8 +300,8 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m)
                 if (key[m] != 0xFFFFFFFFu && (old[m] & (1u << (key[m] & 31)))) {
-                    const uint32_t h = rep_hash(key[m]);
-                    atomicOr(&s.rep[h >> 5], 1u << (h & 31));
+                    const uint32_t ii = i + m * kScanThreads;
+                    atomicOr(&s.repat[ii >> 5], 1u << (ii & 31));
                 }
         }
         __syncthreads();
@@ -331,9 +340,11 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                 bb[m] = 0xFFFFFFFFu;
                 if (ii < n) {
                     const uint32_t p = x[ii - 1], v = x[ii], a = ii >= 2 ? x[ii - 2] : 0u;
-                    const uint32_t h1 = rep_hash(p << 8 | v), h2 = rep_hash(a << 8 | p);
-                    const bool exc = ((s.rep[h1 >> 5] >> (h1 & 31)) & 1) ||
-                                     (ii >= 2 && ((s.rep[h2 >> 5] >> (h2 & 31)) & 1));
+                    // full statistics where v may already be in the order-1
+                    // context (its bigram occurred before) or the order-2
+                    // context exists (the bigram before it occurred before);
+                    // every other position is plain (see walk_full)
+                    const bool exc = !ordered || bit_at(s.repat, ii) || (ii >= 2 && bit_at(s.repat, ii - 1));
                     w[m] = ii | v << 11 | (ii >= 2 ? (a | 256u) << 19 : 0u) | (exc ? kExc : 0u);
                     bb[m] = p;
                     if (exc) s.excb[p] = 1;
