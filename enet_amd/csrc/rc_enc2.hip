@@ -137,6 +137,16 @@ DEV void fallback(const E2Params& e, uint32_t* slot, uint32_t pkt)
 
 DEV bool bit_at(const uint32_t* m, uint32_t i) { return (m[i >> 5] >> (i & 31)) & 1; }
 
+// The scan's workgroup is one wavefront, and LDS operations of a wavefront
+// complete in order: lanes see each other's LDS writes without a workgroup
+// barrier.  This only keeps the compiler from moving memory operations
+// across the point.
+DEV void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // one predecessor u of an element (v, akey): SWAR accumulators
 // t | same << 8 | less << 16 | dist << 24 of order 2 and order 1
 DEV void pair(uint32_t u, uint32_t v, uint32_t akey, bool in, uint32_t& acc2, uint32_t& acc1)
@@ -251,8 +261,8 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
     // on gfx950, tools/atomorder.hip)?  The repeat bits and bucket ranks below
     // rely on it; without it every position takes the full statistics.
     if (t == 0) s.probe = 0;
-    __syncthreads();
-    const bool ordered = __syncthreads_and(atomicAdd(&s.probe, 1u) == t);
+    wave_sync();
+    const bool ordered = !any_lane(atomicAdd(&s.probe, 1u) != t);
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const uint32_t pkt = packet_of(e, idx);
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
@@ -276,7 +286,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         if (t < 16) *reinterpret_cast<uint4*>(&s.repat[4 * t]) = z;
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(&s.seen[4 * (t + 64 * k)]) = z;
-        __syncthreads();
+        wave_sync();
         E2P(0)
         const uint8_t* x = s.x + mis;
         // bucket sizes, and the positions whose bigram occurred before (the
@@ -304,12 +314,12 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                     atomicOr(&s.repat[ii >> 5], 1u << (ii & 31));
                 }
         }
-        __syncthreads();
+        wave_sync();
         E2P(1)
         // lane t owns buckets 4t .. 4t+3: sizes, 4-aligned starts
         const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
         const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
-        if (__syncthreads_or(mx > kE2Bucket)) {
+        if (any_lane(mx > kE2Bucket)) {
             if (t == 0) fallback(e, slot, pkt);
             continue;
         }
@@ -319,10 +329,10 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint4 s4 = make_uint4(st, st + a0, st + a0 + a1, st + a0 + a1 + a2);
         *reinterpret_cast<uint4*>(&s.start[4 * t]) = s4;
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
-        __syncthreads();
+        wave_sync();
         E2P(2)
         if (t < 16) *reinterpret_cast<uint4*>(&s.excb[16 * t]) = z;
-        __syncthreads();
+        wave_sync();
         // Scatter into buckets, and each position's record as in a bucket with
         // no exceptional position: t1 = dist1 = its rank j in the bucket (the
         // walk below rewrites the buckets that have one).  The rank is the
@@ -332,10 +342,10 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         // bucket, and any disorder sends the packet down the sorting walk.
         uint2* rec = reinterpret_cast<uint2*>(slot);
         bool disorder = false;
-        for (uint32_t i = 1 + t; i < n; i += 2 * kScanThreads) {
-            uint32_t w[2], k[2], bb[2];
+        for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
+            uint32_t w[4], k[4], bb[4];
 #pragma unroll
-            for (uint32_t m = 0; m < 2; ++m) {
+            for (uint32_t m = 0; m < 4; ++m) {
                 const uint32_t ii = i + m * kScanThreads;
                 bb[m] = 0xFFFFFFFFu;
                 if (ii < n) {
@@ -351,23 +361,23 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                 }
             }
 #pragma unroll
-            for (uint32_t m = 0; m < 2; ++m) k[m] = bb[m] != 0xFFFFFFFFu ? atomicAdd(&s.cnt[bb[m]], 1u) : 0u;
+            for (uint32_t m = 0; m < 4; ++m) k[m] = bb[m] != 0xFFFFFFFFu ? atomicAdd(&s.cnt[bb[m]], 1u) : 0u;
 #pragma unroll
-            for (uint32_t m = 0; m < 2; ++m) {
+            for (uint32_t m = 0; m < 4; ++m) {
                 if (bb[m] != 0xFFFFFFFFu) {
                     s.e[k[m]] = w[m];
                     const uint32_t j = k[m] - s.start[bb[m]];
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
                 }
             }
-            __syncthreads();
+            wave_sync();
 #pragma unroll
-            for (uint32_t m = 0; m < 2; ++m)
+            for (uint32_t m = 0; m < 4; ++m)
                 if (bb[m] != 0xFFFFFFFFu && k[m] != s.start[bb[m]])
                     disorder = disorder || (s.e[k[m] - 1] & 2047) > (w[m] & 2047);
         }
         const uint32_t x0 = x[0];
-        disorder = __syncthreads_or(disorder);
+        disorder = any_lane(disorder);
         E2P(3)
         // buckets with exceptional positions: compacted over the lanes, one
         // per lane, each walked in full
@@ -382,7 +392,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             if (m2) s.xlist[o++] = static_cast<uint8_t>(4 * t + 2);
             if (m3) s.xlist[o++] = static_cast<uint8_t>(4 * t + 3);
             const uint32_t nx = __shfl(incl, 63, 64);
-            __syncthreads();
+            wave_sync();
 #pragma unroll 1
             for (uint32_t q = t; q < nx; q += kScanThreads) {
                 const uint32_t bk = s.xlist[q];
@@ -396,7 +406,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         }
         E2P(4)
         if (rare_lane(disorder)) {                    // (not seen on gfx950) the plain buckets sorted and rewritten
-        __syncthreads();
+        wave_sync();
 #pragma unroll 1
         for (uint32_t r = 0; r < 4; ++r) {
             const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
@@ -409,7 +419,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         }
         }
         if (t == 0) rec[0] = make_uint2(0u, x0 << 24);  // position 0: root only
-        __syncthreads();                              // LDS reuse by the next packet
+        wave_sync();                              // LDS reuse by the next packet
         E2P(5)
     }
     E2P_FLUSH
