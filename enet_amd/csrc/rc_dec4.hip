@@ -292,13 +292,20 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     uint32_t order = 0, a = 0, p = 0, nodes = 1;
     bool fail = false, off = false;
 
+    PROF_DECL
     for (;;) {
+#ifdef RC_PROFILE_DRAIN
+        __builtin_amdgcn_s_waitcnt(0);
+        PROF(9)
+#endif
         if (!fwd) bk_from(rw, epoch, B);
         sink_flush(o);
         src_fill(in, true);
+        PROF(0)
         const uint32_t nd = live_dwords(bk_k(B.h));
         Groups s;
         bk_groups(B, nd, a, order >= 2, s);
+        PROF(1)
         int at = -1;
         uint32_t v = 0;
         bool new0 = false;
@@ -312,6 +319,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (sub_decode(B, s.g1, s.t1, s.d1, low, code, range, in, v, fail)) at = 1;
             if (fail) break;
         }
+        PROF(2)
         // root, compress.c:570-596
         if (at < 0) {
             const uint32_t cd = dec_read(range, low, code, rtot, true);
@@ -330,6 +338,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // load issued now so that its latency overlaps the rest of the step.
         // The step's memory operations are unconditional (the scratch record
         // for lanes that need none; see rc_lane3.hip lane_prefetch).
+        PROF(3)
         const bool nfwd = order >= 1 && v == p;
         raw4_load(reg, nfwd ? kDummyRec : kO1Base + v * kRec4, rw);
         fail = o.n >= o.cap;                                         // compress.c:617
@@ -341,21 +350,25 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         const bool n2 = order >= 2 && (s.g2 & eqr) == 0;
         const bool n1 = order >= 1 && at != 2 && (s.g1 & eqr) == 0;
         nodes += (new0 ? 1u : 0u) + (n2 ? 1u : 0u) + (n1 ? 1u : 0u);
+        PROF(4)
         const bool full = order >= 1 && bk_k(B.h) >= kCap4;
         const uint32_t first = order == 1 ? 1u : 0u;                 // position 1: hit and new
         bk_insert(B, nd, le, a, v, (at == 2 ? 1u : 0u) | first, (n2 ? 1u : 0u) | first, lt == le ? 1u : 0u,
                   (1u << 16) + (at == 2 ? (1u << 21) : 0u) + (n1 ? (1u << 26) : 0u), order >= 1 && !full);
         // (the step's last memory operation)
         bk_store(reg, order >= 1 ? kO1Base + p * kRec4 : kDummyRec, B);
+        PROF(5)
         off = full || nodes >= kNodeLimit4 || *wbail >= kWaveBail;
         if (fail || off) break;
         sink_put(o, v, 1, true);
         src_adv(in);
+        PROF(6)
         fwd = nfwd ? 1u : 0u;
         a = p;
         p = v;
         order += order < 2 ? 1u : 0u;
     }
+    PROF_FLUSH(16)
     if (off && !fail) { atomicAdd(wbail, 1u); bail(ws, pkt); return; }
     sink_finish(o, !fail);
     bt.out_len[pkt] = fail ? 0u : o.n;
@@ -364,6 +377,9 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
 }  // namespace
 
 #ifndef RC_LANE_HOST_TEST
+// per lane in LDS: the root counts, pad (68 dwords: b128 conflict-free)
+constexpr uint32_t kDec4Lds = kRootStrideDec;
+
 // one wave per SIMD by design (a packet per lane, 65536 lanes fill the chip)
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void rc_decompress_dec4(rc_batch_dev b, rc_workspace_dev ws)
@@ -373,8 +389,8 @@ void rc_decompress_dec4(rc_batch_dev b, rc_workspace_dev ws)
     const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (l >= act) return;
     const uint32_t local = wave * act + l;
-    uint8_t* root = smem + local * kRootStrideDec;
-    uint32_t* wbail = reinterpret_cast<uint32_t*>(smem + 4 * act * kRootStrideDec) + wave;
+    uint8_t* root = smem + local * kDec4Lds;
+    uint32_t* wbail = reinterpret_cast<uint32_t*>(smem + 4 * act * kDec4Lds) + wave;
     if (l == 0) *wbail = 0u;
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
@@ -391,7 +407,7 @@ void rc_decompress_dec4(rc_batch_dev b, rc_workspace_dev ws)
 extern "C" int rc_hip_dec4_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kRootStrideDec + 16;   // + wbail[4]
+    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kDec4Lds + 16;   // + wbail[4]
     hipLaunchKernelGGL(rc_decompress_dec4, dim3(blocks), dim3(256), lds, st, *b, *ws);
     return static_cast<int>(hipGetLastError());
 }

@@ -24,6 +24,7 @@ inline uint32_t host_sad_u8(uint32_t a, uint32_t b, uint32_t acc)
 using std::min;
 using std::max;
 inline uint32_t atomicAdd(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
+inline uint32_t atomicOr(uint32_t* p, uint32_t v) { uint32_t o = *p; *p |= v; return o; }
 
 inline uint32_t host_udot4(uint32_t a, uint32_t b, uint32_t c, bool)
 {
