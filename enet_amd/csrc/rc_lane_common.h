@@ -680,6 +680,13 @@ DEV uint32_t dec_read(uint32_t& range, uint32_t low, uint32_t code, uint32_t tot
     return udiv_lo16(code - low, en ? r : 1u);
 }
 
+// dec_read with the reciprocal of total at hand (rc_udiv.h udiv16r)
+DEV uint32_t dec_read_r(uint32_t& range, uint32_t low, uint32_t code, uint32_t total, float rtotal)
+{
+    range = udiv16r(range, total, rtotal);
+    return udiv_lo16(code - low, range);
+}
+
 // compress.c:354-371 where `en`
 DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count,
                   ByteSrc& in, bool en)

@@ -82,13 +82,17 @@ DEV void root3_add(uint8_t* r, Root& R, uint32_t v, uint32_t cnt)
 DEV uint32_t root3_search(const uint8_t* r, const Root& R, uint32_t code, uint32_t& under, uint32_t& cnt)
 {
     const uint32_t x1 = (code + 1) * 0x00010001u;
-    uint32_t acc = 0, pm = 0;
+    // (sums and maxima as trees, not chains: this is on the decoder's critical path)
+    uint32_t b[8], m[8];
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
-        const uint32_t b = pk_min(pk_subsat(x1, R.d[i]), 0x00010001u);   // 1 where D <= code
-        acc = pk_add(acc, b);
-        pm = pk_max(pm, pk_mul(R.d[i], b));
+        b[i] = pk_min(pk_subsat(x1, R.d[i]), 0x00010001u);             // 1 where D <= code
+        m[i] = pk_mul(R.d[i], b[i]);
     }
+    const uint32_t acc = pk_add(pk_add(pk_add(b[0], b[1]), pk_add(b[2], b[3])),
+                                pk_add(pk_add(b[4], b[5]), pk_add(b[6], b[7])));
+    const uint32_t pm = pk_max(pk_max(pk_max(m[0], m[1]), pk_max(m[2], m[3])),
+                               pk_max(pk_max(m[4], m[5]), pk_max(m[6], m[7])));
     const uint32_t g = (acc & 0xFFFF) + (acc >> 16);
     const uint32_t prev = max(pm & 0xFFFF, pm >> 16);                 // D[g - 1], 0 for g = 0
     const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);

@@ -39,6 +39,19 @@ __device__ __forceinline__ uint32_t udiv16(uint32_t a, uint32_t b)
     return q;
 }
 
+// udiv16 with the reciprocal of b already at hand (rb = rcp(float(b)),
+// computed off the dependency chain): the same two-step quotient.
+__device__ __forceinline__ uint32_t udiv16r(uint32_t a, uint32_t b, float rb)
+{
+    uint32_t q = static_cast<uint32_t>(static_cast<float>(a) * rb);
+    const int32_t r = static_cast<int32_t>(a - q * b);
+    q += static_cast<int32_t>(static_cast<float>(r) * rb);
+    const int32_t r2 = static_cast<int32_t>(a - q * b);
+    q += r2 < 0 ? 0xFFFFFFFFu : (r2 >= static_cast<int32_t>(b) ? 1u : 0u);
+    return q;
+}
+__device__ __forceinline__ float rcp16(uint32_t b) { return __builtin_amdgcn_rcpf(static_cast<float>(b)); }
+
 // floor(a / b) & 0xFFFF for any b >= 1 (the decoder's READ, compress.c:352):
 // single precision while the quotient is below 2^16 (every valid stream:
 // code - low < range), udiv otherwise.
@@ -55,5 +68,7 @@ __device__ __forceinline__ uint32_t udiv_lo16(uint32_t a, uint32_t b)
 #else
 inline uint32_t udiv(uint32_t a, uint32_t b) { return a / b; }
 inline uint32_t udiv16(uint32_t a, uint32_t b) { return a / b; }
+inline uint32_t udiv16r(uint32_t a, uint32_t b, float) { return a / b; }
+inline float rcp16(uint32_t b) { return 1.0f / static_cast<float>(b); }
 inline uint32_t udiv_lo16(uint32_t a, uint32_t b) { return (a / b) & 0xFFFF; }
 #endif
