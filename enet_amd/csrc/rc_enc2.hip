@@ -66,7 +66,15 @@ __device__ unsigned long long g_e2prof[16];
 #define E2P(k) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
                  e2p_acc[k] += t_ - e2p_t; e2p_t = t_; __builtin_amdgcn_sched_barrier(0); }
 #define E2P_FLUSH { if (threadIdx.x == 0) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_e2prof[k_], e2p_acc[k_]); }
+// the code pass: per-phase stamps of code_step, into g_e2prof[8..15]
+struct E2Prof { unsigned long long t, acc[8]; };
+#define E2Q(k) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+                 pf.acc[k] += t_ - pf.t; pf.t = t_; __builtin_amdgcn_sched_barrier(0); }
+#define E2Q_FLUSH { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_e2prof[8 + k_], pf.acc[k_]); }
 #else
+struct E2Prof {};
+#define E2Q(k)
+#define E2Q_FLUSH
 #define E2P_DECL
 #define E2P(k)
 #define E2P_FLUSH
@@ -489,20 +497,31 @@ DEV void ring_finish(Ring& o, bool en)
     }
 }
 
-// compress.c:121-137 where `en`; clears `ok` when the output is full
-DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total, Ring& o,
+// compress.c:121-137 where `en`; clears `ok` when the output is full.
+// rt = rcp(float(total)), computed off the dependency chain; GUARD: skip the
+// code when no lane of the wave has one (the order-1 code after an order-2
+// escape; the others run on nearly every step).
+template <bool GUARD>
+DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total, float rt, Ring& o,
               bool en, bool& ok)
 {
     en = en && ok;
-    if (!any_lane(en)) return;
-    const uint32_t r = udiv16(range, en ? total : 1u);
+    if (GUARD && !any_lane(en)) return;
+    const uint32_t r = udiv16r(range, en ? total : 1u, en ? rt : 1.0f);
     low = en ? low + under * r : low;
     range = en ? r * count : range;
     const uint32_t k = en ? settled_bytes(low, range) : 0u;
     const bool full = o.n + k > o.cap;
     ok = ok && !full;
     const bool put = en && !full;
-    ring_put(o, low, k, put);
+    // (the three byte writes unconditional: bytes past the count are rewritten
+    // before their chunk completes, and a lane without a code writes its
+    // current position's bytes, which the same holds for)
+    const uint32_t p = static_cast<uint32_t>(o.lo) + o.n;
+    o.r[p & 31] = static_cast<uint8_t>(low >> 24);
+    o.r[(p + 1) & 31] = static_cast<uint8_t>(low >> 16);
+    o.r[(p + 2) & 31] = static_cast<uint8_t>(low >> 8);
+    o.n += put ? k : 0u;
     low = put ? low << (8 * k) : low;
     range = put ? range << (8 * k) : range;
     bool more = put && range < kBot;
@@ -533,14 +552,16 @@ DEV void sub_interval(uint32_t t, uint32_t d, uint32_t same, uint32_t less, bool
 
 struct CodeState {
     uint32_t low, range, rtot;
+    float rrt;                  // rcp(rtot)
     bool ok;
     Root R;                     // the root's group boundaries (rc_root3.h)
 };
 
 // one position: its sub-context codes, then the root (compress.c:286-337)
 DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, uint32_t w0, uint32_t w1, bool en,
-                   uintptr_t dummy)
+                   uintptr_t dummy, E2Prof& pf)
 {
+    E2Q(0)
     en = en && k.ok;
     const uint32_t n0 = o.n;
     const uint32_t typ = w0 & 7, ext = w0 >> 16, v = w1 >> 24;
@@ -548,23 +569,32 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, ui
     // overlaps the sub-context codes
     uint32_t under0, cnt0;
     root3_lookup(root, mtab, v, under0, cnt0);
+    E2Q(1)
     // first sub-context code: order 2 (types 3-6) or order 1 (types 1, 2)
-    uint32_t un, ct, tt;
+    uint32_t un, ct, tt, un2, ct2, tt2;
     sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
-    code(k.low, k.range, un, ct, tt, o, en && typ != 0, k.ok);
     // order 1 after an order-2 escape (types 4, 5)
     const uint32_t fb = typ == 5 ? w1 : ext;
-    sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un, ct, tt);
-    code(k.low, k.range, un, ct, tt, o, en && (typ == 4 || typ == 5), k.ok);
+    sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un2, ct2, tt2);
+    // (the totals' reciprocals ahead of the chain through low and range)
+    const float rt = rcp16(max(tt, 1u)), rt2 = rcp16(max(tt2, 1u));
+    code<false>(k.low, k.range, un, ct, tt, rt, o, en && typ != 0, k.ok);
+    E2Q(2)
+    code<true>(k.low, k.range, un2, ct2, tt2, rt2, o, en && (typ == 4 || typ == 5), k.ok);
+    E2Q(3)
     // root, compress.c:318-329
     const bool en0 = en && (typ <= 1 || typ == 3 || typ == 4);
     if (en0) root3_add<true>(root, k.R, v, cnt0);
-    code(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, o, en0, k.ok);
+    E2Q(4)
+    code<false>(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, k.rrt, o, en0, k.ok);
+    E2Q(5)
     k.rtot = en0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
     const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
     if (any_lane(rs0)) { if (rs0) k.rtot = root3_rescale<true>(root, k.R); }
+    k.rrt = rcp16(k.rtot);                            // (for the next root code)
     ring_store(o);                                    // the chunk read back a step ago
     ring_chunk(o, n0, dummy);
+    E2Q(6)
 }
 
 // Per lane: the root (counts, D copy) at 0, the ring at 288, pad to 336 B
@@ -607,7 +637,13 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     CodeState k;
     root3_clear<true>(root, k.R);
     k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
+    k.rrt = rcp16(k.rtot);
     __builtin_amdgcn_s_waitcnt(0);                    // settle the first chunks before the loop
+    E2Prof pf;
+#ifdef E2_PROF
+    pf.t = __builtin_amdgcn_s_memtime();
+    for (int k_ = 0; k_ < 8; ++k_) pf.acc[k_] = 0;
+#endif
     // Six positions per iteration from three chunk registers; each register
     // is reloaded right after its two positions are coded, with the chunk
     // three ahead, and is next read two register-steps later.  (Rotating one
@@ -615,16 +651,18 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     // iteration that issued it, i.e. wait for it.)
     uintptr_t a = base + 48;
     for (uint32_t i = 0; any_lane(i < len && k.ok); i += 6, a += 48) {
-        code_step(k, o, root, mtab, c0.x, c0.y, i < len, dummy);
-        code_step(k, o, root, mtab, c0.z, c0.w, i + 1 < len, dummy);
+        code_step(k, o, root, mtab, c0.x, c0.y, i < len, dummy, pf);
+        code_step(k, o, root, mtab, c0.z, c0.w, i + 1 < len, dummy, pf);
         c0 = gload16(a);
-        code_step(k, o, root, mtab, c1.x, c1.y, i + 2 < len, dummy);
-        code_step(k, o, root, mtab, c1.z, c1.w, i + 3 < len, dummy);
+        code_step(k, o, root, mtab, c1.x, c1.y, i + 2 < len, dummy, pf);
+        code_step(k, o, root, mtab, c1.z, c1.w, i + 3 < len, dummy, pf);
         c1 = gload16(a + 16);
-        code_step(k, o, root, mtab, c2.x, c2.y, i + 4 < len, dummy);
-        code_step(k, o, root, mtab, c2.z, c2.w, i + 5 < len, dummy);
+        code_step(k, o, root, mtab, c2.x, c2.y, i + 4 < len, dummy, pf);
+        code_step(k, o, root, mtab, c2.z, c2.w, i + 5 < len, dummy, pf);
         c2 = gload16(a + 32);
     }
+    E2Q(7)
+    E2Q_FLUSH
     ring_store(o);
     ring_chunk(o, o.n, dummy);                        // (nothing new: the next store goes to the dummy)
     // flush, compress.c:139-146

@@ -32,3 +32,11 @@ tot = sum(buf[k] for k in range(8))
 for k, nm in enumerate(names):
     print(f"{nm:14s} {buf[k] / n:10.0f} cycles/packet  {100.0 * buf[k] / max(tot, 1):5.1f} %")
 print(f"{'total':14s} {tot / n:10.0f} cycles/packet")
+# the code pass: cycles per wavefront-step (one position of each of the wave's 64 packets)
+cnames = ["loop/loads", "record+root lookup", "code 1 (sub)", "code 2 (o1 after o2)", "root add+update",
+          "code 3 (root)", "rescale chk+ring", "-"]
+steps = (n // 64) * 1200
+ctot = sum(buf[8 + k] for k in range(8))
+for k, nm in enumerate(cnames):
+    print(f"code {nm:22s} {buf[8 + k] / steps:8.0f} cycles/wave-step  {100.0 * buf[8 + k] / max(ctot, 1):5.1f} %")
+print(f"code {'total':22s} {ctot / steps:8.0f} cycles/wave-step")
