@@ -470,16 +470,19 @@ DEV void ring_store(Ring& o)
 }
 
 // after a step's codes: a chunk completed since n0 is read back for storing
+// (positions as the address's low 32 bits; one 64-bit add for the store)
 DEV void ring_chunk(Ring& o, uint32_t n0, uintptr_t dummy)
 {
-    const uintptr_t e0 = o.lo + n0, e1 = o.lo + o.n;
+    const uint32_t lo32 = static_cast<uint32_t>(o.lo);
+    const uint32_t e0 = lo32 + n0, e1 = lo32 + o.n;
     const bool done = (e0 >> 4) != (e1 >> 4);         // codes add <= 12 bytes: at most one chunk
-    const uintptr_t c = (e1 & ~static_cast<uintptr_t>(15)) - 16;
+    const uint32_t c = (e1 & ~15u) - 16u;
     o.ch = *reinterpret_cast<const uint4*>(o.r + (c & 31));
-    const bool edge = done && c < o.lo;               // the first chunk starts before the output
-    o.ca = (done && !edge) ? c : dummy;
+    const int32_t rel = static_cast<int32_t>(c - lo32);   // the chunk's start, from the output start
+    const bool edge = done && rel < 0;                // the first chunk starts before the output
+    o.ca = (done && !edge) ? o.lo + static_cast<intptr_t>(rel) : dummy;
     if (rare_lane(edge)) {
-        if (edge) sink_bytes(c, o.ch, 0, 16, o.lo);
+        if (edge) sink_bytes(o.lo + static_cast<intptr_t>(rel), o.ch, 0, 16, o.lo);
     }
 }
 
@@ -554,12 +557,11 @@ struct CodeState {
     uint32_t low, range, rtot;
     float rrt;                  // rcp(rtot)
     bool ok;
-    Root R;                     // the root's group boundaries (rc_root3.h)
 };
 
 // one position: its sub-context codes, then the root (compress.c:286-337)
-DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, uint32_t w0, uint32_t w1, bool en,
-                   uintptr_t dummy, E2Prof& pf)
+DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, const uint8_t* itab, uint32_t w0,
+                   uint32_t w1, bool en, uintptr_t dummy, E2Prof& pf)
 {
     E2Q(0)
     en = en && k.ok;
@@ -584,13 +586,15 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, ui
     E2Q(3)
     // root, compress.c:318-329
     const bool en0 = en && (typ <= 1 || typ == 3 || typ == 4);
-    if (en0) root3_add<true>(root, k.R, v, cnt0);
+    if (en0) root3_add_tab(root, itab, v, cnt0);
     E2Q(4)
     code<false>(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, k.rrt, o, en0, k.ok);
     E2Q(5)
     k.rtot = en0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
     const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
-    if (any_lane(rs0)) { if (rs0) k.rtot = root3_rescale<true>(root, k.R); }
+    if (any_lane(rs0)) {
+        if (rs0) { Root R; k.rtot = root3_rescale<true>(root, R); }
+    }
     k.rrt = rcp16(k.rtot);                            // (for the next root code)
     ring_store(o);                                    // the chunk read back a step ago
     ring_chunk(o, n0, dummy);
@@ -604,13 +608,16 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, ui
 constexpr uint32_t kRingAt = 288;
 constexpr uint32_t kCodeLds = 336;
 constexpr uint32_t kCodeMtab = 256 * kCodeLds;         // the block's prefix-mask table (rc_root3.h)
+constexpr uint32_t kCodeItab = kCodeMtab + 256;        // the block's D increment table
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void rc_enc2_code(rc_batch_dev b, E2Params e)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint8_t* mtab = smem + kCodeMtab;
+    const uint8_t* itab = smem + kCodeItab;
     if (threadIdx.x < 16) root3_mask_init(smem + kCodeMtab, threadIdx.x);
+    if (threadIdx.x < 16) root3_inc_init(smem + kCodeItab, threadIdx.x);
     __syncthreads();
     const uint32_t l = threadIdx.x & 63;
     if (l >= e.act) return;
@@ -635,7 +642,10 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     o.ch = make_uint4(0u, 0u, 0u, 0u);
     o.ca = dummy;
     CodeState k;
-    root3_clear<true>(root, k.R);
+    {
+        Root R;
+        root3_clear<true>(root, R);
+    }
     k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
     k.rrt = rcp16(k.rtot);
     __builtin_amdgcn_s_waitcnt(0);                    // settle the first chunks before the loop
@@ -651,14 +661,14 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     // iteration that issued it, i.e. wait for it.)
     uintptr_t a = base + 48;
     for (uint32_t i = 0; any_lane(i < len && k.ok); i += 6, a += 48) {
-        code_step(k, o, root, mtab, c0.x, c0.y, i < len, dummy, pf);
-        code_step(k, o, root, mtab, c0.z, c0.w, i + 1 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, c0.x, c0.y, i < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, c0.z, c0.w, i + 1 < len, dummy, pf);
         c0 = gload16(a);
-        code_step(k, o, root, mtab, c1.x, c1.y, i + 2 < len, dummy, pf);
-        code_step(k, o, root, mtab, c1.z, c1.w, i + 3 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, c1.x, c1.y, i + 2 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, c1.z, c1.w, i + 3 < len, dummy, pf);
         c1 = gload16(a + 16);
-        code_step(k, o, root, mtab, c2.x, c2.y, i + 4 < len, dummy, pf);
-        code_step(k, o, root, mtab, c2.z, c2.w, i + 5 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, c2.x, c2.y, i + 4 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, c2.z, c2.w, i + 5 < len, dummy, pf);
         c2 = gload16(a + 32);
     }
     E2Q(7)
@@ -730,7 +740,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         const uint32_t cnt = static_cast<uint32_t>(hi - lo);
         hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
                            0, st, *b, e);
-        hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 4 * e.act - 1) / (4 * e.act)), dim3(256), kCodeMtab + 256, st,
+        hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 4 * e.act - 1) / (4 * e.act)), dim3(256), kCodeItab + 512, st,
                            *b, e);
     }
     return static_cast<int>(hipGetLastError());

@@ -56,6 +56,33 @@ DEV void root3_clear(uint8_t* r, Root& R)
     root3_store_d<COPY>(r, R);
 }
 
+// Encoder: the block-wide table of D increments, entry g = +3 in every D[t]
+// with t >= g (packed like R.d), so that an update of the LDS copy of D is
+// two table reads and eight adds (no carry can cross a half: D <= 64256).
+DEV void root3_inc_init(uint8_t* tab, uint32_t g)
+{
+    uint32_t w[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i)
+        w[i] = (2 * i >= g ? kRootDelta : 0u) | ((2 * i + 1 >= g ? kRootDelta : 0u) << 16);
+    reinterpret_cast<uint4*>(tab)[2 * g] = make_uint4(w[0], w[1], w[2], w[3]);
+    reinterpret_cast<uint4*>(tab)[2 * g + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// encoder update: count[v] and the LDS copy of D (the registers R.d are not kept)
+DEV void root3_add_tab(uint8_t* r, const uint8_t* itab, uint32_t v, uint32_t cnt)
+{
+    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
+    const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (v >> 4));
+    uint4* dp = reinterpret_cast<uint4*>(r + kRootD);
+    uint4 d0 = dp[0], d1 = dp[1];
+    const uint4 i0 = ip[0], i1 = ip[1];
+    d0.x += i0.x; d0.y += i0.y; d0.z += i0.z; d0.w += i0.w;
+    d1.x += i1.x; d1.y += i1.y; d1.z += i1.z; d1.w += i1.w;
+    dp[0] = d0;
+    dp[1] = d1;
+}
+
 // under = cumulative frequency below v, cnt = count[v] (compress.c:159-199, minimum 1)
 DEV void root3_lookup(const uint8_t* r, const uint8_t* mtab, uint32_t v, uint32_t& under, uint32_t& cnt)
 {
