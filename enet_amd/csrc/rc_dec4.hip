@@ -199,11 +199,11 @@ DEV void bk_rank(const Bucket& B, uint32_t nd, uint32_t u, uint32_t& lt, uint32_
 // member the code selects (true; v, with its interval decoded).  fail: the
 // code is past the context's symbols (compress.c:416).  The members with the
 // selected value form the run of the run mask that holds it.
-DEV bool sub_decode(const Bucket& B, uint32_t g, uint32_t t, uint32_t dd, float rtot, uint32_t& low,
+DEV bool sub_decode(const Bucket& B, uint32_t g, uint32_t t, uint32_t dd, double rtot, uint32_t& low,
                     uint32_t& code, uint32_t& range, ByteSrc& in, uint32_t& v, bool& fail)
 {
     const uint32_t esc = kSubEscDelta * dd, tot = esc + kSubDelta * t;
-    const uint32_t cd = dec_read_r(range, low, code, tot, rtot);
+    const uint32_t cd = dec_read_d(range, low, code, tot, rtot);
     if (cd < esc) {
         dec_code(low, code, range, 0, esc, in, true);
         return false;
@@ -279,7 +279,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     Root R;
     root3_clear<false>(root, R);
     uint32_t rtot = 1 + 256;
-    float rrt = rcp16(rtot);
+    double rrt = rcp64(rtot);
     uint32_t low = 0, range = ~0u;
     uint32_t code = static_cast<uint32_t>(in.la >> 32);            // compress.c:344-350 (0 past the end)
     in.la <<= 32;
@@ -307,8 +307,8 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         Groups s;
         bk_groups(B, nd, a, order >= 2, s);
         // the totals' reciprocals, ahead of the READs that divide by them
-        const float rt2 = rcp16(max(kSubEscDelta * s.d2 + kSubDelta * s.t2, 1u));
-        const float rt1 = rcp16(max(kSubEscDelta * s.d1 + kSubDelta * s.t1, 1u));
+        const double rt2 = rcp64(max(kSubEscDelta * s.d2 + kSubDelta * s.t2, 1u));
+        const double rt1 = rcp64(max(kSubEscDelta * s.d1 + kSubDelta * s.t1, 1u));
         PROF(1)
         int at = -1;
         uint32_t v = 0;
@@ -326,7 +326,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         PROF(2)
         // root, compress.c:570-596
         if (at < 0) {
-            const uint32_t cd = dec_read_r(range, low, code, rtot, rrt);
+            const uint32_t cd = dec_read_d(range, low, code, rtot, rrt);
             if (cd < 1) { dec_code(low, code, range, 0, 1, in, true); break; }   // end of stream
             if (cd - 1 >= rtot - 1) { off = true; break; }                 // past symbol 255
             uint32_t under, cnt;
@@ -336,7 +336,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
             rtot = (rtot + kRootDelta) & 0xFFFF;
             if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
-            rrt = rcp16(rtot);                       // (for the next root READ)
+            rrt = rcp64(rtot);                       // (for the next root READ)
             at = 0;
         }
         // the next step's bucket: this one when v == p (updated below), else a

@@ -501,16 +501,16 @@ DEV void ring_finish(Ring& o, bool en)
 }
 
 // compress.c:121-137 where `en`; clears `ok` when the output is full.
-// rt = rcp(float(total)), computed off the dependency chain; GUARD: skip the
+// rt = rcp64(total), computed off the dependency chain; GUARD: skip the
 // code when no lane of the wave has one (the order-1 code after an order-2
 // escape; the others run on nearly every step).
 template <bool GUARD>
-DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total, float rt, Ring& o,
+DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total, double rt, Ring& o,
               bool en, bool& ok)
 {
     en = en && ok;
     if (GUARD && !any_lane(en)) return;
-    const uint32_t r = udiv16r(range, en ? total : 1u, en ? rt : 1.0f);
+    const uint32_t r = udiv16d(range, en ? total : 1u, en ? rt : 1.0);
     low = en ? low + under * r : low;
     range = en ? r * count : range;
     const uint32_t k = en ? settled_bytes(low, range) : 0u;
@@ -555,7 +555,7 @@ DEV void sub_interval(uint32_t t, uint32_t d, uint32_t same, uint32_t less, bool
 
 struct CodeState {
     uint32_t low, range, rtot;
-    float rrt;                  // rcp(rtot)
+    double rrt;                 // rcp64(rtot)
     bool ok;
 };
 
@@ -579,7 +579,7 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, co
     const uint32_t fb = typ == 5 ? w1 : ext;
     sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un2, ct2, tt2);
     // (the totals' reciprocals ahead of the chain through low and range)
-    const float rt = rcp16(max(tt, 1u)), rt2 = rcp16(max(tt2, 1u));
+    const double rt = rcp64(max(tt, 1u)), rt2 = rcp64(max(tt2, 1u));
     code<false>(k.low, k.range, un, ct, tt, rt, o, en && typ != 0, k.ok);
     E2Q(2)
     code<true>(k.low, k.range, un2, ct2, tt2, rt2, o, en && (typ == 4 || typ == 5), k.ok);
@@ -595,7 +595,7 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, co
     if (any_lane(rs0)) {
         if (rs0) { Root R; k.rtot = root3_rescale<true>(root, R); }
     }
-    k.rrt = rcp16(k.rtot);                            // (for the next root code)
+    k.rrt = rcp64(k.rtot);                            // (for the next root code)
     ring_store(o);                                    // the chunk read back a step ago
     ring_chunk(o, n0, dummy);
     E2Q(6)
@@ -647,7 +647,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
         root3_clear<true>(root, R);
     }
     k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
-    k.rrt = rcp16(k.rtot);
+    k.rrt = rcp64(k.rtot);
     __builtin_amdgcn_s_waitcnt(0);                    // settle the first chunks before the loop
     E2Prof pf;
 #ifdef E2_PROF

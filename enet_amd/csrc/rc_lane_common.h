@@ -687,6 +687,13 @@ DEV uint32_t dec_read_r(uint32_t& range, uint32_t low, uint32_t code, uint32_t t
     return udiv_lo16(code - low, range);
 }
 
+// dec_read with the double reciprocal of total at hand (rc_udiv.h udiv16d)
+DEV uint32_t dec_read_d(uint32_t& range, uint32_t low, uint32_t code, uint32_t total, double rtotal)
+{
+    range = udiv16d(range, total, rtotal);
+    return udiv_lo16(code - low, range);
+}
+
 // compress.c:354-371 where `en`
 DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count,
                   ByteSrc& in, bool en)

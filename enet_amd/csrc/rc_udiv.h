@@ -52,6 +52,29 @@ __device__ __forceinline__ uint32_t udiv16r(uint32_t a, uint32_t b, float rb)
 }
 __device__ __forceinline__ float rcp16(uint32_t b) { return __builtin_amdgcn_rcpf(static_cast<float>(b)); }
 
+// 1/b in double precision, relative error < 2^-52 (two Newton steps, as udiv)
+__device__ __forceinline__ double rcp64(uint32_t b)
+{
+    const double db = static_cast<double>(b);
+    double r = __builtin_amdgcn_rcp(db);
+    double e = __builtin_fma(-db, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-db, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// floor(a / b) for 1 <= b <= 65535 with rb = rcp64(b): three dependent
+// instructions (convert, fma, convert; ~20 cycles against ~90 for udiv16r,
+// tools/mb/chainlat.hip).  a * rb is within 2^32 * 2^-52 = 2^-20 of a/b, the
+// fma's rounding adds < 2^-21, so a/b + 2^-17 is computed within 2^-19: at
+// least the integer a/b when it is one, and below the next integer otherwise
+// (the fraction of a/b is then at most 1 - 1/b < 1 - 2^-17 - 2^-19 for b <
+// 104857).  Exact over every pair (tests/test_udiv.py, chainlat's sweep).
+__device__ __forceinline__ uint32_t udiv16d(uint32_t a, uint32_t, double rb)
+{
+    return static_cast<uint32_t>(__builtin_fma(static_cast<double>(a), rb, 0x1p-17));
+}
+
 // floor(a / b) & 0xFFFF for any b >= 1 (the decoder's READ, compress.c:352):
 // single precision while the quotient is below 2^16 (every valid stream:
 // code - low < range), udiv otherwise.
@@ -70,5 +93,7 @@ inline uint32_t udiv(uint32_t a, uint32_t b) { return a / b; }
 inline uint32_t udiv16(uint32_t a, uint32_t b) { return a / b; }
 inline uint32_t udiv16r(uint32_t a, uint32_t b, float) { return a / b; }
 inline float rcp16(uint32_t b) { return 1.0f / static_cast<float>(b); }
+inline double rcp64(uint32_t b) { return 1.0 / static_cast<double>(b); }
+inline uint32_t udiv16d(uint32_t a, uint32_t b, double) { return a / b; }
 inline uint32_t udiv_lo16(uint32_t a, uint32_t b) { return (a / b) & 0xFFFF; }
 #endif

@@ -31,6 +31,11 @@ extern "C" __global__ void udiv_check(uint64_t seed, uint32_t iters, unsigned lo
         const uint32_t q16 = a0 / b16;
         const uint32_t c16[4] = {a0, q16 * b16, q16 * b16 ? q16 * b16 - 1 : 0u, 0xFFFFFFFFu};
         for (int c = 0; c < 4; ++c) nbad += udiv16(c16[c], b16) != c16[c] / b16;
+        // udiv16d: the same divisors, the double-precision quotient
+        const double r16 = rcp64(b16);
+        for (int c = 0; c < 4; ++c) nbad += udiv16d(c16[c], b16, r16) != c16[c] / b16;
+        nbad += udiv16d(q16 * b16 + b16 - 1 >= q16 * b16 ? q16 * b16 + b16 - 1 : 0xFFFFFFFFu, b16, r16) !=
+                (q16 * b16 + b16 - 1 >= q16 * b16 ? q16 * b16 + b16 - 1 : 0xFFFFFFFFu) / b16;
         // udiv_lo16: any divisor, low 16 bits of the quotient
         for (int c = 0; c < 4; ++c) nbad += udiv_lo16(cases[c], b) != ((cases[c] / b) & 0xFFFF);
         // quotients just below 2^16 (a READ at the top of a context's range)
