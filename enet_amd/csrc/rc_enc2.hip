@@ -479,8 +479,9 @@ DEV void ring_chunk(Ring& o, uint32_t n0, uintptr_t dummy)
     const uint32_t c = (e1 & ~15u) - 16u;
     o.ch = *reinterpret_cast<const uint4*>(o.r + (c & 31));
     const int32_t rel = static_cast<int32_t>(c - lo32);   // the chunk's start, from the output start
-    const bool edge = done && rel < 0;                // the first chunk starts before the output
-    o.ca = (done && !edge) ? o.lo + static_cast<intptr_t>(rel) : dummy;
+    const bool fits = rel + 16 <= static_cast<int32_t>(o.cap);   // (only a failing packet has one that does not)
+    const bool edge = done && fits && rel < 0;        // the first chunk starts before the output
+    o.ca = (done && fits && rel >= 0) ? o.lo + static_cast<intptr_t>(rel) : dummy;
     if (rare_lane(edge)) {
         if (edge) sink_bytes(o.lo + static_cast<intptr_t>(rel), o.ch, 0, 16, o.lo);
     }
@@ -500,47 +501,46 @@ DEV void ring_finish(Ring& o, bool en)
     }
 }
 
-// compress.c:121-137 where `en`; clears `ok` when the output is full.
-// rt = rcp64(total), computed off the dependency chain; GUARD: skip the
-// code when no lane of the wave has one (the order-1 code after an order-2
-// escape; the others run on nearly every step).
-template <bool GUARD>
-DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, uint32_t total, double rt, Ring& o,
-              bool en, bool& ok)
+// the rest of compress.c:125-136 after the settled bytes: range < BOTTOM
+// (rare: one ballot on the common path)
+DEV void code_slow(uint32_t& low, uint32_t& range, Ring& o)
 {
-    en = en && ok;
-    if (GUARD && !any_lane(en)) return;
-    const uint32_t r = udiv16d(range, en ? total : 1u, en ? rt : 1.0);
-    low = en ? low + under * r : low;
-    range = en ? r * count : range;
-    const uint32_t k = en ? settled_bytes(low, range) : 0u;
-    const bool full = o.n + k > o.cap;
-    ok = ok && !full;
-    const bool put = en && !full;
-    // (the three byte writes unconditional: bytes past the count are rewritten
-    // before their chunk completes, and a lane without a code writes its
-    // current position's bytes, which the same holds for)
-    const uint32_t p = static_cast<uint32_t>(o.lo) + o.n;
-    o.r[p & 31] = static_cast<uint8_t>(low >> 24);
-    o.r[(p + 1) & 31] = static_cast<uint8_t>(low >> 16);
-    o.r[(p + 2) & 31] = static_cast<uint8_t>(low >> 8);
-    o.n += put ? k : 0u;
-    low = put ? low << (8 * k) : low;
-    range = put ? range << (8 * k) : range;
-    bool more = put && range < kBot;
-    while (rare_lane(more)) {
+    bool more = range < kBot;
+    while (any_lane(more)) {
         const bool carry = (low ^ (low + range)) >= kTop;
         const bool stop = carry && range >= kBot;
         more = more && !stop;
         if (!any_lane(more)) break;
         range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
-        const bool f = more && o.n >= o.cap;
-        ok = ok && !f;
-        more = more && !f;
         ring_put(o, low, 1, more);
         range = more ? range << 8 : range;
         low = more ? low << 8 : low;
     }
+}
+
+// compress.c:121-137, branch-free: rt = rcp64(total), prepared a step ahead.
+// A lane without this code passes (under, count, rt) = (0, 1, 1.0), which
+// leaves low and range as they are and settles no byte (a normalised coder
+// has no settled byte), so no lane needs a mask.  The output capacity is not
+// checked per code: compress.c returns 0 as soon as a byte does not fit
+// (compress.c:116-117), i.e. iff the whole output exceeds it, which the
+// caller checks at the end; chunks past the capacity are never stored.
+DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, double rt, Ring& o)
+{
+    const uint32_t r = udiv16d(range, 0u, rt);
+    low = low + under * r;
+    range = r * count;
+    const uint32_t k = settled_bytes(low, range);
+    // (three byte writes: bytes past the count are rewritten by the next code
+    // before their chunk completes)
+    const uint32_t p = static_cast<uint32_t>(o.lo) + o.n;
+    o.r[p & 31] = static_cast<uint8_t>(low >> 24);
+    o.r[(p + 1) & 31] = static_cast<uint8_t>(low >> 16);
+    o.r[(p + 2) & 31] = static_cast<uint8_t>(low >> 8);
+    o.n += k;
+    low <<= 8 * k;
+    range <<= 8 * k;
+    if (rare_lane(range < kBot)) code_slow(low, range, o);
 }
 
 // interval of a sub-context code from (t, dist[, same, less]): compress.c:301-308
@@ -553,51 +553,78 @@ DEV void sub_interval(uint32_t t, uint32_t d, uint32_t same, uint32_t less, bool
     count = hit ? 2 * same : esc;
 }
 
+// A position's sub-context codes, prepared from its record a step ahead (off
+// the chain through low and range): order 2 (types 3-6) or order 1 (types 1,
+// 2) first, then order 1 after an order-2 escape (types 4, 5); e0: the root
+// codes it (types 0, 1, 3, 4).
+struct Pre {
+    uint32_t u1, c1, u2, c2, v;
+    double r1, r2;
+    bool e2, e0;
+};
+
+DEV Pre prep(uint32_t w0, uint32_t w1, bool en)
+{
+    Pre p;
+    const uint32_t typ = w0 & 7, ext = w0 >> 16;
+    uint32_t un, ct, tt, un2, ct2, tt2;
+    sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
+    const uint32_t fb = typ == 5 ? w1 : ext;
+    sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un2, ct2, tt2);
+    const bool e1 = en && typ != 0;
+    p.e2 = en && (typ == 4 || typ == 5);
+    p.e0 = en && (typ <= 1 || typ == 3 || typ == 4);
+    p.u1 = e1 ? un : 0u;
+    p.c1 = e1 ? ct : 1u;
+    p.r1 = rcp64(e1 ? tt : 1u);
+    p.u2 = p.e2 ? un2 : 0u;
+    p.c2 = p.e2 ? ct2 : 1u;
+    p.r2 = rcp64(p.e2 ? tt2 : 1u);
+    p.v = w1 >> 24;
+    return p;
+}
+
 struct CodeState {
     uint32_t low, range, rtot;
     double rrt;                 // rcp64(rtot)
-    bool ok;
 };
 
-// one position: its sub-context codes, then the root (compress.c:286-337)
-DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, const uint8_t* itab, uint32_t w0,
-                   uint32_t w1, bool en, uintptr_t dummy, E2Prof& pf)
+// one position: its sub-context codes, then the root (compress.c:286-337);
+// p = this position's prepared codes, replaced by the next position's
+// (record words w0n, w1n)
+DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, const uint8_t* itab, Pre& p,
+                   uint32_t w0n, uint32_t w1n, bool enn, uintptr_t dummy, E2Prof& pf)
 {
     E2Q(0)
-    en = en && k.ok;
     const uint32_t n0 = o.n;
-    const uint32_t typ = w0 & 7, ext = w0 >> 16, v = w1 >> 24;
-    // the root lookup needs only v: three independent LDS reads whose latency
-    // overlaps the sub-context codes
+    // the root lookup needs only v: LDS reads whose latency overlaps the
+    // sub-context codes
     uint32_t under0, cnt0;
-    root3_lookup(root, mtab, v, under0, cnt0);
+    root3_lookup(root, mtab, p.v, under0, cnt0);
+    const RootAddPre ra = root3_add_read(root, itab, p.v);   // (the update's reads, early)
     E2Q(1)
-    // first sub-context code: order 2 (types 3-6) or order 1 (types 1, 2)
-    uint32_t un, ct, tt, un2, ct2, tt2;
-    sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
-    // order 1 after an order-2 escape (types 4, 5)
-    const uint32_t fb = typ == 5 ? w1 : ext;
-    sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un2, ct2, tt2);
-    // (the totals' reciprocals ahead of the chain through low and range)
-    const double rt = rcp64(max(tt, 1u)), rt2 = rcp64(max(tt2, 1u));
-    code<false>(k.low, k.range, un, ct, tt, rt, o, en && typ != 0, k.ok);
+    const Pre q = prep(w0n, w1n, enn);
+    const uint32_t rtot1 = p.e0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
+    double rrt1 = rcp64(rtot1);                       // (the next root code's, unless a rescale)
+    code(k.low, k.range, p.u1, p.c1, p.r1, o);
     E2Q(2)
-    code<true>(k.low, k.range, un2, ct2, tt2, rt2, o, en && (typ == 4 || typ == 5), k.ok);
+    if (any_lane(p.e2)) code(k.low, k.range, p.u2, p.c2, p.r2, o);
     E2Q(3)
-    // root, compress.c:318-329
-    const bool en0 = en && (typ <= 1 || typ == 3 || typ == 4);
-    if (en0) root3_add_tab(root, itab, v, cnt0);
     E2Q(4)
-    code<false>(k.low, k.range, 1 + under0, 1 + cnt0, k.rtot, k.rrt, o, en0, k.ok);
+    // root, compress.c:318-329
+    code(k.low, k.range, p.e0 ? 1 + under0 : 0u, p.e0 ? 1 + cnt0 : 1u, p.e0 ? k.rrt : 1.0, o);
+    if (p.e0) root3_add_write(root, p.v, cnt0, ra);
     E2Q(5)
-    k.rtot = en0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
-    const bool rs0 = en0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
+    k.rtot = rtot1;
+    const bool rs0 = p.e0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
     if (any_lane(rs0)) {
         if (rs0) { Root R; k.rtot = root3_rescale<true>(root, R); }
+        rrt1 = rcp64(k.rtot);
     }
-    k.rrt = rcp64(k.rtot);                            // (for the next root code)
+    k.rrt = rrt1;
     ring_store(o);                                    // the chunk read back a step ago
     ring_chunk(o, n0, dummy);
+    p = q;
     E2Q(6)
 }
 
@@ -646,7 +673,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
         Root R;
         root3_clear<true>(root, R);
     }
-    k.rtot = 1 + 256; k.low = 0; k.range = ~0u; k.ok = true;
+    k.rtot = 1 + 256; k.low = 0; k.range = ~0u;
     k.rrt = rcp64(k.rtot);
     __builtin_amdgcn_s_waitcnt(0);                    // settle the first chunks before the loop
     E2Prof pf;
@@ -655,20 +682,22 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     for (int k_ = 0; k_ < 8; ++k_) pf.acc[k_] = 0;
 #endif
     // Six positions per iteration from three chunk registers; each register
-    // is reloaded right after its two positions are coded, with the chunk
+    // is reloaded right after its two positions are prepared, with the chunk
     // three ahead, and is next read two register-steps later.  (Rotating one
     // set of registers instead would copy a load's result within the
-    // iteration that issued it, i.e. wait for it.)
+    // iteration that issued it, i.e. wait for it.)  Each step prepares the
+    // next position's codes.
+    Pre p = prep(c0.x, c0.y, 0 < len);
     uintptr_t a = base + 48;
-    for (uint32_t i = 0; any_lane(i < len && k.ok); i += 6, a += 48) {
-        code_step(k, o, root, mtab, itab, c0.x, c0.y, i < len, dummy, pf);
-        code_step(k, o, root, mtab, itab, c0.z, c0.w, i + 1 < len, dummy, pf);
+    for (uint32_t i = 0; any_lane(i < len && o.n <= o.cap); i += 6, a += 48) {
+        code_step(k, o, root, mtab, itab, p, c0.z, c0.w, i + 1 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, p, c1.x, c1.y, i + 2 < len, dummy, pf);
         c0 = gload16(a);
-        code_step(k, o, root, mtab, itab, c1.x, c1.y, i + 2 < len, dummy, pf);
-        code_step(k, o, root, mtab, itab, c1.z, c1.w, i + 3 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, p, c1.z, c1.w, i + 3 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, p, c2.x, c2.y, i + 4 < len, dummy, pf);
         c1 = gload16(a + 16);
-        code_step(k, o, root, mtab, itab, c2.x, c2.y, i + 4 < len, dummy, pf);
-        code_step(k, o, root, mtab, itab, c2.z, c2.w, i + 5 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, p, c2.z, c2.w, i + 5 < len, dummy, pf);
+        code_step(k, o, root, mtab, itab, p, c0.x, c0.y, i + 6 < len, dummy, pf);
         c2 = gload16(a + 32);
     }
     E2Q(7)
@@ -676,7 +705,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     ring_store(o);
     ring_chunk(o, o.n, dummy);                        // (nothing new: the next store goes to the dummy)
     // flush, compress.c:139-146
-    bool ok = k.ok;
+    bool ok = o.n <= o.cap;
     uint32_t low = k.low;
     while (any_lane(ok && low != 0)) {
         const bool more = ok && low != 0;

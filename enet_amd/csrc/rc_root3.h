@@ -83,6 +83,25 @@ DEV void root3_add_tab(uint8_t* r, const uint8_t* itab, uint32_t v, uint32_t cnt
     dp[1] = d1;
 }
 
+// root3_add_tab in two halves: the reads, issued early in a step, and the
+// writes, after the step's codes (no wait for the reads on the coder's chain)
+struct RootAddPre { uint4 d0, d1, i0, i1; };
+DEV RootAddPre root3_add_read(const uint8_t* r, const uint8_t* itab, uint32_t v)
+{
+    const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (v >> 4));
+    const uint4* dp = reinterpret_cast<const uint4*>(r + kRootD);
+    return RootAddPre{dp[0], dp[1], ip[0], ip[1]};
+}
+DEV void root3_add_write(uint8_t* r, uint32_t v, uint32_t cnt, RootAddPre a)
+{
+    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
+    uint4* dp = reinterpret_cast<uint4*>(r + kRootD);
+    a.d0.x += a.i0.x; a.d0.y += a.i0.y; a.d0.z += a.i0.z; a.d0.w += a.i0.w;
+    a.d1.x += a.i1.x; a.d1.y += a.i1.y; a.d1.z += a.i1.z; a.d1.w += a.i1.w;
+    dp[0] = a.d0;
+    dp[1] = a.d1;
+}
+
 // under = cumulative frequency below v, cnt = count[v] (compress.c:159-199, minimum 1)
 DEV void root3_lookup(const uint8_t* r, const uint8_t* mtab, uint32_t v, uint32_t& under, uint32_t& cnt)
 {

@@ -186,6 +186,39 @@ def test_protocol_out_limit_mode(coder):
         assert r == port.compress(p, out_limit=len(p))
 
 
+def test_no_write_past_out_cap(coder):
+    """A packet whose output does not fit returns 0 (compress.c:116-117) and
+    writes nothing past its capacity: every output slot is followed by a
+    64-B canary that must survive.  Caps below, at and just above what each
+    packet needs, misaligned slot starts."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(23)
+    pk = [synth.random_bytes(int(n), 40 + i).tobytes() for i, n in enumerate(rng.integers(1, 1500, 768))]
+    pk += [rng.integers(0, 7, size=int(n)).astype(np.uint8).tobytes() for n in rng.integers(1, 1500, 256)]
+    need = [port.compress(p, out_limit=2 * len(p) + 64)[0] for p in pk]
+    caps = [max(1, int(c + rng.integers(-20, 3))) for c in need]
+    d, o, l = _pack(pk)
+    caps = np.asarray(caps, np.int64)
+    gap = 64 + 3
+    out_off = np.zeros(len(caps), np.int64)
+    out_off[1:] = np.cumsum(caps[:-1] + gap)
+    total = int(out_off[-1] + caps[-1] + gap)
+    out = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    out_len = torch.zeros(len(caps), dtype=torch.int32, device="cuda")
+    coder.compress_batch(_dev(d, torch.uint8), _dev(o, torch.int64), _dev(l, torch.int32), out,
+                         _dev(out_off, torch.int64), _dev(caps, torch.int32), out_len, max_len=int(l.max()))
+    torch.cuda.synchronize()
+    ob, ol = out.cpu().numpy(), out_len.cpu().numpy()
+    for i, p in enumerate(pk):
+        e = port.compress(p, out_limit=int(caps[i]))
+        assert int(ol[i]) == e[0], i
+        if e[0]:
+            assert ob[out_off[i]: out_off[i] + e[0]].tobytes() == e[1], i
+        canary = ob[out_off[i] + caps[i]: out_off[i] + caps[i] + gap]
+        assert (canary == 0xA5).all(), (i, int(caps[i]), need[i])
+
+
 def test_long_packets_and_model_reset(coder):
     from oracle.pyoracle import Coder
     port = Coder("port")
