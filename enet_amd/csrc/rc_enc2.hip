@@ -543,6 +543,10 @@ DEV void code(uint32_t& low, uint32_t& range, uint32_t under, uint32_t count, do
     if (rare_lane(range < kBot)) code_slow(low, range, o);
 }
 
+// keeps a value's computation ahead of this point: the compiler otherwise
+// sinks it next to its use, where it stalls the in-order issue
+DEV void pin(double& x) { asm volatile("" : "+v"(x)); }
+
 // interval of a sub-context code from (t, dist[, same, less]): compress.c:301-308
 DEV void sub_interval(uint32_t t, uint32_t d, uint32_t same, uint32_t less, bool hit, uint32_t& under,
                       uint32_t& count, uint32_t& total)

@@ -52,24 +52,26 @@ __device__ __forceinline__ uint32_t udiv16r(uint32_t a, uint32_t b, float rb)
 }
 __device__ __forceinline__ float rcp16(uint32_t b) { return __builtin_amdgcn_rcpf(static_cast<float>(b)); }
 
-// 1/b in double precision, relative error < 2^-52 (two Newton steps, as udiv)
+// 1/b in double precision for 1 <= b <= 65535: v_rcp_f64 (relative error up
+// to 2^-24.4) and one Newton step, relative error < 2^-48.7 for every such b
+// (measured exhaustively, tools/mb/rcpacc.hip) -- at least 89x inside what
+// udiv16d needs (below b * 2^-49 * 0.9375 and below 2^-33).
 __device__ __forceinline__ double rcp64(uint32_t b)
 {
     const double db = static_cast<double>(b);
-    double r = __builtin_amdgcn_rcp(db);
-    double e = __builtin_fma(-db, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-db, r, 1.0);
-    return __builtin_fma(r, e, r);
+    const double r = __builtin_amdgcn_rcp(db);
+    return __builtin_fma(r, __builtin_fma(-db, r, 1.0), r);
 }
 
 // floor(a / b) for 1 <= b <= 65535 with rb = rcp64(b): three dependent
 // instructions (convert, fma, convert; ~20 cycles against ~90 for udiv16r,
-// tools/mb/chainlat.hip).  a * rb is within 2^32 * 2^-52 = 2^-20 of a/b, the
-// fma's rounding adds < 2^-21, so a/b + 2^-17 is computed within 2^-19: at
-// least the integer a/b when it is one, and below the next integer otherwise
-// (the fraction of a/b is then at most 1 - 1/b < 1 - 2^-17 - 2^-19 for b <
-// 104857).  Exact over every pair (tests/test_udiv.py, chainlat's sweep).
+// tools/mb/chainlat.hip).  With rb = (1/b)(1 + d), a * rb is within
+// (2^32 / b) d of a/b and the fma's rounding adds < 2^-21, so a/b + 2^-17 is
+// computed at least at the integer a/b when it is one (needs (2^32/b) d +
+// 2^-21 < 2^-17: d < b * 2^-49 * 0.9375), and below the next integer
+// otherwise, the fraction of a/b being at most 1 - 1/b (needs 2^-17 + 2^-21 +
+// (2^32/b) d < 1/b: d < 2^-33 for b <= 65535).  GPU-checked over random and
+// boundary pairs (tests/test_udiv.py, chainlat's sweep).
 __device__ __forceinline__ uint32_t udiv16d(uint32_t a, uint32_t, double rb)
 {
     return static_cast<uint32_t>(__builtin_fma(static_cast<double>(a), rb, 0x1p-17));

@@ -8,20 +8,6 @@
 
 #include "../../enet_amd/csrc/rc_udiv.h"
 
-__device__ __forceinline__ double rcp64(uint32_t b)
-{
-    const double db = static_cast<double>(b);
-    double r = __builtin_amdgcn_rcp(db);
-    double e = __builtin_fma(-db, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-db, r, 1.0);
-    return __builtin_fma(r, e, r);
-}
-__device__ __forceinline__ uint32_t udiv16d(uint32_t a, double rb)
-{
-    return static_cast<uint32_t>(__builtin_fma(static_cast<double>(a), rb, 0x1p-17));
-}
-
 template <int K>
 __global__ __launch_bounds__(64) void chain(uint32_t* out, unsigned long long* cyc, uint32_t n, uint32_t seed)
 {
@@ -38,7 +24,7 @@ __global__ __launch_bounds__(64) void chain(uint32_t* out, unsigned long long* c
             if (K == 1) x = x * y;                                   // v_mul_lo_u32
             if (K == 2) x = static_cast<uint32_t>(static_cast<uint64_t>(x) * y + y);  // mad_u64
             if (K == 3) x = (udiv16r(x | 0x80000000u, b, rb)) ^ y;   // the coder's division now
-            if (K == 4) x = (udiv16d(x | 0x80000000u, rbd)) ^ y;     // f64 quotient
+            if (K == 4) x = (udiv16d(x | 0x80000000u, b, rbd)) ^ y;     // f64 quotient
             if (K == 5) x = __float_as_uint(__builtin_amdgcn_rcpf(__uint_as_float(x)));
             if (K == 6) x = static_cast<uint32_t>(static_cast<double>(x) * 0.75);   // cvt + mul f64 + cvt
             if (K == 7) { const uint32_t l = x + y; x = (x ^ l) == 0 ? x : (x << (8 * (__builtin_clz(x ^ l) >> 3))); }
@@ -74,7 +60,7 @@ __global__ void check(uint32_t* bad, uint32_t b0)
         const uint32_t a = t * 262139u + j * 16777259u;
         const uint32_t m = (a / b) * b;
         const uint32_t c[5] = {a, m, m - 1, m + b - 1, 0xFFFFFFFFu - t};
-        for (int k = 0; k < 5; ++k) nb += udiv16d(c[k], rbd) != c[k] / b;
+        for (int k = 0; k < 5; ++k) nb += udiv16d(c[k], b, rbd) != c[k] / b;
     }
     if (nb) atomicAdd(bad, nb);
 }
