@@ -345,6 +345,9 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // for lanes that need none; see rc_lane3.hip lane_prefetch).
         PROF(3)
         const bool nfwd = order >= 1 && v == p;
+#ifdef DEC4_PAD
+        __builtin_amdgcn_s_sleep(DEC4_PAD);           // (timing experiment: compute added before the load)
+#endif
         raw4_load(reg, nfwd ? kDummyRec : kO1Base + v * kRec4, rw);
         fail = o.n >= o.cap;                                         // compress.c:617
         // the element joins bucket p (compress.c:598-615: every visited
