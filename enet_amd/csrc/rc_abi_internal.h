@@ -55,6 +55,9 @@ typedef struct {
     /* bucket-history decoder (rc_dec4.hip) in front of the v3 lane decoder; the packets it
        leaves go to enc2_list / counters[3] (ENET_RC_DEC4=0: off) */
     uint32_t  dec4;
+    /* test switch (ENET_RC_ENC2_SLOW=1): the scan takes its slow paths (every position
+       exceptional, every bucket sorted and re-walked) */
+    uint32_t  enc2_slow;
     /* lane kernels: when set, run only the sub_count[0] packets of sub_list */
     const uint32_t *sub_list;
     const uint32_t *sub_count;

@@ -98,6 +98,7 @@ struct E2Params {
     uint32_t*       count;
     uint32_t        act;        // pass 2: packets per wavefront (64 or 32)
     uint8_t*        dummy;      // pass 2: 1 MB, 16 B per lane, the target of stores with nothing to store
+    uint32_t        slow;       // test switch (ENET_RC_ENC2_SLOW=1): every position exceptional, every bucket re-walked
 };
 
 DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
@@ -117,8 +118,8 @@ struct ScanLds {
     };
     uint32_t repat[64];               // position i's bigram (x[i-1], x[i]) occurred before i (2048 bits)
     uint32_t probe;                   // lane-order probe (rc_enc2_scan)
-    uint8_t  excb[256];               // bucket holds an exceptional position
-    uint8_t  xlist[256];              // those buckets
+    uint32_t xfirst[256];             // rank of the bucket's first exceptional position (~0: none)
+    uint8_t  xlist[256];              // buckets with one
 };
 
 // element word: pos (0-10) | v (11-18) | a | 256 (19-27, 0 for position 1) |
@@ -234,29 +235,27 @@ DEV void sort_bucket(ScanLds& s, uint32_t bs, uint32_t be)
 // A bucket holding exceptional positions, in position order: each
 // exceptional position needs the flags of the earlier ones; a plain one
 // codes t1 = j - (earlier order-2 hits), dist1 = t1 - (earlier order-1 hits),
-// hits that occur only at exceptional positions.  Returns false if the
-// bucket is not in position order (nothing is final then).
-DEV bool walk_full(ScanLds& s, uint32_t bs, uint32_t k, uint2* rec)
+// hits that occur only at exceptional positions.  The walk starts at the
+// first exceptional position j0 (the positions before it are plain with no
+// hit before them: the scatter's records stand) and rewrites a plain record
+// only once a hit has changed it (all: every record, after a sort).
+DEV void walk_from(ScanLds& s, uint32_t bs, uint32_t k, uint32_t j0, bool all, uint2* rec)
 {
-    uint32_t nf2 = 0, nh1 = 0, prev = 0;
-    bool sorted = true;
+    uint32_t nf2 = 0, nh1 = 0;
     uint4 u = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll 1
-    for (uint32_t j = 0; j < k; ++j) {
-        if ((j & 3) == 0) u = *reinterpret_cast<const uint4*>(&s.e[bs + j]);
+    for (uint32_t j = j0; j < k; ++j) {
+        if (j == j0 || (j & 3) == 0) u = *reinterpret_cast<const uint4*>(&s.e[bs + (j & ~3u)]);
         const uint32_t w = pick4(j & 3, u);
-        sorted = sorted && (w & 2047) > prev;
-        prev = w & 2047;
         if (w & kExc) {
             const uint32_t fl = scan_exceptional(s, bs, bs + j, w, rec);
             nf2 += (fl & kF2) ? 1u : 0u;
             nh1 += (fl & kF1) ? 1u : 0u;
-        } else {
+        } else if (all || (nf2 | nh1) != 0) {
             const uint32_t t1 = j - nf2, d1 = t1 - nh1;
             rec[w & 2047] = make_uint2(t1 ? (1u | t1 << 3 | d1 << 9) : 0u, ((w >> 11) & 255) << 24);
         }
     }
-    return sorted;
 }
 
 extern "C" __global__ __launch_bounds__(kScanThreads)
@@ -270,7 +269,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
     // rely on it; without it every position takes the full statistics.
     if (t == 0) s.probe = 0;
     wave_sync();
-    const bool ordered = !any_lane(atomicAdd(&s.probe, 1u) != t);
+    const bool ordered = !any_lane(atomicAdd(&s.probe, 1u) != t) && !e.slow;
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const uint32_t pkt = packet_of(e, idx);
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
@@ -339,7 +338,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
         wave_sync();
         E2P(2)
-        if (t < 16) *reinterpret_cast<uint4*>(&s.excb[16 * t]) = z;
+        *reinterpret_cast<uint4*>(&s.xfirst[4 * t]) = make_uint4(~0u, ~0u, ~0u, ~0u);
         wave_sync();
         // Scatter into buckets, and each position's record as in a bucket with
         // no exceptional position: t1 = dist1 = its rank j in the bucket (the
@@ -361,11 +360,10 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                     // full statistics where v may already be in the order-1
                     // context (its bigram occurred before) or the order-2
                     // context exists (the bigram before it occurred before);
-                    // every other position is plain (see walk_full)
+                    // every other position is plain (see walk_from)
                     const bool exc = !ordered || bit_at(s.repat, ii) || (ii >= 2 && bit_at(s.repat, ii - 1));
                     w[m] = ii | v << 11 | (ii >= 2 ? (a | 256u) << 19 : 0u) | (exc ? kExc : 0u);
                     bb[m] = p;
-                    if (exc) s.excb[p] = 1;
                 }
             }
 #pragma unroll
@@ -376,6 +374,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                     s.e[k[m]] = w[m];
                     const uint32_t j = k[m] - s.start[bb[m]];
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
+                    if (w[m] & kExc) atomicMin(&s.xfirst[bb[m]], j);
                 }
             }
             wave_sync();
@@ -385,13 +384,13 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                     disorder = disorder || (s.e[k[m] - 1] & 2047) > (w[m] & 2047);
         }
         const uint32_t x0 = x[0];
-        disorder = any_lane(disorder);
+        disorder = any_lane(disorder) || e.slow;
         E2P(3)
         // buckets with exceptional positions: compacted over the lanes, one
         // per lane, each walked in full
         {
-            const uint32_t f = *reinterpret_cast<const uint32_t*>(&s.excb[4 * t]);
-            const uint32_t m0 = f & 1, m1 = (f >> 8) & 1, m2 = (f >> 16) & 1, m3 = (f >> 24) & 1;
+            const uint4 f = *reinterpret_cast<const uint4*>(&s.xfirst[4 * t]);
+            const uint32_t m0 = f.x != ~0u, m1 = f.y != ~0u, m2 = f.z != ~0u, m3 = f.w != ~0u;
             const uint32_t cntx = m0 + m1 + m2 + m3;
             const uint32_t incl = wave_incl_scan(cntx);
             uint32_t o = incl - cntx;
@@ -405,26 +404,22 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             for (uint32_t q = t; q < nx; q += kScanThreads) {
                 const uint32_t bk = s.xlist[q];
                 const uint32_t bs = s.start[bk], kk = s.cnt[bk] - bs;
-                if (rare_lane(!walk_full(s, bs, kk, rec))) {   // (not seen on gfx950) sort, walk again
-                    for (uint32_t j = 0; j < kk; ++j) s.e[bs + j] &= ~(kF2 | kNV1 | kF1);
-                    sort_bucket(s, bs, bs + kk);
-                    walk_full(s, bs, kk, rec);
-                }
+                walk_from(s, bs, kk, s.xfirst[bk], false, rec);
             }
         }
         E2P(4)
-        if (rare_lane(disorder)) {                    // (not seen on gfx950) the plain buckets sorted and rewritten
-        wave_sync();
+        if (rare_lane(disorder)) {
+            // (not seen on gfx950) the scatter's ranks were not position
+            // order somewhere: every bucket sorted, its flags cleared, walked
+            // from its start with every record rewritten
+            wave_sync();
 #pragma unroll 1
-        for (uint32_t r = 0; r < 4; ++r) {
-            const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
-            if (s.excb[4 * t + r]) continue;
-            sort_bucket(s, bs, bs + kk);
-            for (uint32_t j = 0; j < kk; ++j) {
-                const uint32_t w = s.e[bs + j];
-                rec[w & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w >> 11) & 255) << 24);
+            for (uint32_t r = 0; r < 4; ++r) {
+                const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
+                for (uint32_t j = 0; j < kk; ++j) s.e[bs + j] &= ~(kF2 | kNV1 | kF1);
+                sort_bucket(s, bs, bs + kk);
+                walk_from(s, bs, kk, 0, true, rec);
             }
-        }
         }
         if (t == 0) rec[0] = make_uint2(0u, x0 << 24);  // position 0: root only
         wave_sync();                              // LDS reuse by the next packet
@@ -766,6 +761,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     const uint32_t scan_blocks_max = ws->cus * 16;
     static const char* lanes = getenv("ENET_RC_ENC2_LANES");      // experiment: 32 packets per wavefront
     e.act = (lanes && atoi(lanes) == 32) ? 32u : 64u;
+    e.slow = ws->enc2_slow;
     for (uint64_t lo = 0; lo < b->n; lo += per) {
         const uint64_t hi = lo + per < b->n ? lo + per : b->n;
         e.lo = static_cast<uint32_t>(lo);

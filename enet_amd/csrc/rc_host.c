@@ -191,6 +191,8 @@ void *enet_range_coder_create(void)
         c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
         const char *d4 = getenv("ENET_RC_DEC4");
         c->ws.dec4 = !(d4 && strcmp(d4, "0") == 0);
+        const char *es = getenv("ENET_RC_ENC2_SLOW");
+        c->ws.enc2_slow = (es && strcmp(es, "1") == 0) ? 1u : 0u;
         const char *sl = getenv("ENET_RC_SLOTS");
         c->max_slots = MAX_LANE_SLOTS;
         if (sl && atol(sl) >= 256 && atol(sl) <= (1l << 22)) c->max_slots = (uint32_t) atol(sl);

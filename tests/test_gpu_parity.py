@@ -21,6 +21,10 @@ VARIANTS = {
     # default: two-pass encoder (rc_enc2.hip) and bucket-history decoder
     # (rc_dec4.hip) in front of the v3 lane kernels (rc_lane3.hip)
     "lane3": {"ENET_RC_KERNEL": "lane3"},
+    # the two-pass encoder's slow paths forced (every position exceptional,
+    # every bucket sorted and re-walked: what a device without lane-ordered
+    # LDS atomics would take)
+    "enc2-slow": {"ENET_RC_KERNEL": "lane3", "ENET_RC_ENC2_SLOW": "1"},
     # the v3 lane kernels alone, both directions
     "lane3-only": {"ENET_RC_KERNEL": "lane3", "ENET_RC_ENC2": "0", "ENET_RC_DEC4": "0"},
     # model v2 (rc_lane.hip)
