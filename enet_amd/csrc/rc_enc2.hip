@@ -118,7 +118,7 @@ struct ScanLds {
     };
     uint32_t repat[64];               // position i's bigram (x[i-1], x[i]) occurred before i (2048 bits)
     uint32_t probe;                   // lane-order probe (rc_enc2_scan)
-    uint32_t xfirst[256];             // rank of the bucket's first exceptional position (~0: none)
+    uint32_t xmask[256];              // ranks of the bucket's exceptional positions (bit min(rank, 31))
     uint8_t  xlist[256];              // buckets with one
 };
 
@@ -235,18 +235,19 @@ DEV void sort_bucket(ScanLds& s, uint32_t bs, uint32_t be)
 // A bucket holding exceptional positions, in position order: each
 // exceptional position needs the flags of the earlier ones; a plain one
 // codes t1 = j - (earlier order-2 hits), dist1 = t1 - (earlier order-1 hits),
-// hits that occur only at exceptional positions.  The walk starts at the
-// first exceptional position j0 (the positions before it are plain with no
-// hit before them: the scatter's records stand) and rewrites a plain record
-// only once a hit has changed it (all: every record, after a sort).
-DEV void walk_from(ScanLds& s, uint32_t bs, uint32_t k, uint32_t j0, bool all, uint2* rec)
+// hits that occur only at exceptional positions.  xm marks the exceptional
+// ranks (bit min(rank, 31)): until the first hit the walk visits only those
+// (the plain positions between keep the scatter's records), after it every
+// position (their t1, dist1 change).  xm = ~0: every position, every record
+// rewritten (after a sort).
+DEV void walk_from(ScanLds& s, uint32_t bs, uint32_t k, uint32_t xm, uint2* rec)
 {
+    const bool all = xm == ~0u;
     uint32_t nf2 = 0, nh1 = 0;
-    uint4 u = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t j = static_cast<uint32_t>(__builtin_ctz(xm));
 #pragma unroll 1
-    for (uint32_t j = j0; j < k; ++j) {
-        if (j == j0 || (j & 3) == 0) u = *reinterpret_cast<const uint4*>(&s.e[bs + (j & ~3u)]);
-        const uint32_t w = pick4(j & 3, u);
+    while (j < k) {
+        const uint32_t w = s.e[bs + j];
         if (w & kExc) {
             const uint32_t fl = scan_exceptional(s, bs, bs + j, w, rec);
             nf2 += (fl & kF2) ? 1u : 0u;
@@ -255,6 +256,9 @@ DEV void walk_from(ScanLds& s, uint32_t bs, uint32_t k, uint32_t j0, bool all, u
             const uint32_t t1 = j - nf2, d1 = t1 - nh1;
             rec[w & 2047] = make_uint2(t1 ? (1u | t1 << 3 | d1 << 9) : 0u, ((w >> 11) & 255) << 24);
         }
+        // the next position: the next exceptional one while there was no hit
+        const uint32_t rest = (j >= 31 || all || (nf2 | nh1) != 0) ? 0u : (xm & ~((2u << j) - 1u));
+        j = (j >= 31 || all || (nf2 | nh1) != 0) ? j + 1 : (rest ? static_cast<uint32_t>(__builtin_ctz(rest)) : k);
     }
 }
 
@@ -338,7 +342,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
         wave_sync();
         E2P(2)
-        *reinterpret_cast<uint4*>(&s.xfirst[4 * t]) = make_uint4(~0u, ~0u, ~0u, ~0u);
+        *reinterpret_cast<uint4*>(&s.xmask[4 * t]) = z;
         wave_sync();
         // Scatter into buckets, and each position's record as in a bucket with
         // no exceptional position: t1 = dist1 = its rank j in the bucket (the
@@ -374,7 +378,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                     s.e[k[m]] = w[m];
                     const uint32_t j = k[m] - s.start[bb[m]];
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
-                    if (w[m] & kExc) atomicMin(&s.xfirst[bb[m]], j);
+                    if (w[m] & kExc) atomicOr(&s.xmask[bb[m]], 1u << min(j, 31u));
                 }
             }
             wave_sync();
@@ -389,8 +393,8 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         // buckets with exceptional positions: compacted over the lanes, one
         // per lane, each walked in full
         {
-            const uint4 f = *reinterpret_cast<const uint4*>(&s.xfirst[4 * t]);
-            const uint32_t m0 = f.x != ~0u, m1 = f.y != ~0u, m2 = f.z != ~0u, m3 = f.w != ~0u;
+            const uint4 f = *reinterpret_cast<const uint4*>(&s.xmask[4 * t]);
+            const uint32_t m0 = f.x != 0, m1 = f.y != 0, m2 = f.z != 0, m3 = f.w != 0;
             const uint32_t cntx = m0 + m1 + m2 + m3;
             const uint32_t incl = wave_incl_scan(cntx);
             uint32_t o = incl - cntx;
@@ -404,7 +408,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             for (uint32_t q = t; q < nx; q += kScanThreads) {
                 const uint32_t bk = s.xlist[q];
                 const uint32_t bs = s.start[bk], kk = s.cnt[bk] - bs;
-                walk_from(s, bs, kk, s.xfirst[bk], false, rec);
+                walk_from(s, bs, kk, s.xmask[bk], rec);
             }
         }
         E2P(4)
@@ -418,7 +422,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                 const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
                 for (uint32_t j = 0; j < kk; ++j) s.e[bs + j] &= ~(kF2 | kNV1 | kF1);
                 sort_bucket(s, bs, bs + kk);
-                walk_from(s, bs, kk, 0, true, rec);
+                walk_from(s, bs, kk, ~0u, rec);
             }
         }
         if (t == 0) rec[0] = make_uint2(0u, x0 << 24);  // position 0: root only
