@@ -109,14 +109,14 @@ DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 // ------------------------------------------------------------------ pass 1
 
 struct ScanLds {
-    uint8_t  x[2048];                 // packet bytes at x[mis + i]
+    uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i]
     uint32_t cnt[256];                // bucket sizes, then fill pointers
     uint32_t start[256];              // bucket starts (4-aligned)
     union {
         uint32_t seen[2048];          // bigrams (x[i-1], x[i]) seen, 64 Ki bits
         uint32_t e[2048 + 768];       // elements in bucket order (below), buckets 4-aligned
     };
-    uint32_t repat[64];               // position i's bigram (x[i-1], x[i]) occurred before i (2048 bits)
+    uint32_t excm[64];                // exceptional positions: i or i - 1 repeats an earlier bigram (2048 bits)
     uint32_t probe;                   // lane-order probe (rc_enc2_scan)
     uint32_t xmask[256];              // ranks of the bucket's exceptional positions (bit min(rank, 31))
     uint8_t  xlist[256];              // buckets with one
@@ -145,6 +145,15 @@ DEV void fallback(const E2Params& e, uint32_t* slot, uint32_t pkt)
 }
 
 DEV bool bit_at(const uint32_t* m, uint32_t i) { return (m[i >> 5] >> (i & 31)) & 1; }
+
+// bytes q-2, q-1, q of the LDS byte array xb (q >= 4) in bits 0-23: two
+// dword reads and a funnel shift instead of three byte reads
+DEV uint32_t bytes3(const uint8_t* xb, uint32_t q)
+{
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(xb) + (q >> 2) - 1;
+    const uint64_t w = static_cast<uint64_t>(d[1]) << 32 | d[0];
+    return static_cast<uint32_t>(w >> (8 * ((q & 3) + 2)));
+}
 
 // The scan's workgroup is one wavefront, and LDS operations of a wavefront
 // complete in order: lanes see each other's LDS writes without a workgroup
@@ -291,15 +300,16 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint32_t mis = static_cast<uint32_t>(src & 15);
         const uint32_t chunks = (mis + n + 15) >> 4;
         for (uint32_t c = t; c < chunks; c += kScanThreads)
-            *reinterpret_cast<uint4*>(s.x + 16 * c) = gload16(a16 + 16 * c);
+            *reinterpret_cast<uint4*>(s.x + 16 + 16 * c) = gload16(a16 + 16 * c);
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = z;
-        if (t < 16) *reinterpret_cast<uint4*>(&s.repat[4 * t]) = z;
+        if (t < 16) *reinterpret_cast<uint4*>(&s.excm[4 * t]) = z;
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(&s.seen[4 * (t + 64 * k)]) = z;
         wave_sync();
         E2P(0)
-        const uint8_t* x = s.x + mis;
+        const uint8_t* x = s.x + 16 + mis;
+        const uint32_t q0 = 16 + mis;                  // s.x index of position 0
         // bucket sizes, and the positions whose bigram occurred before (the
         // old bit of the seen set: position order, when same-address
         // atomics of one instruction apply in lane order -- `ordered`)
@@ -308,7 +318,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
                 const uint32_t ii = i + m * kScanThreads;
-                key[m] = ii < n ? static_cast<uint32_t>(x[ii - 1]) << 8 | x[ii] : 0xFFFFFFFFu;
+                key[m] = ii < n ? (__builtin_bswap32(bytes3(s.x, q0 + ii)) >> 8) & 0xFFFFu : 0xFFFFFFFFu;
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
@@ -321,8 +331,10 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m)
                 if (key[m] != 0xFFFFFFFFu && (old[m] & (1u << (key[m] & 31)))) {
+                    // position ii's bigram repeats: ii and ii + 1 are exceptional
                     const uint32_t ii = i + m * kScanThreads;
-                    atomicOr(&s.repat[ii >> 5], 1u << (ii & 31));
+                    atomicOr(&s.excm[ii >> 5], 1u << (ii & 31));
+                    atomicOr(&s.excm[(ii + 1) >> 5], 1u << ((ii + 1) & 31));
                 }
         }
         wave_sync();
@@ -360,23 +372,27 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                 const uint32_t ii = i + m * kScanThreads;
                 bb[m] = 0xFFFFFFFFu;
                 if (ii < n) {
-                    const uint32_t p = x[ii - 1], v = x[ii], a = ii >= 2 ? x[ii - 2] : 0u;
+                    const uint32_t b3 = bytes3(s.x, q0 + ii);
+                    const uint32_t p = (b3 >> 8) & 255, v = (b3 >> 16) & 255, a = ii >= 2 ? b3 & 255 : 0u;
                     // full statistics where v may already be in the order-1
                     // context (its bigram occurred before) or the order-2
                     // context exists (the bigram before it occurred before);
                     // every other position is plain (see walk_from)
-                    const bool exc = !ordered || bit_at(s.repat, ii) || (ii >= 2 && bit_at(s.repat, ii - 1));
+                    const bool exc = !ordered || bit_at(s.excm, ii);
                     w[m] = ii | v << 11 | (ii >= 2 ? (a | 256u) << 19 : 0u) | (exc ? kExc : 0u);
                     bb[m] = p;
                 }
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) k[m] = bb[m] != 0xFFFFFFFFu ? atomicAdd(&s.cnt[bb[m]], 1u) : 0u;
+            uint32_t jj[4];
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
+                jj[m] = 0;
                 if (bb[m] != 0xFFFFFFFFu) {
                     s.e[k[m]] = w[m];
                     const uint32_t j = k[m] - s.start[bb[m]];
+                    jj[m] = j;
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
                     if (w[m] & kExc) atomicOr(&s.xmask[bb[m]], 1u << min(j, 31u));
                 }
@@ -384,7 +400,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             wave_sync();
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m)
-                if (bb[m] != 0xFFFFFFFFu && k[m] != s.start[bb[m]])
+                if (bb[m] != 0xFFFFFFFFu && jj[m] != 0)
                     disorder = disorder || (s.e[k[m] - 1] & 2047) > (w[m] & 2047);
         }
         const uint32_t x0 = x[0];
