@@ -109,7 +109,7 @@ DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 // ------------------------------------------------------------------ pass 1
 
 struct ScanLds {
-    uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i]
+    uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i] (128 chunks of 16 B)
     uint32_t cnt[256];                // bucket sizes, then fill pointers
     uint32_t start[256];              // bucket starts (4-aligned)
     union {
@@ -271,6 +271,52 @@ DEV void walk_from(ScanLds& s, uint32_t bs, uint32_t k, uint32_t xm, uint2* rec)
     }
 }
 
+// The next packet of a scan wavefront, fetched while the current one is
+// walked: its length, where its bytes start, and its 16-B chunks in
+// registers (two per lane cover 1919 B at any alignment).
+struct ScanPf {
+    uint32_t pkt, n, mis;
+    uint4 r0, r1;
+};
+
+// A read-only input array read through the constant address space: wave-
+// uniform reads of it become scalar loads (counted in lgkmcnt, so using them
+// never waits for the vector stores in flight).  The batch's lengths, offsets
+// and the length order are not written while the scan runs.
+template <typename T>
+DEV T const_load(const T* p, uint32_t i)
+{
+    typedef const __attribute__((address_space(4))) T* cptr;
+    return ((cptr) reinterpret_cast<uintptr_t>(p))[i];
+}
+
+DEV ScanPf scan_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t idx)
+{
+    ScanPf f;
+    f.pkt = 0; f.n = 0; f.mis = 0;
+    // (the loads are issued on every path -- a register written on one path
+    // only would make the compiler wait for them at the merge; with nothing to
+    // fetch they read the batch's first 16 B)
+    uintptr_t a0 = reinterpret_cast<uintptr_t>(b.in) & ~static_cast<uintptr_t>(15), a1 = a0;
+    if (idx < e.hi) {
+        f.pkt = (e.order && !const_load(e.bins, RC_LEN_BINS)) ? const_load(e.order, idx) : idx;
+        f.n = const_load(b.in_len, f.pkt);
+        if (f.n != 0 && f.n <= kE2MaxLen) {
+            const uintptr_t src = reinterpret_cast<uintptr_t>(b.in + const_load(b.in_off, f.pkt));
+            const uintptr_t a16 = src & ~static_cast<uintptr_t>(15);
+            f.mis = static_cast<uint32_t>(src & 15);
+            // (clamped to the packet's last chunk: chunks past it land in LDS
+            // past the packet, where nothing reads them)
+            const uint32_t last = (f.mis + f.n - 1) >> 4;
+            a0 = a16 + 16 * min(threadIdx.x, last);
+            a1 = a16 + 16 * min(threadIdx.x + kScanThreads, last);
+        }
+    }
+    f.r0 = gload16(a0);
+    f.r1 = gload16(a1);
+    return f;
+}
+
 extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_scan(rc_batch_dev b, E2Params e)
 {
@@ -283,24 +329,22 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
     if (t == 0) s.probe = 0;
     wave_sync();
     const bool ordered = !any_lane(atomicAdd(&s.probe, 1u) != t) && !e.slow;
+    ScanPf pf = scan_prefetch(b, e, e.lo + blockIdx.x);
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
-        const uint32_t pkt = packet_of(e, idx);
+        const ScanPf cur = pf;
+        const uint32_t pkt = cur.pkt, n = cur.n, mis = cur.mis;
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
-        const uint32_t n = b.in_len[pkt];
         if (n == 0 || n > kE2MaxLen) {                 // compress.c:257 / possible model reset
             if (t == 0) {
                 if (n == 0) { slot[0] = kSkipDone; b.out_len[pkt] = 0; }
                 else fallback(e, slot, pkt);
             }
+            pf = scan_prefetch(b, e, idx + gridDim.x);
             continue;
         }
-        // the packet into LDS: aligned 16-B chunks, x = s.x + misalignment
-        const uintptr_t src = reinterpret_cast<uintptr_t>(b.in + b.in_off[pkt]);
-        const uintptr_t a16 = src & ~static_cast<uintptr_t>(15);
-        const uint32_t mis = static_cast<uint32_t>(src & 15);
-        const uint32_t chunks = (mis + n + 15) >> 4;
-        for (uint32_t c = t; c < chunks; c += kScanThreads)
-            *reinterpret_cast<uint4*>(s.x + 16 + 16 * c) = gload16(a16 + 16 * c);
+        // the packet into LDS (prefetched): aligned 16-B chunks, x = s.x + 16 + misalignment
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = cur.r0;
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = cur.r1;
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = z;
         if (t < 16) *reinterpret_cast<uint4*>(&s.excm[4 * t]) = z;
@@ -344,6 +388,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
         if (any_lane(mx > kE2Bucket)) {
             if (t == 0) fallback(e, slot, pkt);
+            pf = scan_prefetch(b, e, idx + gridDim.x);
             continue;
         }
         const uint32_t a0 = (c4.x + 3) & ~3u, a1 = (c4.y + 3) & ~3u, a2 = (c4.z + 3) & ~3u, a3 = (c4.w + 3) & ~3u;
@@ -405,6 +450,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         }
         const uint32_t x0 = x[0];
         disorder = any_lane(disorder) || e.slow;
+        pf = scan_prefetch(b, e, idx + gridDim.x);     // (the bytes in LDS are not read past here)
         E2P(3)
         // buckets with exceptional positions: compacted over the lanes, one
         // per lane, each walked in full
