@@ -117,7 +117,7 @@ struct ScanLds {
         uint32_t e[2048 + 768];       // elements in bucket order (below), buckets 4-aligned
     };
     uint32_t excm[64];                // exceptional positions: i or i - 1 repeats an earlier bigram (2048 bits)
-    uint32_t probe;                   // lane-order probe (rc_enc2_scan)
+    uint32_t probe[16];               // lane-order probe (rc_enc2_scan)
     uint32_t xmask[256];              // ranks of the bucket's exceptional positions (bit min(rank, 31))
     uint8_t  xlist[256];              // buckets with one
 };
@@ -317,18 +317,41 @@ DEV ScanPf scan_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t idx)
     return f;
 }
 
+// Same-address LDS atomics in lane order within an instruction and in
+// program order across instructions, for a full conflict (twice) and for
+// partial ones (4 words, lanes interleaved, blocked and hashed onto them).
+// Checked once per wavefront; the scan's shortcuts are taken only if it holds.
+DEV bool lane_order_probe(uint32_t* pr, uint32_t t)
+{
+    if (t < 16) pr[t] = 0;
+    wave_sync();
+    const uint64_t below = (1ull << t) - 1ull;
+    const uint32_t k3 = (t * 2654435761u >> 28) & 3;
+    uint64_t same3 = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(k3 == q);
+        same3 = k3 == q ? m : same3;
+    }
+    bool ok = atomicAdd(&pr[0], 1u) == t;
+    ok = (atomicAdd(&pr[0], 1u) == 64 + t) && ok;
+    ok = (atomicAdd(&pr[1 + (t & 3)], 1u) == (t >> 2)) && ok;
+    ok = (atomicAdd(&pr[5 + (t >> 4)], 1u) == (t & 15)) && ok;
+    ok = (atomicAdd(&pr[9 + k3], 1u) == static_cast<uint32_t>(__builtin_popcountll(same3 & below))) && ok;
+    return !any_lane(!ok);
+}
+
 extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_scan(rc_batch_dev b, E2Params e)
 {
     __shared__ __attribute__((aligned(16))) ScanLds s;
     const uint32_t t = threadIdx.x;
     E2P_DECL
-    // Do same-address LDS atomics of one instruction apply in lane order (as
-    // on gfx950, tools/atomorder.hip)?  The repeat bits and bucket ranks below
-    // rely on it; without it every position takes the full statistics.
-    if (t == 0) s.probe = 0;
-    wave_sync();
-    const bool ordered = !any_lane(atomicAdd(&s.probe, 1u) != t) && !e.slow;
+    // The repeat bits and bucket ranks below rely on same-address LDS atomics
+    // applying in lane order within an instruction and in program order
+    // across instructions (gfx950 does, tools/atomorder.hip); without it
+    // every position takes the full statistics and every bucket is sorted.
+    const bool ordered = lane_order_probe(s.probe, t) && !e.slow;
     ScanPf pf = scan_prefetch(b, e, e.lo + blockIdx.x);
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const ScanPf cur = pf;
@@ -405,11 +428,12 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         // no exceptional position: t1 = dist1 = its rank j in the bucket (the
         // walk below rewrites the buckets that have one).  The rank is the
         // slot from the LDS atomic, i.e. position order when same-address
-        // atomics of one instruction apply in lane order (gfx950 does,
-        // tools/atomorder.hip); each position checks its predecessor in the
-        // bucket, and any disorder sends the packet down the sorting walk.
+        // atomics apply in lane and program order (lane_order_probe; gfx950
+        // does, tools/atomorder.hip); otherwise every bucket is sorted and
+        // walked in full below.  (A per-position check of the predecessor
+        // slot cost 4 % of the encoder and could not see a later position
+        // taking an earlier slot, whose write comes after the check.)
         uint2* rec = reinterpret_cast<uint2*>(slot);
-        bool disorder = false;
         for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
             uint32_t w[4], k[4], bb[4];
 #pragma unroll
@@ -430,26 +454,19 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) k[m] = bb[m] != 0xFFFFFFFFu ? atomicAdd(&s.cnt[bb[m]], 1u) : 0u;
-            uint32_t jj[4];
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
-                jj[m] = 0;
                 if (bb[m] != 0xFFFFFFFFu) {
                     s.e[k[m]] = w[m];
                     const uint32_t j = k[m] - s.start[bb[m]];
-                    jj[m] = j;
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
                     if (w[m] & kExc) atomicOr(&s.xmask[bb[m]], 1u << min(j, 31u));
                 }
             }
-            wave_sync();
-#pragma unroll
-            for (uint32_t m = 0; m < 4; ++m)
-                if (bb[m] != 0xFFFFFFFFu && jj[m] != 0)
-                    disorder = disorder || (s.e[k[m] - 1] & 2047) > (w[m] & 2047);
         }
         const uint32_t x0 = x[0];
-        disorder = any_lane(disorder) || e.slow;
+        const bool disorder = !ordered;                // (wave-uniform)
+        wave_sync();
         pf = scan_prefetch(b, e, idx + gridDim.x);     // (the bytes in LDS are not read past here)
         E2P(3)
         // buckets with exceptional positions: compacted over the lanes, one
