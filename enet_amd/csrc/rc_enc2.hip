@@ -101,6 +101,10 @@ struct E2Params {
     uint32_t        slow;       // test switch (ENET_RC_ENC2_SLOW=1): every position exceptional, every bucket re-walked
 };
 
+// the last element slot: buckets of 1918 positions, each padded to 4, end
+// below it (1918 + 3 * 255 < 2815); lanes past a packet's end write there
+constexpr uint32_t kScanDummyE = 2048 + 768 - 1;
+
 DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 {
     return (e.order && !e.bins[RC_LEN_BINS]) ? e.order[idx] : idx;
@@ -118,6 +122,7 @@ struct ScanLds {
     };
     uint32_t excm[64];                // exceptional positions: i or i - 1 repeats an earlier bigram (2048 bits)
     uint32_t probe[16];               // lane-order probe (rc_enc2_scan)
+    uint32_t dummy[4];                // target of the atomics of lanes past the packet's end
     uint32_t xmask[256];              // ranks of the bucket's exceptional positions (bit min(rank, 31))
     uint8_t  xlist[256];              // buckets with one
 };
@@ -380,24 +385,26 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         // bucket sizes, and the positions whose bigram occurred before (the
         // old bit of the seen set: position order, when same-address
         // atomics of one instruction apply in lane order -- `ordered`)
+        // (branch-free: a lane past the packet's end reads the last position
+        // and sends its atomics to a dummy word, so no wait sits inside a
+        // per-position branch)
         for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
             uint32_t key[4], old[4];
+            bool ok[4];
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
                 const uint32_t ii = i + m * kScanThreads;
-                key[m] = ii < n ? (__builtin_bswap32(bytes3(s.x, q0 + ii)) >> 8) & 0xFFFFu : 0xFFFFFFFFu;
+                ok[m] = ii < n;
+                key[m] = (__builtin_bswap32(bytes3(s.x, q0 + min(ii, n - 1))) >> 8) & 0xFFFFu;
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
-                old[m] = 0;
-                if (key[m] != 0xFFFFFFFFu) {
-                    atomicAdd(&s.cnt[key[m] >> 8], 1u);
-                    old[m] = atomicOr(&s.seen[key[m] >> 5], 1u << (key[m] & 31));
-                }
+                atomicAdd(ok[m] ? &s.cnt[key[m] >> 8] : &s.dummy[0], 1u);
+                old[m] = atomicOr(ok[m] ? &s.seen[key[m] >> 5] : &s.dummy[1], 1u << (key[m] & 31));
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m)
-                if (key[m] != 0xFFFFFFFFu && (old[m] & (1u << (key[m] & 31)))) {
+                if (ok[m] && (old[m] & (1u << (key[m] & 31)))) {
                     // position ii's bigram repeats: ii and ii + 1 are exceptional
                     const uint32_t ii = i + m * kScanThreads;
                     atomicOr(&s.excm[ii >> 5], 1u << (ii & 31));
@@ -435,30 +442,38 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         // taking an earlier slot, whose write comes after the check.)
         uint2* rec = reinterpret_cast<uint2*>(slot);
         for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
-            uint32_t w[4], k[4], bb[4];
+            // (branch-free as above: reads, then atomics and starts, then writes)
+            uint32_t b3[4], ew[4], w[4], k[4], bb[4], st[4];
+            bool ok[4];
+#pragma unroll
+            for (uint32_t m = 0; m < 4; ++m) {
+                const uint32_t ii = min(i + m * kScanThreads, n - 1);
+                b3[m] = bytes3(s.x, q0 + ii);
+                ew[m] = s.excm[ii >> 5];
+            }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
                 const uint32_t ii = i + m * kScanThreads;
-                bb[m] = 0xFFFFFFFFu;
-                if (ii < n) {
-                    const uint32_t b3 = bytes3(s.x, q0 + ii);
-                    const uint32_t p = (b3 >> 8) & 255, v = (b3 >> 16) & 255, a = ii >= 2 ? b3 & 255 : 0u;
-                    // full statistics where v may already be in the order-1
-                    // context (its bigram occurred before) or the order-2
-                    // context exists (the bigram before it occurred before);
-                    // every other position is plain (see walk_from)
-                    const bool exc = !ordered || bit_at(s.excm, ii);
-                    w[m] = ii | v << 11 | (ii >= 2 ? (a | 256u) << 19 : 0u) | (exc ? kExc : 0u);
-                    bb[m] = p;
-                }
+                ok[m] = ii < n;
+                const uint32_t p = (b3[m] >> 8) & 255, v = (b3[m] >> 16) & 255, a = ii >= 2 ? b3[m] & 255 : 0u;
+                // full statistics where v may already be in the order-1
+                // context (its bigram occurred before) or the order-2
+                // context exists (the bigram before it occurred before);
+                // every other position is plain (see walk_from)
+                const bool exc = ((ew[m] >> (ii & 31)) & 1u) != 0 || !ordered;
+                w[m] = ii | v << 11 | (ii >= 2 ? (a | 256u) << 19 : 0u) | (exc ? kExc : 0u);
+                bb[m] = p;
             }
 #pragma unroll
-            for (uint32_t m = 0; m < 4; ++m) k[m] = bb[m] != 0xFFFFFFFFu ? atomicAdd(&s.cnt[bb[m]], 1u) : 0u;
+            for (uint32_t m = 0; m < 4; ++m) {
+                k[m] = atomicAdd(ok[m] ? &s.cnt[bb[m]] : &s.dummy[0], 1u);
+                st[m] = s.start[bb[m]];
+            }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
-                if (bb[m] != 0xFFFFFFFFu) {
-                    s.e[k[m]] = w[m];
-                    const uint32_t j = k[m] - s.start[bb[m]];
+                s.e[ok[m] ? k[m] : kScanDummyE] = w[m];
+                const uint32_t j = k[m] - st[m];
+                if (ok[m]) {
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
                     if (w[m] & kExc) atomicOr(&s.xmask[bb[m]], 1u << min(j, 31u));
                 }
