@@ -707,17 +707,23 @@ DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under
     low <<= 8 * kk;
     range <<= 8 * kk;
     bool more = en && (!fast || range < kBot);
-    while (rare_lane(more)) {
-        const bool carry = (low ^ (low + range)) >= kTop;
-        const bool stop = carry && range >= kBot;
-        more = more && !stop;
-        if (!any_lane(more)) break;
-        range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
-        src_adv(in);                       // (the decoder's top src_fill may have used c up)
-        src_fill(in, more && in.na == 0);
-        code = src_shift_in(in, code, more ? 1u : 0u);
-        range = more ? range << 8 : range;
-        low = more ? low << 8 : low;
+    if (rare_lane(more)) {
+        do {
+            const bool carry = (low ^ (low + range)) >= kTop;
+            const bool stop = carry && range >= kBot;
+            more = more && !stop;
+            if (!any_lane(more)) break;
+            range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
+            src_adv(in);                   // (the decoder's top src_fill may have used c up)
+            src_fill(in, more && in.na == 0);
+            code = src_shift_in(in, code, more ? 1u : 0u);
+            range = more ? range << 8 : range;
+            low = more ? low << 8 : low;
+        } while (rare_lane(more));
+        // settle this path's input load here: left in flight, it makes the
+        // compiler wait for vmcnt(0) -- behind every store -- wherever its
+        // registers are next touched on the common path, i.e. on every step
+        __builtin_amdgcn_s_waitcnt(0);
     }
 }
 
