@@ -114,6 +114,26 @@ DEV void root3_lookup(const uint8_t* r, const uint8_t* mtab, uint32_t v, uint32_
     under = (g ? dprev : 0u) + j + within;
 }
 
+// root3_lookup in two halves: the LDS reads (several issued together by the
+// encoder's helper) and the sums
+struct RootLk { uint4 q, m; uint32_t dprev, cnt; };
+DEV RootLk root3_lookup_read(const uint8_t* r, const uint8_t* mtab, uint32_t v)
+{
+    const uint32_t g = v >> 4, j = v & 15;
+    RootLk l;
+    l.q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    l.m = *reinterpret_cast<const uint4*>(mtab + 16 * j);
+    l.dprev = reinterpret_cast<const uint16_t*>(r + kRootD)[static_cast<int>(g) - 1];   // (g = 0: unused)
+    l.cnt = r[v];
+    return l;
+}
+DEV void root3_lookup_sum(const RootLk& l, uint32_t v, uint32_t& under, uint32_t& cnt)
+{
+    const uint32_t within = sad(l.q.w & l.m.w, sad(l.q.z & l.m.z, sad(l.q.y & l.m.y, sad(l.q.x & l.m.x, 0u))));
+    under = ((v >> 4) ? l.dprev : 0u) + (v & 15) + within;
+    cnt = l.cnt;
+}
+
 template <bool COPY>
 DEV void root3_add(uint8_t* r, Root& R, uint32_t v, uint32_t cnt)
 {
