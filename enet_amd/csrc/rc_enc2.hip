@@ -820,18 +820,29 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
 
 // ---- pass 2, two wavefronts per SIMD: a helper and a coder per packet.
 // The root model (order 0) evolves with the packet's symbols only, never with
-// the coder's state, so everything but the chain through (low, range) can
-// run ahead of it.  A block holds 256 packets in 8 wavefronts: wavefronts 4-7
-// (helpers) read the records, keep the root in LDS and queue per position
-// the three codes' intervals and reciprocals (a 32-B entry; a code a position
-// does not make is queued as the identity); wavefronts 0-3 (coders) run the
-// range coder over the queue and own the output ring.  The queue holds two
-// parts of four positions per packet: the helpers fill one while the coders
-// drain the other, a block barrier between parts.  With two wavefronts per
-// SIMD the SIMD issues a vector instruction every 2 cycles instead of every 4
-// for one wavefront alone.
+// the coder's state, so it can run ahead of the coder.  A block holds 256
+// packets in 8 wavefronts: wavefronts 4-7 (helpers) read the records, keep
+// the root in LDS and queue per position its record words with the root's
+// interval and total at that position (a 16-B entry); wavefronts 0-3
+// (coders) prepare the sub-context intervals from the record words and run
+// the range coder and the output ring.  The queue holds two parts of four
+// positions per packet: the helpers fill one while the coders drain the
+// other, a block barrier between parts.  With two wavefronts per SIMD the
+// SIMD issues a vector instruction every 2 cycles instead of every 4 for one
+// wavefront alone.
+#ifdef E2_PROF
+#define C2P_DECL unsigned long long c2t = __builtin_amdgcn_s_memtime(), c2w = 0, c2b = 0;
+#define C2P_WORK { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c2w += t_ - c2t; c2t = t_; __builtin_amdgcn_sched_barrier(0); }
+#define C2P_WAIT { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c2b += t_ - c2t; c2t = t_; __builtin_amdgcn_sched_barrier(0); }
+#define C2P_FLUSH(k) { if ((threadIdx.x & 63) == 0) { atomicAdd(&g_e2prof[k], c2w); atomicAdd(&g_e2prof[(k) + 1], c2b); } }
+#else
+#define C2P_DECL
+#define C2P_WORK
+#define C2P_WAIT
+#define C2P_FLUSH(k)
+#endif
 constexpr uint32_t kQPart = 4;                                   // positions per part
-constexpr uint32_t kQEntry = 32;                                 // bytes per queued position
+constexpr uint32_t kQEntry = 16;                                 // bytes per queued position
 constexpr uint32_t kC2Mtab = 256 * kCodeLds;                     // helper roots, then tables
 constexpr uint32_t kC2Itab = kC2Mtab + 256;
 constexpr uint32_t kC2Ring = kC2Itab + 512;                      // coder rings, 32 B per packet
@@ -853,36 +864,25 @@ DEV uint8_t* q_entry(uint8_t* smem, uint32_t part, uint32_t j, uint32_t lane)
     return smem + kC2Queue + (((part & 1) * kQPart + j) * 256 + lane) * kQEntry;
 }
 
-// helper: one position's entry (compress.c:286-337 without the coder)
+DEV bool root_codes(uint32_t w0) { const uint32_t typ = w0 & 7; return typ <= 1 || typ == 3 || typ == 4; }
+
+// helper: one position (the rare path: a part where some lane rescales)
 DEV void help_pos(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, uint32_t w0, uint32_t w1, bool en,
-                  uint32_t& rtot, double& rrt, uint8_t* qe)
+                  uint32_t& rtot, uint8_t* qe)
 {
-    const uint32_t typ = w0 & 7, ext = w0 >> 16, v = w1 >> 24;
+    const uint32_t v = w1 >> 24;
     uint32_t under0, cnt0;
     root3_lookup(root, mtab, v, under0, cnt0);
     const RootAddPre ra = root3_add_read(root, itab, v);
-    uint32_t un, ct, tt, un2, ct2, tt2;
-    sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
-    const uint32_t fb = typ == 5 ? w1 : ext;
-    sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un2, ct2, tt2);
-    const bool e1 = en && typ != 0, e2 = en && (typ == 4 || typ == 5), e0 = en && (typ <= 1 || typ == 3 || typ == 4);
-    const double r1 = rcp64(e1 ? tt : 1u), r0 = e0 ? rrt : 1.0;
-    const uint32_t u1 = e1 ? un : 0u, c1 = e1 ? ct : 1u;
-    const uint32_t u2 = e2 ? un2 : 0u, c2 = e2 ? ct2 : 1u, t2 = e2 ? tt2 : 0u;
-    const uint32_t u0 = e0 ? 1 + under0 : 0u, c0 = e0 ? 1 + cnt0 : 1u;
+    const bool e0 = en && root_codes(w0);
     if (e0) root3_add_write(root, v, cnt0, ra);
     uint32_t rt = e0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
     const bool rs = e0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rt > kTotalLimit);
     if (any_lane(rs)) {
         if (rs) { Root R; rt = root3_rescale<true>(root, R); }
     }
+    *reinterpret_cast<uint4*>(qe) = make_uint4(w0, w1, under0 | cnt0 << 16, rtot);
     rtot = rt;
-    rrt = rcp64(rt);
-    const uint64_t b1 = static_cast<uint64_t>(__double_as_longlong(r1)), b0 = static_cast<uint64_t>(__double_as_longlong(r0));
-    uint4* q = reinterpret_cast<uint4*>(qe);
-    q[0] = make_uint4(static_cast<uint32_t>(b1), static_cast<uint32_t>(b1 >> 32), static_cast<uint32_t>(b0),
-                      static_cast<uint32_t>(b0 >> 32));
-    q[1] = make_uint4(u1 | c1 << 16, u0 | c0 << 16, u2 | c2 << 16, t2);
 }
 
 // helper: a part of four positions with one round of LDS reads.  The four
@@ -892,7 +892,7 @@ DEV void help_pos(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, uint3
 // to the count where it is the same), and the updates are written after.
 // A part where some lane would rescale the root is done position by position.
 DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, const uint4& ca, const uint4& cb,
-                   uint32_t i, uint32_t len, uint32_t& rtot, double& rrt, uint8_t* smem, uint32_t part, uint32_t lane)
+                   uint32_t i, uint32_t len, uint32_t& rtot, uint8_t* smem, uint32_t part, uint32_t lane)
 {
     const uint32_t w0[4] = {ca.x, ca.z, cb.x, cb.z}, w1[4] = {ca.y, ca.w, cb.y, cb.w};
     uint32_t v[4], under[4], cnt[4], rt[4];
@@ -902,8 +902,7 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
         v[j] = w1[j] >> 24;
-        const uint32_t typ = w0[j] & 7;
-        e0[j] = i + j < len && (typ <= 1 || typ == 3 || typ == 4);
+        e0[j] = i + j < len && root_codes(w0[j]);
         lk[j] = root3_lookup_read(root, mtab, v[j]);
         const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (v[j] >> 4));
         inc[j][0] = ip[0];
@@ -911,7 +910,6 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
     }
     const uint4* dp = reinterpret_cast<const uint4*>(root + kRootD);
     uint4 d0 = dp[0], d1 = dp[1];
-    // intervals, corrected for the part's earlier updates; the root totals
     bool rs = false;
     uint32_t t = rtot;
 #pragma unroll
@@ -929,7 +927,7 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
     if (any_lane(rs)) {                               // (rare) position by position, rescales included
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
-            help_pos(root, mtab, itab, w0[j], w1[j], i + j < len, rtot, rrt, q_entry(smem, part, j, lane));
+            help_pos(root, mtab, itab, w0[j], w1[j], i + j < len, rtot, q_entry(smem, part, j, lane));
         return;
     }
     // the part's updates: counts (in position order: a repeated symbol's
@@ -944,39 +942,22 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
     uint4* dw = reinterpret_cast<uint4*>(root + kRootD);
     dw[0] = d0;
     dw[1] = d1;
-    // the entries
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t typ = w0[j] & 7, ext = w0[j] >> 16;
-        const bool en = i + j < len;
-        uint32_t un, ct, tt, un2, ct2, tt2;
-        sub_interval((w0[j] >> 3) & 63, (w0[j] >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
-        const uint32_t fb = typ == 5 ? w1[j] : ext;
-        sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un2, ct2, tt2);
-        const bool e1 = en && typ != 0, e2 = en && (typ == 4 || typ == 5);
-        const double r1 = rcp64(e1 ? tt : 1u), r0 = e0[j] ? (j == 0 ? rrt : rcp64(rt[j])) : 1.0;
-        const uint32_t u1 = e1 ? un : 0u, c1 = e1 ? ct : 1u;
-        const uint32_t u2 = e2 ? un2 : 0u, c2 = e2 ? ct2 : 1u, t2 = e2 ? tt2 : 0u;
-        const uint32_t u0 = e0[j] ? 1 + under[j] : 0u, c0 = e0[j] ? 1 + cnt[j] : 1u;
-        const uint64_t b1 = static_cast<uint64_t>(__double_as_longlong(r1)), b0 = static_cast<uint64_t>(__double_as_longlong(r0));
-        uint4* qe = reinterpret_cast<uint4*>(q_entry(smem, part, j, lane));
-        qe[0] = make_uint4(static_cast<uint32_t>(b1), static_cast<uint32_t>(b1 >> 32), static_cast<uint32_t>(b0),
-                           static_cast<uint32_t>(b0 >> 32));
-        qe[1] = make_uint4(u1 | c1 << 16, u0 | c0 << 16, u2 | c2 << 16, t2);
-    }
+    for (uint32_t j = 0; j < 4; ++j)
+        *reinterpret_cast<uint4*>(q_entry(smem, part, j, lane)) = make_uint4(w0[j], w1[j], under[j] | cnt[j] << 16, rt[j]);
     rtot = t;
-    rrt = rcp64(t);
 }
 
-// coder: one position from its entry
-DEV void code_pos(CodeState& k, Ring& o, const uint4& qa, const uint4& qb, uintptr_t dummy)
+// coder: one position from its entry (record words; the root's under,
+// count and total at the position)
+DEV void code_pos(CodeState& k, Ring& o, const uint4& qe, bool en, uintptr_t dummy)
 {
     const uint32_t n0 = o.n;
-    const double r1 = __longlong_as_double(static_cast<long long>(static_cast<uint64_t>(qa.y) << 32 | qa.x));
-    const double r0 = __longlong_as_double(static_cast<long long>(static_cast<uint64_t>(qa.w) << 32 | qa.z));
-    code(k.low, k.range, qb.x & 0xFFFF, qb.x >> 16, r1, o);
-    if (any_lane(qb.w != 0)) code(k.low, k.range, qb.z & 0xFFFF, qb.z >> 16, rcp64(max(qb.w, 1u)), o);
-    code(k.low, k.range, qb.y & 0xFFFF, qb.y >> 16, r0, o);
+    const Pre p = prep(qe.x, qe.y, en);
+    const double r0 = rcp64(p.e0 ? qe.w : 1u);
+    code(k.low, k.range, p.u1, p.c1, p.r1, o);
+    if (any_lane(p.e2)) code(k.low, k.range, p.u2, p.c2, p.r2, o);
+    code(k.low, k.range, p.e0 ? 1 + (qe.z & 0xFFFF) : 0u, p.e0 ? 1 + (qe.z >> 16) : 1u, r0, o);
     ring_store(o);                                    // the chunk read back a step ago
     ring_chunk(o, n0, dummy);
 }
@@ -1010,32 +991,37 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
             root3_clear<true>(root, R);
         }
         uint32_t rtot = 1 + 256;
-        double rrt = rcp64(rtot);
         // records: a part is two 16-B chunks; two register sets, each reloaded
         // right after its part is queued with the part two ahead
         uint4 x0 = gload16(base), x1 = gload16(min(base + 16, slot_last));
         uint4 y0 = gload16(min(base + 32, slot_last)), y1 = gload16(min(base + 48, slot_last));
         __builtin_amdgcn_s_waitcnt(0);
         // part 0 before the loop
-        help_part(root, mtab, itab, x0, x1, 0, len, rtot, rrt, smem, 0, lane);
+        help_part(root, mtab, itab, x0, x1, 0, len, rtot, smem, 0, lane);
         x0 = gload16(min(base + 64, slot_last));
         x1 = gload16(min(base + 80, slot_last));
         lds_barrier();
+        C2P_DECL
         for (uint32_t s = 0; s < parts; s += 2) {
             // part s + 1 (set y) while the coders drain part s
             uint32_t i = 4 * (s + 1);
-            help_part(root, mtab, itab, y0, y1, i, len, rtot, rrt, smem, s + 1, lane);
+            help_part(root, mtab, itab, y0, y1, i, len, rtot, smem, s + 1, lane);
             y0 = gload16(min(base + 32 * (s + 3), slot_last));
             y1 = gload16(min(base + 32 * (s + 3) + 16, slot_last));
+            C2P_WORK
             lds_barrier();
+            C2P_WAIT
             if (s + 1 >= parts) break;
             // part s + 2 (set x) while the coders drain part s + 1
             i = 4 * (s + 2);
-            help_part(root, mtab, itab, x0, x1, i, len, rtot, rrt, smem, s + 2, lane);
+            help_part(root, mtab, itab, x0, x1, i, len, rtot, smem, s + 2, lane);
             x0 = gload16(min(base + 32 * (s + 4), slot_last));
             x1 = gload16(min(base + 32 * (s + 4) + 16, slot_last));
+            C2P_WORK
             lds_barrier();
+            C2P_WAIT
         }
+        C2P_FLUSH(8)
         return;
     }
     // coder
@@ -1050,18 +1036,22 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     CodeState k;
     k.rtot = 0; k.rrt = 0.0; k.low = 0; k.range = ~0u;
     lds_barrier();                                    // part 0 queued
+    C2P_DECL
     for (uint32_t s = 0; s < parts; ++s) {
-        const uint4* q0 = reinterpret_cast<const uint4*>(q_entry(smem, s, 0, lane));
-        const uint4* q1 = reinterpret_cast<const uint4*>(q_entry(smem, s, 1, lane));
-        const uint4* q2 = reinterpret_cast<const uint4*>(q_entry(smem, s, 2, lane));
-        const uint4* q3 = reinterpret_cast<const uint4*>(q_entry(smem, s, 3, lane));
-        const uint4 a0 = q0[0], b0 = q0[1], a1 = q1[0], b1 = q1[1], a2 = q2[0], b2 = q2[1], a3 = q3[0], b3 = q3[1];
-        code_pos(k, o, a0, b0, dummy);
-        code_pos(k, o, a1, b1, dummy);
-        code_pos(k, o, a2, b2, dummy);
-        code_pos(k, o, a3, b3, dummy);
+        const uint4 q0 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 0, lane));
+        const uint4 q1 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 1, lane));
+        const uint4 q2 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 2, lane));
+        const uint4 q3 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 3, lane));
+        const uint32_t i = 4 * s;
+        code_pos(k, o, q0, i < len, dummy);
+        code_pos(k, o, q1, i + 1 < len, dummy);
+        code_pos(k, o, q2, i + 2 < len, dummy);
+        code_pos(k, o, q3, i + 3 < len, dummy);
+        C2P_WORK
         lds_barrier();                                // (the helpers may overwrite this part now)
+        C2P_WAIT
     }
+    C2P_FLUSH(10)
     ring_store(o);
     ring_chunk(o, o.n, dummy);                        // (nothing new: the next store goes to the dummy)
     // flush, compress.c:139-146

@@ -40,3 +40,7 @@ ctot = sum(buf[8 + k] for k in range(8))
 for k, nm in enumerate(cnames):
     print(f"code {nm:22s} {buf[8 + k] / steps:8.0f} cycles/wave-step  {100.0 * buf[8 + k] / max(ctot, 1):5.1f} %")
 print(f"code {'total':22s} {ctot / steps:8.0f} cycles/wave-step")
+# the two-wavefront code pass (rc_enc2_code2): per wavefront and part of 4 positions
+parts = (n // 64) * 1200 / 4
+print(f"code2 helper work {buf[8] / parts:7.0f}  barrier wait {buf[9] / parts:7.0f} cycles/wave-part")
+print(f"code2 coder  work {buf[10] / parts:7.0f}  barrier wait {buf[11] / parts:7.0f} cycles/wave-part")
