@@ -681,6 +681,30 @@ DEV Pre prep(uint32_t w0, uint32_t w1, bool en)
     return p;
 }
 
+// prep with the reciprocals of the sub-context totals (<= 5 * 63 + 2 * 63)
+// from an LDS table instead of computed
+constexpr uint32_t kRcpTab = 5 * 63 + 2 * 63 + 1;
+DEV Pre prep_tab(uint32_t w0, uint32_t w1, bool en, const double* rtab)
+{
+    Pre p;
+    const uint32_t typ = w0 & 7, ext = w0 >> 16;
+    uint32_t un, ct, tt, un2, ct2, tt2;
+    sub_interval((w0 >> 3) & 63, (w0 >> 9) & 63, ext & 63, (ext >> 6) & 63, typ == 2 || typ == 6, un, ct, tt);
+    const uint32_t fb = typ == 5 ? w1 : ext;
+    sub_interval(fb & 63, (fb >> 6) & 63, (fb >> 12) & 63, (fb >> 18) & 63, typ == 5, un2, ct2, tt2);
+    const bool e1 = en && typ != 0;
+    p.e2 = en && (typ == 4 || typ == 5);
+    p.e0 = en && (typ <= 1 || typ == 3 || typ == 4);
+    p.u1 = e1 ? un : 0u;
+    p.c1 = e1 ? ct : 1u;
+    p.r1 = rtab[e1 ? tt : 1u];
+    p.u2 = p.e2 ? un2 : 0u;
+    p.c2 = p.e2 ? ct2 : 1u;
+    p.r2 = rtab[p.e2 ? tt2 : 1u];
+    p.v = w1 >> 24;
+    return p;
+}
+
 struct CodeState {
     uint32_t low, range, rtot;
     double rrt;                 // rcp64(rtot)
@@ -845,10 +869,11 @@ constexpr uint32_t kQPart = 4;                                   // positions pe
 constexpr uint32_t kQEntry = 16;                                 // bytes per queued position
 constexpr uint32_t kC2Mtab = 256 * kCodeLds;                     // helper roots, then tables
 constexpr uint32_t kC2Itab = kC2Mtab + 256;
-constexpr uint32_t kC2Ring = kC2Itab + 512;                      // coder rings, 32 B per packet
+constexpr uint32_t kC2Ring = kC2Itab + 544;                      // (row 16 of the increment table: zeros); coder rings, 32 B per packet
 constexpr uint32_t kC2Queue = kC2Ring + 256 * 32;                // [2 parts][kQPart][256 packets] entries
 constexpr uint32_t kC2Max = kC2Queue + 2 * kQPart * 256 * kQEntry;   // the block's longest packet
-constexpr uint32_t kC2Lds = kC2Max + 16;
+constexpr uint32_t kC2Rcp = kC2Max + 16;                         // rcp64 of the sub-context totals
+constexpr uint32_t kC2Lds = kC2Rcp + 8 * kRcpTab;
 
 // barrier for the block's LDS traffic only (a workgroup fence would also wait
 // for the helpers' record loads and the coders' output stores)
@@ -904,7 +929,7 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
         v[j] = w1[j] >> 24;
         e0[j] = i + j < len && root_codes(w0[j]);
         lk[j] = root3_lookup_read(root, mtab, v[j]);
-        const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (v[j] >> 4));
+        const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (e0[j] ? v[j] >> 4 : 16u));   // (row 16: no update)
         inc[j][0] = ip[0];
         inc[j][1] = ip[1];
     }
@@ -935,9 +960,8 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
         if (e0[j]) root[v[j]] = static_cast<uint8_t>(cnt[j] + kRootDelta);
-        const uint32_t m = e0[j] ? 0xFFFFFFFFu : 0u;
-        d0.x += inc[j][0].x & m; d0.y += inc[j][0].y & m; d0.z += inc[j][0].z & m; d0.w += inc[j][0].w & m;
-        d1.x += inc[j][1].x & m; d1.y += inc[j][1].y & m; d1.z += inc[j][1].z & m; d1.w += inc[j][1].w & m;
+        d0.x += inc[j][0].x; d0.y += inc[j][0].y; d0.z += inc[j][0].z; d0.w += inc[j][0].w;
+        d1.x += inc[j][1].x; d1.y += inc[j][1].y; d1.z += inc[j][1].z; d1.w += inc[j][1].w;
     }
     uint4* dw = reinterpret_cast<uint4*>(root + kRootD);
     dw[0] = d0;
@@ -950,10 +974,10 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
 
 // coder: one position from its entry (record words; the root's under,
 // count and total at the position)
-DEV void code_pos(CodeState& k, Ring& o, const uint4& qe, bool en, uintptr_t dummy)
+DEV void code_pos(CodeState& k, Ring& o, const uint4& qe, bool en, const double* rtab, uintptr_t dummy)
 {
     const uint32_t n0 = o.n;
-    const Pre p = prep(qe.x, qe.y, en);
+    const Pre p = prep_tab(qe.x, qe.y, en, rtab);
     const double r0 = rcp64(p.e0 ? qe.w : 1u);
     code(k.low, k.range, p.u1, p.c1, p.r1, o);
     if (any_lane(p.e2)) code(k.low, k.range, p.u2, p.c2, p.r2, o);
@@ -969,10 +993,14 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     const uint8_t* mtab = smem + kC2Mtab;
     const uint8_t* itab = smem + kC2Itab;
     uint32_t* bmax = reinterpret_cast<uint32_t*>(smem + kC2Max);
+    double* rtab = reinterpret_cast<double*>(smem + kC2Rcp);
+    if (threadIdx.x < kRcpTab) rtab[threadIdx.x] = rcp64(max(threadIdx.x, 1u));
     const bool helper = threadIdx.x >= 256;
     const uint32_t lane = threadIdx.x & 255;               // the block's packet
     if (threadIdx.x < 16) root3_mask_init(smem + kC2Mtab, threadIdx.x);
     if (threadIdx.x < 16) root3_inc_init(smem + kC2Itab, threadIdx.x);
+    if (threadIdx.x == 16)
+        reinterpret_cast<uint4*>(smem + kC2Itab)[32] = reinterpret_cast<uint4*>(smem + kC2Itab)[33] = make_uint4(0u, 0u, 0u, 0u);
     if (threadIdx.x == 0) *bmax = 0;
     const uint32_t idx = e.lo + blockIdx.x * 256 + lane;
     const uintptr_t base = reinterpret_cast<uintptr_t>(e.stream) + static_cast<size_t>(min(idx, e.hi - 1) - e.lo) * e.slot_bytes;
@@ -1043,10 +1071,10 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
         const uint4 q2 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 2, lane));
         const uint4 q3 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 3, lane));
         const uint32_t i = 4 * s;
-        code_pos(k, o, q0, i < len, dummy);
-        code_pos(k, o, q1, i + 1 < len, dummy);
-        code_pos(k, o, q2, i + 2 < len, dummy);
-        code_pos(k, o, q3, i + 3 < len, dummy);
+        code_pos(k, o, q0, i < len, rtab, dummy);
+        code_pos(k, o, q1, i + 1 < len, rtab, dummy);
+        code_pos(k, o, q2, i + 2 < len, rtab, dummy);
+        code_pos(k, o, q3, i + 3 < len, rtab, dummy);
         C2P_WORK
         lds_barrier();                                // (the helpers may overwrite this part now)
         C2P_WAIT
