@@ -300,7 +300,11 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         PROF(9)
 #endif
         if (!fwd) bk_from(rw, epoch, B);
+#ifdef DEC4_NO_OUT
+        o.pend = false;                               // (timing experiment: output not stored)
+#else
         sink_flush(o);
+#endif
         src_fill(in, true);
         PROF(0)
         const uint32_t nd = live_dwords(bk_k(B.h));

@@ -1129,6 +1129,10 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     const uint64_t slot = rc_hip_enc2_slot_bytes(b->max_len ? b->max_len : 4096);
     uint64_t per = ws->enc2_cap / slot;
     if (per == 0) return static_cast<int>(hipErrorInvalidValue);
+    // chunks of whole code-pass rounds (one 256-packet block per CU): a chunk
+    // of 1.5 rounds costs the code pass two rounds of its longest packets
+    const uint64_t round = static_cast<uint64_t>(ws->cus ? ws->cus : 256) * 256;
+    if (per < b->n && per > round) per -= per % round;
     E2Params e;
     e.stream = static_cast<uint8_t*>(ws->enc2_stream);
     e.slot_bytes = slot;
