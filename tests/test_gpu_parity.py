@@ -485,3 +485,38 @@ def test_host_batches_around_checksummed_datagrams(coder):
     for i in range(0, len(dg), 97):
         assert enc[i] == datagram_encode(dg[i], True, seeds[i], port)
     host_round()
+
+
+_CHUNK_CASE = {}
+
+
+def test_encoder_chunks_vs_oracle(coder):
+    """More packets than one record-stream chunk: at max_len 1392 the 1-GB
+    stream (rc_host.c ENC2_STREAM_MAX) holds ~96 Ki packet slots, rounded down
+    to whole code-pass rounds (rc_enc2.hip rc_hip_enc2_launch), so 100000 ragged
+    packets run as two chunks over the length-binned order.  Bit-exact against
+    the oracle (batch digest), then the round trip."""
+    from oracle.pyoracle import compress_batch as ocompress, fnv_digest
+    if not _CHUNK_CASE:
+        d, o, l = synth.mixed_batch(100000, seed=synth.SEED ^ 0x43484B53)
+        out, oo, cap, ol = ocompress(d, o, l, "port")
+        _CHUNK_CASE.update(d=d, o=o, l=l, cap=cap, digest=fnv_digest(out, oo, ol), total=int(ol.sum()))
+    c = _CHUNK_CASE
+    n = len(c["l"])
+    din, doff, dlen = _dev(c["d"], torch.uint8), _dev(c["o"], torch.int64), _dev(c["l"], torch.int32)
+    cap = _dev(c["cap"], torch.int32)
+    coff = torch.zeros(n, dtype=torch.int64, device="cuda")
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+    cout = torch.empty(int(coff[-1] + cap[-1]), dtype=torch.uint8, device="cuda")
+    clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=int(c["l"].max()))
+    torch.cuda.synchronize()
+    cl = clen.cpu().numpy().astype(np.uint32)
+    assert int(cl.sum()) == c["total"]
+    assert fnv_digest(cout.cpu().numpy(), coff.cpu().numpy().astype(np.uint64), cl) == c["digest"]
+    dout = torch.empty_like(din)
+    dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    coder.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
+    torch.cuda.synchronize()
+    assert torch.equal(dl, dlen)
+    assert torch.equal(dout, din)
