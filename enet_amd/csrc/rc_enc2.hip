@@ -125,6 +125,8 @@ struct ScanLds {
     uint32_t dummy[4];                // target of the atomics of lanes past the packet's end
     uint32_t xmask[256];              // ranks of the bucket's exceptional positions (bit min(rank, 31))
     uint8_t  xlist[256];              // buckets with one
+    uint32_t fb[32];                  // packets for the lane kernels, not yet listed
+    uint32_t nfb;
 };
 
 // element word: pos (0-10) | v (11-18) | a | 256 (19-27, 0 for position 1) |
@@ -141,12 +143,6 @@ DEV uint32_t wave_incl_scan(uint32_t x)
         x += l >= d ? y : 0u;
     }
     return x;
-}
-
-DEV void fallback(const E2Params& e, uint32_t* slot, uint32_t pkt)
-{
-    slot[0] = kSkipFallback;
-    e.list[atomicAdd(e.count, 1u)] = pkt;
 }
 
 DEV bool bit_at(const uint32_t* m, uint32_t i) { return (m[i >> 5] >> (i & 31)) & 1; }
@@ -168,6 +164,35 @@ DEV void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+}
+
+// The wavefront's packets for the lane kernels are listed 32 at a time: one
+// global atomic per 32 packets instead of one per packet (a batch of low-
+// entropy packets sends every packet there, and atomics on one address
+// serialise).
+DEV void fb_flush(ScanLds& s, const E2Params& e, uint32_t t)
+{
+    wave_sync();
+    const uint32_t k = s.nfb;
+    if (k == 0) return;
+    uint32_t base = 0;
+    if (t == 0) base = atomicAdd(e.count, k);
+    base = __shfl(base, 0, 64);
+    if (t < k) e.list[base + t] = s.fb[t];
+    wave_sync();
+    if (t == 0) s.nfb = 0;
+    wave_sync();
+}
+
+DEV void fb_add(ScanLds& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uint32_t t)
+{
+    if (t == 0) {
+        slot[0] = kSkipFallback;
+        s.fb[s.nfb] = pkt;
+        s.nfb = s.nfb + 1;
+    }
+    wave_sync();
+    if (s.nfb == 32) fb_flush(s, e, t);
 }
 
 // one predecessor u of an element (v, akey): SWAR accumulators
@@ -357,15 +382,17 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
     // across instructions (gfx950 does, tools/atomorder.hip); without it
     // every position takes the full statistics and every bucket is sorted.
     const bool ordered = lane_order_probe(s.probe, t) && !e.slow;
+    if (t == 0) s.nfb = 0;
     ScanPf pf = scan_prefetch(b, e, e.lo + blockIdx.x);
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const ScanPf cur = pf;
         const uint32_t pkt = cur.pkt, n = cur.n, mis = cur.mis;
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
         if (n == 0 || n > kE2MaxLen) {                 // compress.c:257 / possible model reset
-            if (t == 0) {
-                if (n == 0) { slot[0] = kSkipDone; b.out_len[pkt] = 0; }
-                else fallback(e, slot, pkt);
+            if (n == 0) {
+                if (t == 0) { slot[0] = kSkipDone; b.out_len[pkt] = 0; }
+            } else {
+                fb_add(s, e, slot, pkt, t);
             }
             pf = scan_prefetch(b, e, idx + gridDim.x);
             continue;
@@ -402,6 +429,15 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
                 atomicAdd(ok[m] ? &s.cnt[key[m] >> 8] : &s.dummy[0], 1u);
                 old[m] = atomicOr(ok[m] ? &s.seen[key[m] >> 5] : &s.dummy[1], 1u << (key[m] & 31));
             }
+            if (i == 1 + t) {
+                // after the first 256 positions: a bucket already past kE2Bucket
+                // sends the packet to the lane kernels now (the check below);
+                // low-entropy packets would otherwise count on through
+                // same-address atomics that serialise (C3: 7x this loop's time)
+                wave_sync();
+                const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
+                if (any_lane(max(max(c4.x, c4.y), max(c4.z, c4.w)) > kE2Bucket)) break;
+            }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m)
                 if (ok[m] && (old[m] & (1u << (key[m] & 31)))) {
@@ -417,7 +453,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
         const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
         if (any_lane(mx > kE2Bucket)) {
-            if (t == 0) fallback(e, slot, pkt);
+            fb_add(s, e, slot, pkt, t);
             pf = scan_prefetch(b, e, idx + gridDim.x);
             continue;
         }
@@ -523,6 +559,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         wave_sync();                              // LDS reuse by the next packet
         E2P(5)
     }
+    fb_flush(s, e, t);
     E2P_FLUSH
 }
 

@@ -15,7 +15,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 lib = get_lib()
 lib.rc_enc2_prof_read.restype = C.c_int
 lib.rc_enc2_prof_read.argtypes = [C.c_void_p, C.c_int]
-d, o, l = synth.random_batch(n, 1200)
+d, o, l = (synth.gamestate_batch if len(sys.argv) > 2 and sys.argv[2] == "c3" else synth.random_batch)(n, 1200)
 din = torch.from_numpy(d).cuda()
 doff = torch.from_numpy(o.astype("int64")).cuda()
 dlen = torch.from_numpy(l.astype("int32")).cuda()
