@@ -345,14 +345,22 @@ DEV bool dense_search(const uint8_t* blk, uint32_t code, bool links, Dense& z, u
     return inside && cnt != 0 && code < base + cnt;
 }
 
-// compress.c:90-112 on a dense context; returns sum of the halved counts
+// compress.c:90-112 on a dense context; returns sum of the halved counts.
+// All 16 group loads are issued before any of them is used: one memory round
+// trip (the compiler otherwise interleaves them with the stores four at a
+// time, each batch behind a vmcnt(0): four round trips, taken on ~1/3 of the
+// wavefront-steps of a game-state batch, where some lane rescales).
 DEV uint32_t dense_rescale(uint8_t* blk)
 {
     uint4* p = reinterpret_cast<uint4*>(blk);
     uint32_t sum = 0, cw[8];
+    uint4 qs[16];
+#pragma unroll
+    for (uint32_t g = 0; g < 16; ++g) qs[g] = p[2 + g];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t g = 0; g < 16; ++g) {
-        uint4 q = p[2 + g];
+        uint4 q = qs[g];
         q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
         q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
         q.z -= (q.z >> 1) & 0x7F7F7F7Fu;

@@ -20,6 +20,7 @@ inline uint32_t host_sad_u8(uint32_t a, uint32_t b, uint32_t acc)
 }
 #define __builtin_amdgcn_sad_u8 host_sad_u8
 #define __builtin_amdgcn_s_waitcnt(x) ((void) 0)
+#define __builtin_amdgcn_sched_barrier(x) ((void) 0)
 #define __builtin_amdgcn_ballot_w64(p) ((unsigned long long) ((p) ? 1 : 0))
 using std::min;
 using std::max;
