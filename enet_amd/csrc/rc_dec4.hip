@@ -253,6 +253,40 @@ DEV void bk_insert(Bucket& B, uint32_t nd, uint32_t pos, uint32_t a, uint32_t v,
     B.h += en ? hadd : 0u;
 }
 
+// dec_code (rc_lane_common.h) for a code applied after the step's record load
+// is issued: its rare path shifts in bytes from the lookahead and the current
+// chunk (registers) and advances to the next chunk -- a load, then a wait for
+// all loads, the record's included -- only where both are used up.
+DEV void dec_code_late(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count,
+                       ByteSrc& in, bool en)
+{
+    low = en ? low + under * range : low;
+    range = en ? range * count : range;
+    const uint32_t k = en ? settled_bytes(low, range) : 0u;
+    const bool fast = k <= in.na;
+    const uint32_t kk = fast ? k : 0u;
+    code = src_shift_in(in, code, kk);
+    low <<= 8 * kk;
+    range <<= 8 * kk;
+    bool more = en && (!fast || range < kBot);
+    if (rare_lane(more)) {
+        bool loaded = false;
+        do {
+            const bool carry = (low ^ (low + range)) >= kTop;
+            const bool stop = carry && range >= kBot;
+            more = more && !stop;
+            if (!any_lane(more)) break;
+            range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
+            if (rare_lane(more && in.na == 0 && in.q == 4)) { src_adv(in); loaded = true; }
+            src_fill(in, more && in.na == 0);
+            code = src_shift_in(in, code, more ? 1u : 0u);
+            range = more ? range << 8 : range;
+            low = more ? low << 8 : low;
+        } while (rare_lane(more));
+        if (loaded) __builtin_amdgcn_s_waitcnt(0);        // (see dec_code)
+    }
+}
+
 DEV void bail(const rc_workspace_dev& ws, uint32_t pkt)
 {
     const uint32_t slot = atomicAdd(&ws.counters[3], 1u);
@@ -329,7 +363,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         }
         PROF(2)
         // root, compress.c:570-596
-        uint32_t cnt0 = 0;
+        uint32_t cnt0 = 0, under0 = 0;
         if (at < 0) {
             const uint32_t cd = dec_read_d(range, low, code, rtot, rrt);
             if (cd < 1) { dec_code(low, code, range, 0, 1, in, true); break; }   // end of stream
@@ -338,7 +372,7 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             v = root3_search(root, R, cd - 1, under, cnt);
             new0 = cnt == 0;
             cnt0 = cnt;
-            dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
+            under0 = under;
             at = 0;                                  // (the root's update: after the load below)
         }
         // the next step's bucket: this one when v == p (updated below), else a
@@ -351,8 +385,10 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         __builtin_amdgcn_s_sleep(DEC4_PAD);           // (timing experiment: compute added before the load)
 #endif
         raw4_load(reg, nfwd ? kDummyRec : kO1Base + v * kRec4, rw);
-        // the root's update (compress.c:586-595): only the next step's root
-        // READ needs it, so it runs in the shadow of the load (+2.9 %)
+        // the root's code and update (compress.c:583-595): only the next
+        // step's READs need them, so they run in the shadow of the load
+        // (+2.9 % and +1.9 % decompress, same-box A/B)
+        dec_code_late(low, code, range, 1 + under0, 1 + cnt0, in, at == 0);
         if (at == 0) {
             root3_add<false>(root, R, v, cnt0);
             rtot = (rtot + kRootDelta) & 0xFFFF;
