@@ -196,11 +196,11 @@ DEV void bk_rank(const Bucket& B, uint32_t nd, uint32_t u, uint32_t& lt, uint32_
 }
 
 // compress.c:536-568 in one sub-context: READ, then an escape (false) or the
-// member the code selects (true; v, with its interval decoded).  fail: the
-// code is past the context's symbols (compress.c:416).  The members with the
-// selected value form the run of the run mask that holds it.
+// member the code selects (true; v and its member index j: the caller codes
+// its interval, hit_interval, after issuing the next record load).  fail: the
+// code is past the context's symbols (compress.c:416).
 DEV bool sub_decode(const Bucket& B, uint32_t g, uint32_t t, uint32_t dd, double rtot, uint32_t& low,
-                    uint32_t& code, uint32_t& range, ByteSrc& in, uint32_t& v, bool& fail)
+                    uint32_t& code, uint32_t& range, ByteSrc& in, uint32_t& v, uint32_t& j, bool& fail)
 {
     const uint32_t esc = kSubEscDelta * dd, tot = esc + kSubDelta * t;
     const uint32_t cd = dec_read_d(range, low, code, tot, rtot);
@@ -210,15 +210,23 @@ DEV bool sub_decode(const Bucket& B, uint32_t g, uint32_t t, uint32_t dd, double
     }
     const uint32_t r = cd - esc;
     if (r >= kSubDelta * t) { fail = true; return false; }
-    const uint32_t j = select_bit(g, r >> 1);
+    j = select_bit(g, r >> 1);
     v = byte_at(B.v, j);
+    return true;
+}
+
+// the interval of member j's value in the sub-context of members g with
+// escapes esc: the members with that value form the run of the run mask
+// that holds j
+DEV void hit_interval(const Bucket& B, uint32_t g, uint32_t esc, uint32_t j, uint32_t& under, uint32_t& count)
+{
     const uint32_t upto = low_bits(j + 1);
     const uint32_t lo = 31u - static_cast<uint32_t>(__builtin_clz(B.run & upto));   // (bit 0 is a run start)
     const uint32_t above = B.run & ~upto & low_bits(bk_k(B.h));
     const uint32_t hi = above ? static_cast<uint32_t>(__builtin_ctz(above)) : bk_k(B.h);
     const uint32_t less = popc(g & low_bits(lo)), same = popc(g & low_bits(hi)) - less;
-    dec_code(low, code, range, esc + kSubDelta * less, kSubDelta * same, in, true);
-    return true;
+    under = esc + kSubDelta * less;
+    count = kSubDelta * same;
 }
 
 // bit pos of m gets b, bits above move up one
@@ -333,13 +341,15 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         __builtin_amdgcn_s_waitcnt(0);
         PROF(9)
 #endif
-        if (!fwd) bk_from(rw, epoch, B);
+        // (the lookahead refill and the output store need no record: issued
+        // before the wait for it)
+        src_fill(in, true);
 #ifdef DEC4_NO_OUT
         o.pend = false;                               // (timing experiment: output not stored)
 #else
         sink_flush(o);
 #endif
-        src_fill(in, true);
+        if (!fwd) bk_from(rw, epoch, B);
         PROF(0)
         const uint32_t nd = live_dwords(bk_k(B.h));
         Groups s;
@@ -349,16 +359,17 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         const double rt1 = rcp64(max(kSubEscDelta * s.d1 + kSubDelta * s.t1, 1u));
         PROF(1)
         int at = -1;
+        uint32_t hj = 0;                                             // (a hit: the member index)
         uint32_t v = 0;
         bool new0 = false;
         // order 2, then order 1: visited when the context holds elements
         // (escapes 0 < 5 * dist < total, compress.c:536-544)
         if (order >= 2 && s.t2 > 0) {
-            if (sub_decode(B, s.g2, s.t2, s.d2, rt2, low, code, range, in, v, fail)) at = 2;
+            if (sub_decode(B, s.g2, s.t2, s.d2, rt2, low, code, range, in, v, hj, fail)) at = 2;
             if (fail) break;
         }
         if (at < 0 && order >= 1 && s.t1 > 0) {
-            if (sub_decode(B, s.g1, s.t1, s.d1, rt1, low, code, range, in, v, fail)) at = 1;
+            if (sub_decode(B, s.g1, s.t1, s.d1, rt1, low, code, range, in, v, hj, fail)) at = 1;
             if (fail) break;
         }
         PROF(2)
@@ -388,7 +399,14 @@ DEV void decompress_one4(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // the root's code and update (compress.c:583-595): only the next
         // step's READs need them, so they run in the shadow of the load
         // (+2.9 % and +1.9 % decompress, same-box A/B)
-        dec_code_late(low, code, range, 1 + under0, 1 + cnt0, in, at == 0);
+        uint32_t fu = 1 + under0, fc = 1 + cnt0;             // the step's last code: root, or a hit
+        if (any_lane(at != 0)) {
+            uint32_t hu, hc;
+            hit_interval(B, at == 2 ? s.g2 : s.g1, kSubEscDelta * (at == 2 ? s.d2 : s.d1), hj, hu, hc);
+            fu = at != 0 ? hu : fu;
+            fc = at != 0 ? hc : fc;
+        }
+        dec_code_late(low, code, range, fu, fc, in, true);
         if (at == 0) {
             root3_add<false>(root, R, v, cnt0);
             rtot = (rtot + kRootDelta) & 0xFFFF;
