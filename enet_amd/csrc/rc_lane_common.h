@@ -475,7 +475,9 @@ DEV void src_adv(ByteSrc& s)
 {
     const bool adv = s.q == 4;
     if (any_lane(adv)) {
-        const uint4 m = chunk_mask_hi(s.n, s.next - 16, s.hi);
+        // (only a packet's last chunk needs its bytes past the end masked)
+        uint4 m = s.n;
+        if (rare_lane(adv && s.next > s.hi)) m = chunk_mask_hi(s.n, s.next - 16, s.hi);
         s.c.x = adv ? m.x : s.c.x; s.c.y = adv ? m.y : s.c.y;
         s.c.z = adv ? m.z : s.c.z; s.c.w = adv ? m.w : s.c.w;
         s.q = adv ? 0u : s.q;
