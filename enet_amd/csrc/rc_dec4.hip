@@ -261,40 +261,6 @@ DEV void bk_insert(Bucket& B, uint32_t nd, uint32_t pos, uint32_t a, uint32_t v,
     B.h += en ? hadd : 0u;
 }
 
-// dec_code (rc_lane_common.h) for a code applied after the step's record load
-// is issued: its rare path shifts in bytes from the lookahead and the current
-// chunk (registers) and advances to the next chunk -- a load, then a wait for
-// all loads, the record's included -- only where both are used up.
-DEV void dec_code_late(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count,
-                       ByteSrc& in, bool en)
-{
-    low = en ? low + under * range : low;
-    range = en ? range * count : range;
-    const uint32_t k = en ? settled_bytes(low, range) : 0u;
-    const bool fast = k <= in.na;
-    const uint32_t kk = fast ? k : 0u;
-    code = src_shift_in(in, code, kk);
-    low <<= 8 * kk;
-    range <<= 8 * kk;
-    bool more = en && (!fast || range < kBot);
-    if (rare_lane(more)) {
-        bool loaded = false;
-        do {
-            const bool carry = (low ^ (low + range)) >= kTop;
-            const bool stop = carry && range >= kBot;
-            more = more && !stop;
-            if (!any_lane(more)) break;
-            range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
-            if (rare_lane(more && in.na == 0 && in.q == 4)) { src_adv(in); loaded = true; }
-            src_fill(in, more && in.na == 0);
-            code = src_shift_in(in, code, more ? 1u : 0u);
-            range = more ? range << 8 : range;
-            low = more ? low << 8 : low;
-        } while (rare_lane(more));
-        if (loaded) __builtin_amdgcn_s_waitcnt(0);        // (see dec_code)
-    }
-}
-
 DEV void bail(const rc_workspace_dev& ws, uint32_t pkt)
 {
     const uint32_t slot = atomicAdd(&ws.counters[3], 1u);

@@ -707,6 +707,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         Look<6> h2;
         h1.found = 0u;
         bool new0 = false;
+        uint32_t fu = 0, fc = 1, cnt0 = 0;       // the step's last code: applied after the prefetch below
         // order 2, compress.c:529-568
         uint32_t esc2, tot2;
         o2_stats(L, esc2, tot2);
@@ -718,11 +719,11 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
                 if (cd - esc2 >= (L.info >> 8)) { fail = true; break; }
                 v = L.info & 0xFF;
                 h2.under = 0; h2.cnt = L.info >> 8;
-                dec_code(low, code, range, esc2, h2.cnt, in, true);
+                fu = esc2; fc = h2.cnt;
                 at = 2;
             } else {
                 if (!ctx_search<6, false>(reg, L.q, cd - esc2, h2, v)) { fail = true; break; }
-                dec_code(low, code, range, esc2 + h2.under, h2.cnt, in, true);
+                fu = esc2 + h2.under; fc = h2.cnt;
                 at = 2;
             }
         }
@@ -734,7 +735,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
                 dec_code(low, code, range, 0, L.cur.esc, in, true);
             } else {
                 if (!ctx_search<3, true>(reg, L.cur, cd - L.cur.esc, h1, v)) { fail = true; break; }
-                dec_code(low, code, range, L.cur.esc + h1.under, h1.cnt, in, true);
+                fu = L.cur.esc + h1.under; fc = h1.cnt;
                 at = 1;
             }
         }
@@ -747,14 +748,21 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             uint32_t under, cnt;
             v = root3_search(root, R, cd - 1, under, cnt);
             new0 = cnt == 0;
-            root3_add<false>(root, R, v, cnt);
-            dec_code(low, code, range, 1 + under, 1 + cnt, in, true);
-            rtot = (rtot + kRootDelta) & 0xFFFF;
-            if (1 + cnt > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
+            cnt0 = cnt;
+            fu = 1 + under; fc = 1 + cnt;
             at = 0;
         }
         PROF(3)
         lane_prefetch(L, reg, v);
+        // the step's last code and the root's update: only the next step
+        // needs them, so they run after the record load is issued (as in
+        // rc_dec4.hip)
+        dec_code_late(low, code, range, fu, fc, in, true);
+        if (at == 0) {
+            root3_add<false>(root, R, v, cnt0);
+            rtot = (rtot + kRootDelta) & 0xFFFF;
+            if (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
+        }
         // the patched o1 context needs v's lookup (compress.c:598-615)
         if (at == 0 && L.order >= 1) h1 = ctx_find<3, true>(reg, L.cur, v);
         if (at == 2 && L.order >= 1) h1 = ctx_find<3, true>(reg, L.cur, v);
