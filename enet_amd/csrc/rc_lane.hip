@@ -719,7 +719,7 @@ __device__ __forceinline__ uint32_t len_bin(uint32_t len)
     return RC_LEN_BINS - 1 - (b < RC_LEN_BINS - 1 ? b : RC_LEN_BINS - 1);
 }
 
-constexpr uint32_t kBinChunk = 4096;     // packets per binning workgroup (16 per thread)
+constexpr uint32_t kBinChunk = 1024;     // packets per binning workgroup (4 per thread: 64 workgroups for 64 Ki packets)
 
 // Wave-aggregated LDS histogram of one element per lane: lanes that share a
 // bin are served by one LDS atomic (uniform batches take a single pass).
