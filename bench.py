@@ -30,7 +30,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md); ~6.3 TB/s achievable
-RANDOM_RMW_CEILING_GBPS = 3900.0   # line traffic of the lane kernels' access pattern (membench MB_AHEAD)
 GIB = float(1 << 30)
 
 
@@ -48,6 +47,7 @@ def parse():
     p.add_argument("--no-crc", action="store_true", help="skip the CRC-32 kernel line")
     p.add_argument("--no-rccl", action="store_true")
     p.add_argument("--no-dgram", action="store_true", help="skip the datagram-path leg")
+    p.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (C3, C4)")
     return p.parse_args()
 
 
@@ -59,6 +59,105 @@ def make_batch(kind, n, size, rank):
     if kind == "c3":
         return synth.gamestate_batch(n, size, seed=(synth.SEED ^ 0x47414D45) + rank)
     return synth.mixed_batch(n, seed=(synth.SEED ^ 0x4D495845) + rank)
+
+
+WORKLOADS = {"c2": "C2 65536x1200B uniform-random, compress+decompress round trip",
+             "c3": "C3 65536x1200B game-state, compress+decompress round trip",
+             "c4": "C4 1Mi mixed 64-1392B random, compress+decompress round trip"}
+
+
+def run_workload(coder, dev, stream, kind, n, size, rank, steps, warmup, dist=None, world=1):
+    """One workload: W untimed round trips, then K timed ones bracketed by
+    (barrier +) synchronize.  Returns (raw timings, summary dict)."""
+    import torch
+    d, o, l = make_batch(kind, n, size, rank)
+    n = len(l)
+    max_len = int(l.max())
+    din = torch.from_numpy(d).to(dev)
+    doff = torch.from_numpy(o.astype(np.int64)).to(dev)
+    dlen = torch.from_numpy(l.astype(np.int32)).to(dev)
+    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+    coff = torch.zeros(n, dtype=torch.int64, device=dev)
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+    cout = torch.empty(int(coff[-1] + cap[-1]), dtype=torch.uint8, device=dev)
+    clen = torch.zeros(n, dtype=torch.int32, device=dev)
+    dout = torch.empty_like(din)
+    dl = torch.zeros(n, dtype=torch.int32, device=dev)
+    in_bytes = int(l.sum(dtype=np.uint64))
+
+    # size the decoder's bound from the actual compressed lengths
+    coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=max_len, stream=stream)
+    torch.cuda.synchronize()
+    dec_max_len = int(clen.max().item())
+    lanes = [0, 0]
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=max_len, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        coder.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=dec_max_len, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness guard for the timed configuration, and the packets each
+    # direction's fast kernel handed to the lane kernels
+    ok = bool(torch.equal(dl, dlen)) and bool(torch.equal(dout, din))
+    comp_bytes = int(clen.to(torch.int64).sum().item())
+    lanes[1] = coder.last_lane_count()
+    coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=max_len, stream=stream)
+    lanes[0] = coder.last_lane_count()
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_comp = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+    t_dec = sum(e[1].elapsed_time(e[2]) for e in events) / steps / 1e3
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    # roofline of the dominant kernel (whichever direction is slower): its
+    # algorithmic bytes per launch -- compress reads N + offsets, writes C +
+    # lengths; decompress reads C + offsets, writes N + lengths (SURVEY.md
+    # §8d: 2(N+C) per round trip) -- over its HIP-event time on the stream
+    # it runs on (the direction's fast kernel plus the empty lane/exact launches)
+    meta = n * (8 + 4 + 8 + 4 + 4)
+    alg = in_bytes + comp_bytes + meta
+    dom_is_dec = t_dec >= t_comp
+    t_dom = t_dec if dom_is_dec else t_comp
+    achieved = alg / t_dom / 1e9
+    kname = dominant_kernel(dom_is_dec, lanes[1] if dom_is_dec else lanes[0], n)
+    roofline = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "alg_bytes_per_launch": alg,
+                "launch_ms": round(t_dom * 1e3, 4)}
+    summary = {
+        "workload": WORKLOADS[kind], "packets": n, "value": round(in_bytes * world * steps / elapsed / GIB, 4),
+        "unit": "GiB/s", "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+        "bit_exact_roundtrip": ok, "compression_ratio": round(comp_bytes / in_bytes, 5),
+        "compress_GiBps": round(in_bytes / t_comp / GIB, 4), "decompress_GiBps": round(in_bytes / t_dec / GIB, 4),
+        "compress_ms": round(t_comp * 1e3, 4), "decompress_ms": round(t_dec * 1e3, 4),
+        "lane_handoff": {"compress": lanes[0], "decompress": lanes[1]},
+        "roofline": roofline,
+    }
+    raw = dict(d=d, o=o, l=l, din=din, doff=doff, dlen=dlen, in_bytes=in_bytes, n=n, max_len=max_len,
+               elapsed=elapsed, t_dom=t_dom, kname=kname)
+    return raw, summary
 
 
 def main():
@@ -76,121 +175,47 @@ def main():
 
     from enet_amd import RangeCoder
 
-    d, o, l = make_batch(args.workload, args.packets, args.size, rank)
-    n = len(l)
-    max_len = int(l.max())
-    din = torch.from_numpy(d).to(dev)
-    doff = torch.from_numpy(o.astype(np.int64)).to(dev)
-    dlen = torch.from_numpy(l.astype(np.int32)).to(dev)
-    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
-    coff = torch.zeros(n, dtype=torch.int64, device=dev)
-    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
-    cout = torch.empty(int(coff[-1] + cap[-1]), dtype=torch.uint8, device=dev)
-    clen = torch.zeros(n, dtype=torch.int32, device=dev)
-    dout = torch.empty_like(din)
-    dl = torch.zeros(n, dtype=torch.int32, device=dev)
     coder = RangeCoder()
     stream = torch.cuda.current_stream(dev)
-    in_bytes = int(l.sum(dtype=np.uint64))
-
-    # size the decoder's LDS staging from the actual compressed lengths
-    coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=max_len, stream=stream)
-    torch.cuda.synchronize()
-    dec_max_len = int(clen.max().item())
-
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=max_len, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        coder.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=dec_max_len, stream=stream)
-        if ev is not None:
-            ev[2].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    # correctness guard for the timed configuration
-    ok = bool(torch.equal(dl, dlen)) and bool(torch.equal(dout, din))
-    comp_bytes = int(clen.to(torch.int64).sum().item())
-
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    t_comp = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps / 1e3
-    t_dec = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps / 1e3
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
-
-    total_bytes = in_bytes * world * args.steps
-    value = total_bytes / elapsed / GIB
-
-    # roofline of the dominant kernel (whichever of compress/decompress is slower)
-    # algorithmic bytes per launch: compress reads N + offsets, writes C + lengths;
-    # decompress reads C + offsets, writes N + lengths (2(N+C) per round trip)
-    meta = n * (8 + 4 + 8 + 4 + 4)
-    alg_c = in_bytes + comp_bytes + meta
-    alg_d = comp_bytes + in_bytes + meta
-    dom_is_dec = t_dec >= t_comp
-    t_dom = t_dec if dom_is_dec else t_comp
-    alg = alg_d if dom_is_dec else alg_c
-    achieved = alg / t_dom / 1e9
-    kname = dominant_kernel(dom_is_dec)
-    traffic, tsrc = measured_traffic(kname, args.workload, n)
-    roofline = {
-        "kernel": kname,
-        "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "traffic_source": tsrc,
-        "alg_bytes_per_launch": alg, "launch_ms": round(t_dom * 1e3, 4),
-        "compress_ms": round(t_comp * 1e3, 4), "decompress_ms": round(t_dec * 1e3, 4),
-    }
+    raw, main_line = run_workload(coder, dev, stream, args.workload, args.packets, args.size, rank, args.steps,
+                                  args.warmup, dist if world > 1 else None, world)
+    d, o, l, din, doff, dlen = raw["d"], raw["o"], raw["l"], raw["din"], raw["doff"], raw["dlen"]
+    n, in_bytes, max_len = raw["n"], raw["in_bytes"], raw["max_len"]
+    roofline = main_line["roofline"]
+    traffic, tsrc = measured_traffic(roofline["kernel"], args.workload, n)
+    roofline["traffic"] = traffic
+    roofline["traffic_source"] = tsrc
+    roofline["compress_ms"] = main_line["compress_ms"]
+    roofline["decompress_ms"] = main_line["decompress_ms"]
     if traffic:
-        # what the kernel actually moves: PMC HBM bytes per launch / this launch time,
-        # against the peak and against the measured ceiling of its access pattern
-        # (random 128-B line read + 64-B write per record step, tools/mb/membench.hip
-        # MB_AHEAD, profiles/r1_membench_ahead.log: ~3.9 TB/s)
-        rate = traffic / t_dom / 1e9
+        # what the kernel actually moves: PMC HBM bytes per launch (a separate
+        # rocprofv3 --pmc pass of this command) over this launch time
+        rate = traffic / raw["t_dom"] / 1e9
         roofline["traffic_GBps"] = round(rate, 1)
         roofline["traffic_frac_of_peak"] = round(rate / HBM_PEAK_GBPS, 4)
-        roofline["traffic_frac_of_random_rmw_ceiling"] = round(rate / RANDOM_RMW_CEILING_GBPS, 3)
+        roofline["traffic_over_alg"] = round(traffic / roofline["alg_bytes_per_launch"], 2)
 
     result = {
         "metric": "GiB/s device-resident range-coder (de)compress, 64Ki×1200B pkts, 1/2/4/8 GPU",
-        "value": round(value, 4),
+        "value": main_line["value"],
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": main_line["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": {"c2": "C2 65536x1200B uniform-random, compress+decompress round trip",
-                                "c3": "C3 65536x1200B game-state, compress+decompress round trip",
-                                "c4": "C4 mixed 64-1392B random, compress+decompress round trip"}[args.workload],
+        "config": {"workload": WORKLOADS[args.workload],
                    "packets_per_gpu": n, "packet_bytes": args.size if args.workload != "c4" else "64-1392",
                    "parallelism": f"shard{world}", "out_cap": "2N+64"},
-        "bit_exact_roundtrip": ok,
-        "compression_ratio": round(comp_bytes / in_bytes, 5),
-        "compress_GiBps": round(in_bytes / t_comp / GIB, 4),
-        "decompress_GiBps": round(in_bytes / t_dec / GIB, 4),
+        "bit_exact_roundtrip": main_line["bit_exact_roundtrip"],
+        "compression_ratio": main_line["compression_ratio"],
+        "compress_GiBps": main_line["compress_GiBps"],
+        "decompress_GiBps": main_line["decompress_GiBps"],
+        "lane_handoff": main_line["lane_handoff"],
         "roofline": roofline,
     }
 
@@ -200,6 +225,26 @@ def main():
             result[name] = fn(*a)
         except Exception as e:  # noqa: BLE001
             result[name] = {"error": f"{type(e).__name__}: {e}"}
+
+    if world == 1 and not args.no_configs:
+        # the other single-GPU BASELINE configs, measured in the same run
+        # (C2 is the headline above); fewer steps: each is a full batch
+        def other(kind, packets):
+            del_keys = ("d", "o", "l", "din", "doff", "dlen")
+            r, summ = run_workload(coder, dev, stream, kind, packets, 1200, rank, 3, 1)
+            for k in del_keys:
+                r.pop(k, None)
+            torch.cuda.empty_cache()
+            return summ
+        cfg = {}
+        for kind, packets in (("c2", 65536), ("c3", 65536), ("c4", 1 << 20)):
+            if kind == args.workload:
+                continue
+            try:
+                cfg[kind] = other(kind, packets)
+            except Exception as e:  # noqa: BLE001
+                cfg[kind] = {"error": f"{type(e).__name__}: {e}"}
+        result["configs"] = cfg
 
     if not args.no_crc:
         leg("crc32", crc32_bench, coder, din, doff, dlen, in_bytes, n, stream)
@@ -467,15 +512,20 @@ def rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank)
                     "separate from the timed region of value"}
 
 
-def dominant_kernel(decompress):
-    """The kernel that does a direction's work in the library's configuration
-    (rc_host.c reads the same environment when a context is created)."""
-    kern = os.environ.get("ENET_RC_KERNEL", "lane3")
-    if kern in ("lane2", "wave"):
-        return ("rc_decompress_" if decompress else "rc_compress_") + {"lane2": "lane", "wave": "wave"}[kern]
+def dominant_kernel(decompress, handed_off=0, n=1):
+    """The kernel that does most of a direction's work in the library's
+    configuration (rc_host.c / rc_enc2.hip read the same environment): the
+    fast kernel, or the lane kernel when the fast kernel handed most packets
+    to it (C3 today)."""
+    if os.environ.get("ENET_RC_KERNEL", "lane3") == "wave":
+        return "rc_decompress_wave" if decompress else "rc_compress_wave"
     if decompress:
-        return "rc_decompress_dec4" if os.environ.get("ENET_RC_DEC4", "1") != "0" else "rc_decompress_lane3"
-    return "rc_enc2_code" if os.environ.get("ENET_RC_ENC2", "1") != "0" else "rc_compress_lane3"
+        fast = os.environ.get("ENET_RC_DEC4", "1") != "0"
+        return "rc_decompress_dec4" if fast and 2 * handed_off < n else "rc_decompress_lane3"
+    if os.environ.get("ENET_RC_ENC2", "1") == "0" or 2 * handed_off >= n:
+        return "rc_compress_lane3"
+    one = os.environ.get("ENET_RC_ENC2_CODE1") == "1" or os.environ.get("ENET_RC_ENC2_LANES") == "32"
+    return "rc_enc2_code" if one else "rc_enc2_code2"
 
 
 def measured_traffic(kernel, workload, packets):
@@ -498,23 +548,35 @@ def measured_traffic(kernel, workload, packets):
 
 def cpu_baseline(d, o, l, threads):
     """Reference compress.c (oracle/_ref, built from the reference sources) or,
-    if absent, the oracle restatement, timed round trip on host cores."""
+    if absent, the oracle restatement, timed round trip on host cores: on one
+    thread over a bounded sample (the first 8192 packets of the batch), and
+    on `threads` threads (one context each; the GPU box's CPU share is 16,
+    os.cpu_count() there reports the whole machine) over the whole batch."""
     from oracle.pyoracle import cpu_roundtrip, have_reference
     kind = "reference" if have_reference() else "port"
     threads = max(1, min(threads, os.cpu_count() or 1))
-    n = len(l)
-    r = cpu_roundtrip(d, o, l, threads, kind=kind)
-    nb = float(l.sum(dtype=np.uint64))
-    t = r["t_compress"] + r["t_decompress"]
     try:
         model = [x for x in open("/proc/cpuinfo").read().splitlines() if x.startswith("model name")][0].split(":")[1].strip()
     except Exception:
         model = "unknown"
-    return {"value": round(nb / t / GIB, 5), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} packets x {int(l.max())} B (the same synthetic batch), one context per thread",
-            "compress_GiBps": round(nb / r["t_compress"] / GIB, 5),
-            "decompress_GiBps": round(nb / r["t_decompress"] / GIB, 5),
-            "mismatches": int(r["mismatches"]), "cpu": model}
+
+    def one(m, k):
+        r = cpu_roundtrip(d, o[:m], l[:m], k, kind=kind)
+        nb = float(l[:m].sum(dtype=np.uint64))
+        t = r["t_compress"] + r["t_decompress"]
+        return {"value": round(nb / t / GIB, 5), "cores": k, "packets": int(m),
+                "compress_GiBps": round(nb / r["t_compress"] / GIB, 5),
+                "decompress_GiBps": round(nb / r["t_decompress"] / GIB, 5),
+                "mismatches": int(r["mismatches"])}
+
+    single = one(min(len(l), 8192), 1)
+    multi = one(len(l), threads)
+    return {"value": multi["value"], "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"{len(l)} packets x {int(l.max())} B (the bench batch) on {threads} threads, one context "
+                      f"per thread; single_thread: its first {single['packets']} packets on one thread",
+            "compress_GiBps": multi["compress_GiBps"], "decompress_GiBps": multi["decompress_GiBps"],
+            "mismatches": multi["mismatches"] + single["mismatches"], "single_thread": single,
+            "host_cpus_visible": os.cpu_count(), "cpu": model}
 
 
 if __name__ == "__main__":

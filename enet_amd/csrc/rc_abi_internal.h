@@ -1,6 +1,6 @@
 /*
  * rc_abi_internal.h -- descriptors shared by the C host shim (rc_host.c) and
- * the HIP launch code (rc_kernels.hip).  Plain C, plain pointers.
+ * the HIP launch code (rc_kernels.hip, rc_route.hip).  Plain C, plain pointers.
  */
 #ifndef ENET_RC_ABI_INTERNAL_H
 #define ENET_RC_ABI_INTERNAL_H
@@ -52,8 +52,9 @@ typedef struct {
     void     *enc2_stream;  /* NULL: the encoder is off (ENET_RC_ENC2=0) or not allocated yet */
     uint64_t  enc2_cap;     /* bytes */
     uint32_t *enc2_list;    /* [n_cap] */
-    /* bucket-history decoder (rc_dec4.hip) in front of the v3 lane decoder; the packets it
-       leaves go to enc2_list / counters[3] (ENET_RC_DEC4=0: off) */
+    /* bucket-history decoder in front of the v3 lane decoder: 5 = rc_dec5.hip (speculative
+       steps), 4 = rc_dec4.hip, 0 = off (ENET_RC_DEC=5|4|0; ENET_RC_DEC4=0: off); the packets it
+       leaves go to enc2_list / counters[3] */
     uint32_t  dec4;
     /* test switch (ENET_RC_ENC2_SLOW=1): the scan takes its slow paths (every position
        exceptional, every bucket sorted and re-walked) */
@@ -66,7 +67,6 @@ typedef struct {
 #define RC_SMALL_AUTO 0xFFFFFFFFu
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */
-#define RC_KERNEL_LANE 0u   /* one packet per lane, model v2 (rc_lane.hip) */
 #define RC_KERNEL_WAVE 1u   /* one packet per wavefront */
 #define RC_KERNEL_LANE3 2u  /* one packet per lane, model v3 (rc_lane3.hip, default) */
 
@@ -87,10 +87,17 @@ int rc_hip_enc2_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *
  * regions; packets off its fast path are listed in ws->enc2_list, count in
  * ws->counters[3]. */
 int rc_hip_dec4_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
+/* The same model with speculative steps (rc_dec5.hip): the record of a step
+ * is waited for after the step is decoded, and verifies it. */
+int rc_hip_dec5_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
-uint32_t rc_hip_lane_region_bytes(uint32_t max_len);    /* model v2 */
-uint32_t rc_hip_lane3_region_bytes(uint32_t max_len);   /* model v3 */
+uint32_t rc_hip_lane3_region_bytes(uint32_t max_len);
+
+/* Whether a batch runs on the lane path (rc_route.hip: fast kernels + lane
+ * kernels, which need the lane pool and the encoder's record stream) rather
+ * than on the wavefront-per-packet kernels (rc_kernels.hip launch). */
+int rc_hip_uses_lanes(int decompress, const rc_batch_dev *b, const rc_workspace_dev *ws);
 
 /* CRC-32 of each packet (rc_crc32.hip): crc_out[i] = enet_crc32 (packet.c:143-163)
  * of in[in_off[i] .. +in_len[i]).  tables: rc_hip_crc32_table_words() words

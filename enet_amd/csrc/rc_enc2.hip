@@ -91,6 +91,7 @@ constexpr uint32_t kSkipDone = 0xFFFFFFFEu;       // empty packet, out_len alrea
 struct E2Params {
     uint8_t*        stream;     // record stream, one slot per packet of the chunk
     uint64_t        slot_bytes;
+    uint32_t        slot_len;   // longest packet a slot holds: min(max_len or 4096, kE2MaxLen)
     uint32_t        lo, hi;     // chunk: batch indices [lo, hi)
     const uint32_t* order;      // batch index -> packet (length-binned), or null
     const uint32_t* bins;       // bins[RC_LEN_BINS] != 0: order not built (uniform batch)
@@ -331,7 +332,7 @@ DEV ScanPf scan_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t idx)
     if (idx < e.hi) {
         f.pkt = (e.order && !const_load(e.bins, RC_LEN_BINS)) ? const_load(e.order, idx) : idx;
         f.n = const_load(b.in_len, f.pkt);
-        if (f.n != 0 && f.n <= kE2MaxLen) {
+        if (f.n != 0 && f.n <= e.slot_len) {
             const uintptr_t src = reinterpret_cast<uintptr_t>(b.in + const_load(b.in_off, f.pkt));
             const uintptr_t a16 = src & ~static_cast<uintptr_t>(15);
             f.mis = static_cast<uint32_t>(src & 15);
@@ -388,7 +389,9 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const ScanPf cur = pf;
         const uint32_t pkt = cur.pkt, n = cur.n, mis = cur.mis;
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
-        if (n == 0 || n > kE2MaxLen) {                 // compress.c:257 / possible model reset
+        // compress.c:257 / possible model reset, or longer than the caller's
+        // max_len (its slot holds 8 B per position up to slot_len only)
+        if (n == 0 || n > e.slot_len) {
             if (n == 0) {
                 if (t == 0) { slot[0] = kSkipDone; b.out_len[pkt] = 0; }
             } else {
@@ -516,8 +519,28 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             }
         }
         const uint32_t x0 = x[0];
-        const bool disorder = !ordered;                // (wave-uniform)
         wave_sync();
+        // The probe above samples a few conflict patterns once per wavefront;
+        // the ranks this packet's scatter produced are checked as well: in
+        // every bucket the positions must increase (one 16-B LDS read per four
+        // elements).  A violation takes the sorted path below.
+        bool bad = false;
+        if (ordered) {
+#pragma unroll 1
+            for (uint32_t r = 0; r < 4; ++r) {
+                const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
+                uint32_t prev = 0;
+#pragma unroll 1
+                for (uint32_t j = 0; j < kk; j += 4) {
+                    const uint4 u = *reinterpret_cast<const uint4*>(&s.e[bs + j]);
+                    const uint32_t p0 = u.x & 2047, p1 = u.y & 2047, p2 = u.z & 2047, p3 = u.w & 2047;
+                    bad = bad || p0 <= prev || (j + 1 < kk && p1 <= p0) || (j + 2 < kk && p2 <= p1) ||
+                          (j + 3 < kk && p3 <= p2);
+                    prev = p3;
+                }
+            }
+        }
+        const bool disorder = !ordered || any_lane(bad);   // (wave-uniform)
         pf = scan_prefetch(b, e, idx + gridDim.x);     // (the bytes in LDS are not read past here)
         E2P(3)
         // buckets with exceptional positions: compacted over the lanes, one
@@ -544,13 +567,14 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         E2P(4)
         if (rare_lane(disorder)) {
             // (not seen on gfx950) the scatter's ranks were not position
-            // order somewhere: every bucket sorted, its flags cleared, walked
-            // from its start with every record rewritten
+            // order somewhere: every bucket sorted, its flags cleared, every
+            // position exceptional (the repeat bits came from the same
+            // atomics), walked from its start with every record rewritten
             wave_sync();
 #pragma unroll 1
             for (uint32_t r = 0; r < 4; ++r) {
                 const uint32_t bs = pick4(r, s4), kk = pick4(r, c4);
-                for (uint32_t j = 0; j < kk; ++j) s.e[bs + j] &= ~(kF2 | kNV1 | kF1);
+                for (uint32_t j = 0; j < kk; ++j) s.e[bs + j] = (s.e[bs + j] & ~(kF2 | kNV1 | kF1)) | kExc;
                 sort_bucket(s, bs, bs + kk);
                 walk_from(s, bs, kk, ~0u, rec);
             }
@@ -1163,7 +1187,8 @@ extern "C" uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len)
 extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const uint64_t slot = rc_hip_enc2_slot_bytes(b->max_len ? b->max_len : 4096);
+    const uint32_t ml = b->max_len ? b->max_len : 4096;
+    const uint64_t slot = rc_hip_enc2_slot_bytes(ml);
     uint64_t per = ws->enc2_cap / slot;
     if (per == 0) return static_cast<int>(hipErrorInvalidValue);
     // chunks of whole code-pass rounds (one 256-packet block per CU): a chunk
@@ -1173,6 +1198,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     E2Params e;
     e.stream = static_cast<uint8_t*>(ws->enc2_stream);
     e.slot_bytes = slot;
+    e.slot_len = ml < kE2MaxLen ? ml : kE2MaxLen;
     e.dummy = static_cast<uint8_t*>(ws->enc2_stream) + ws->enc2_cap;   // (allocated past the stream)
     e.order = ws->order;
     e.bins = ws->bins;

@@ -30,6 +30,9 @@ extern void enet_free(void *) __attribute__((weak));
 extern void enet_host_compress(ENetHost *, const ENetCompressor *) __attribute__((weak));
 
 #define EXACT_SLOTS 256u            /* concurrent exact-path packets (64 KiB pool each) */
+#ifndef ENET_RC_DEC_DEFAULT
+#define ENET_RC_DEC_DEFAULT 4u      /* the bucket-history decoder: rc_dec4.hip (4) or rc_dec5.hip (5) */
+#endif
 
 typedef struct {
     int device;
@@ -87,8 +90,7 @@ static int ws_reserve(rc_ctx *c, size_t n)
 
 static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 {
-    uint32_t region = c->ws.kernel == RC_KERNEL_LANE3 ? rc_hip_lane3_region_bytes(max_len ? max_len : 4096)
-                                                      : rc_hip_lane_region_bytes(max_len ? max_len : 4096);
+    uint32_t region = rc_hip_lane3_region_bytes(max_len ? max_len : 4096);
     const char *ov = getenv("ENET_RC_REGION");      /* diagnostic: smaller regions (overflows take the exact path) */
     if (ov && atoi(ov) > 0 && (uint32_t) atoi(ov) < region) region = ((uint32_t) atoi(ov) + 255) & ~255u;
     size_t slots = n < c->max_slots ? n : c->max_slots;
@@ -100,7 +102,7 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
     c->ws.lane_pool = NULL; c->ws.lane_slots = 0; c->ws.lane_region = 0;
     if (hipMalloc(&c->ws.lane_pool, slots * (size_t) region) != hipSuccess) return -1;
-    /* lane regions start at epoch 0: no order-1 record is live (rc_lane.hip) */
+    /* lane regions start at epoch 0: no order-1 record is live (rc_lane3.hip) */
     if (hipMemset(c->ws.lane_pool, 0, slots * (size_t) region) != hipSuccess) return -1;
     /* hipMemset runs on the null stream, which the context's non-blocking
      * stream (and a caller's) does not wait for: finish it before any kernel */
@@ -113,15 +115,20 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 }
 
 /* Record stream of the two-pass encoder (rc_enc2.hip): one slot per packet,
- * at most ENC2_STREAM_MAX bytes (larger batches run in chunks). */
+ * at most ENC2_STREAM_MAX bytes (larger batches run in whole code-pass rounds
+ * of chunks; ENET_RC_ENC2_STREAM_MB=m caps it lower).  Reserved only for
+ * batches that take the lane path (run_device). */
 #define ENC2_STREAM_MAX (1ull << 30)
 
 static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 {
     if (!c->enc2_on || c->ws.kernel != RC_KERNEL_LANE3) return 0;
     const uint64_t slot = rc_hip_enc2_slot_bytes(max_len ? max_len : 4096);
+    uint64_t cap = ENC2_STREAM_MAX;
+    const char *mb = getenv("ENET_RC_ENC2_STREAM_MB");
+    if (mb && atol(mb) > 0 && (uint64_t) atol(mb) << 20 < cap) cap = (uint64_t) atol(mb) << 20;
     uint64_t want = (uint64_t) n * slot;
-    if (want > ENC2_STREAM_MAX) want = ENC2_STREAM_MAX > slot ? ENC2_STREAM_MAX : slot;
+    if (want > cap) want = cap > slot ? cap : slot;
     if (want <= c->ws.enc2_cap) return 0;
     hipDeviceSynchronize();
     if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
@@ -175,7 +182,6 @@ void *enet_range_coder_create(void)
         const char *k = getenv("ENET_RC_KERNEL");
         c->ws.kernel = RC_KERNEL_LANE3;
         if (k && strcmp(k, "wave") == 0) c->ws.kernel = RC_KERNEL_WAVE;
-        if (k && strcmp(k, "lane2") == 0) c->ws.kernel = RC_KERNEL_LANE;
         const char *a = getenv("ENET_RC_LANES");
         c->ws.lane_active = 64;
         if (a && (atoi(a) == 32 || atoi(a) == 16)) c->ws.lane_active = (uint32_t) atoi(a);
@@ -189,8 +195,10 @@ void *enet_range_coder_create(void)
         c->ws.cus = (uint32_t) cus;
         const char *e2 = getenv("ENET_RC_ENC2");
         c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
-        const char *d4 = getenv("ENET_RC_DEC4");
-        c->ws.dec4 = !(d4 && strcmp(d4, "0") == 0);
+        const char *d4 = getenv("ENET_RC_DEC4"), *dv = getenv("ENET_RC_DEC");
+        c->ws.dec4 = ENET_RC_DEC_DEFAULT;
+        if (dv && (strcmp(dv, "4") == 0 || strcmp(dv, "5") == 0 || strcmp(dv, "0") == 0)) c->ws.dec4 = (uint32_t) atoi(dv);
+        if (d4 && strcmp(d4, "0") == 0) c->ws.dec4 = 0;
         const char *es = getenv("ENET_RC_ENC2_SLOW");
         c->ws.enc2_slow = (es && strcmp(es, "1") == 0) ? 1u : 0u;
         const char *sl = getenv("ENET_RC_SLOTS");
@@ -238,14 +246,18 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     if (n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
     if (ws_reserve(c, n) != 0) return (int) hipErrorOutOfMemory;
-    if (c->ws.kernel != RC_KERNEL_WAVE && lanes_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
-    if (!decompress && enc2_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
     rc_batch_dev b;
     b.in = in; b.in_off = in_off; b.in_len = in_len;
     b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;
     b.n = (uint32_t) n;
     b.max_len = max_len;
     b.max_out = max_out;
+    /* the lane pool and the encoder's record stream only for batches that run
+     * on the lane path (small batches run on the wave kernel without them) */
+    if (rc_hip_uses_lanes(decompress, &b, &c->ws)) {
+        if (lanes_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
+        if (!decompress && enc2_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
+    }
     /* stream is a hipStream_t; NULL is HIP's default (null) stream */
     return decompress ? rc_hip_decompress(&b, &c->ws, stream) : rc_hip_compress(&b, &c->ws, stream);
 }

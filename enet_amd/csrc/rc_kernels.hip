@@ -1089,12 +1089,11 @@ uint32_t lds_bytes_for(uint32_t max_len)
 extern "C" uint32_t rc_hip_lds_bytes(uint32_t max_len) { return lds_bytes_for(max_len); }
 
 extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
-                                  void* stream);   // rc_lane.hip
+                                  void* stream);   // rc_route.hip
 
 extern "C" const char* rc_hip_fast_kernel_name(int decompress, uint32_t kernel)
 {
     if (kernel == RC_KERNEL_WAVE) return decompress ? "rc_decompress_wave" : "rc_compress_wave";
-    if (kernel == RC_KERNEL_LANE) return decompress ? "rc_decompress_lane" : "rc_compress_lane";
     return decompress ? "rc_decompress_lane3" : "rc_compress_lane3";
 }
 
@@ -1113,20 +1112,15 @@ uint32_t wave_lds(bool decompress, uint32_t max_len, uint32_t max_out)
     return static_cast<uint32_t>(total & ~15ull);
 }
 
-static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
+// Batches that fit on the chip in one wave per packet (the per-datagram
+// drop-in calls and a live host's send / receive passes among them) go to
+// the wavefront-per-packet kernel: a packet's byte chain runs there with
+// its model in LDS, 1.4-2.9x sooner than on one lane of the lane kernels
+// (tools/smallbatch.py).  Larger batches are throughput work: lanes.
+static bool small_batch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t& lds_w)
 {
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    if (b->n == 0) return 0;
-    if (b->n > ws->n_cap) return static_cast<int>(hipErrorInvalidValue);
-    hipError_t err = hipMemsetAsync(ws->counters, 0, 4 * sizeof(uint32_t), st);
-    if (err != hipSuccess) return static_cast<int>(err);
     const uint32_t max_len = b->max_len ? b->max_len : 4096;
-    // Batches that fit on the chip in one wave per packet (the per-datagram
-    // drop-in calls and a live host's send / receive passes among them) go to
-    // the wavefront-per-packet kernel: a packet's byte chain runs there with
-    // its model in LDS, 1.4-2.9x sooner than on one lane of the lane kernels
-    // (tools/smallbatch.py).  Larger batches are throughput work: lanes.
-    const uint32_t lds_w = wave_lds(decompress, max_len, b->max_out);
+    lds_w = wave_lds(decompress, max_len, b->max_out);
     // The decoder caps at 4 wavefronts per CU: with a right-sized model 5 fit,
     // but 1280 random packets then decode slower than on the lanes (5.9 vs
     // 3.9 ms, profiles/r1h_smallbatch.log).
@@ -1135,11 +1129,29 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     const uint32_t resident = ws->cus * per_cu;
     // (not min(): on the host it resolves to the int overload, and small_max
     // RC_SMALL_AUTO would read as -1)
-    const bool small = ws->kernel == RC_KERNEL_LANE3 && b->n <= resident && b->n <= ws->small_max;
+    return ws->kernel == RC_KERNEL_LANE3 && b->n <= resident && b->n <= ws->small_max;
+}
+
+extern "C" int rc_hip_uses_lanes(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws)
+{
+    uint32_t lds_w;
+    return ws->kernel != RC_KERNEL_WAVE && !small_batch(decompress != 0, b, ws, lds_w);
+}
+
+static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (b->n == 0) return 0;
+    if (b->n > ws->n_cap) return static_cast<int>(hipErrorInvalidValue);
+    hipError_t err = hipMemsetAsync(ws->counters, 0, 4 * sizeof(uint32_t), st);
+    if (err != hipSuccess) return static_cast<int>(err);
+    const uint32_t max_len = b->max_len ? b->max_len : 4096;
+    uint32_t lds_w;
+    const bool small = small_batch(decompress, b, ws, lds_w);
     static const bool debug = getenv("ENET_RC_DEBUG") != nullptr;
     if (debug)
-        fprintf(stderr, "enet_rc: %s n=%u max_len=%u cus=%u lds=%u resident=%u small_max=%u -> %s\n",
-                decompress ? "decompress" : "compress", b->n, max_len, ws->cus, lds_w, resident,
+        fprintf(stderr, "enet_rc: %s n=%u max_len=%u cus=%u lds=%u small_max=%u -> %s\n",
+                decompress ? "decompress" : "compress", b->n, max_len, ws->cus, lds_w,
                 ws->small_max, small || ws->kernel == RC_KERNEL_WAVE ? "wave" : "lanes");
     if (ws->kernel != RC_KERNEL_WAVE && !small) {
         const int rc = rc_hip_lane_launch(decompress ? 1 : 0, b, ws, stream);

@@ -6,7 +6,10 @@
  * four enet_range_coder_* symbols and enet_host_compress_with_range_coder
  * below have exactly the reference signatures and return conventions, so
  * host.c / protocol.c call them unchanged.  The batch entry points are new:
- * they are how the GPU is meant to be used (one wavefront per packet).
+ * they are how the GPU is meant to be used: large batches run one packet
+ * per lane (the two-pass encoder and the bucket-history decoder, then the
+ * lane kernels for what they leave), batches that fit on the chip at one
+ * wavefront per packet run on the wavefront-per-packet kernels.
  *
  * Plain C, plain pointers and sizes; no HIP or torch types appear here
  * (streams are passed as void*).
@@ -49,8 +52,8 @@ typedef struct _ENetAddress { enet_uint32 host; enet_uint16 port; } ENetAddress;
  * distinct contexts are independent.
  *
  * Read once here from the environment (all optional):
- *   ENET_RC_KERNEL=wave|lane2   force the wavefront-per-packet kernels, or the
- *                               v2 lane kernels (default: v3 lane kernels)
+ *   ENET_RC_KERNEL=wave         force the wavefront-per-packet kernels
+ *                               (default: the lane path above)
  *   ENET_RC_SMALL_BATCH=n       batches of up to n packets (and no more than
  *                               fit on the chip at one wavefront each) run on
  *                               the wavefront-per-packet kernels; 0 = never;

@@ -1,30 +1,24 @@
-// TEST ONLY: host build of rc_lane.hip's per-lane compress/decompress.
+// TEST ONLY: host build of the lane kernels' per-lane compress/decompress
+// (rc_lane3.hip) and, with -DDEC4 / -DDEC5, the bucket-history decoders
+// (rc_dec4.hip, rc_dec5.hip).
 #define RC_LANE_HOST_TEST 1
 #include <stdlib.h>
 #include <string.h>
-#ifdef LANE3
 #include "../../enet_amd/csrc/rc_lane3.hip"
 #ifdef DEC4
 #include "../../enet_amd/csrc/rc_dec4.hip"
 #endif
+#ifdef DEC5
+#include "../../enet_amd/csrc/rc_dec5.hip"
+#endif
 #define REGION_BYTES rc_hip_lane3_region_bytes
 #define COMPRESS_ONE compress_one3
 #define DECOMPRESS_ONE decompress_one3
-#else
-#include "../../enet_amd/csrc/rc_lane.hip"
-#define REGION_BYTES rc_hip_lane_region_bytes
-#define COMPRESS_ONE compress_one
-#define DECOMPRESS_ONE decompress_one
-#endif
 
 static uint8_t g_root[304] __attribute__((aligned(16)));
-#ifdef LANE3
 static uint8_t g_mtab[256] __attribute__((aligned(16)));
 static bool g_mtab_init = [] { for (uint32_t j = 0; j < 16; ++j) root3_mask_init(g_mtab, j); return true; }();
 #define COMPRESS_ARGS , g_mtab
-#else
-#define COMPRESS_ARGS
-#endif
 
 extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t cap,
                              uint32_t max_len, uint32_t* out_len)
@@ -47,6 +41,15 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     if (decompress) {
         uint32_t wbail = 0;
         decompress_one4(b, ws, 0, region, g_root, &wbail);
+        if (!counters[3]) return 0;
+    }
+#endif
+#ifdef DEC5
+    // the speculative bucket-history decoder first, likewise
+    if (decompress) {
+        static uint8_t g_t[256];
+        uint32_t wbail = 0;
+        decompress_one5(b, ws, 0, region, g_root, g_t, &wbail);
         if (!counters[3]) return 0;
     }
 #endif

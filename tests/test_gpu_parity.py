@@ -27,8 +27,6 @@ VARIANTS = {
     "enc2-slow": {"ENET_RC_KERNEL": "lane3", "ENET_RC_ENC2_SLOW": "1"},
     # the v3 lane kernels alone, both directions
     "lane3-only": {"ENET_RC_KERNEL": "lane3", "ENET_RC_ENC2": "0", "ENET_RC_DEC4": "0"},
-    # model v2 (rc_lane.hip)
-    "lane2": {"ENET_RC_KERNEL": "lane2"},
 }
 
 
@@ -51,6 +49,7 @@ def coder(request):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+    c.variant = request.param
     yield c
     c.close()
 
@@ -128,7 +127,11 @@ def test_per_call_reference_surface(coder):
     assert coder.decompress(b"", 100) == (0, b"")
 
 
-def _digest_roundtrip(coder, name, batch):
+def _digest_roundtrip(coder, name, batch, lanes=None):
+    """Digest + round trip at full size.  lanes = (compress, decompress): the
+    packets the fast kernels (rc_enc2.hip, rc_dec4.hip) must hand to the lane
+    kernels on the default configuration; a fast path that starts bailing
+    silently would pass every parity check and only lose speed."""
     from oracle.pyoracle import fnv_digest
     d, o, l = batch
     g = golden_io.digests()[name]
@@ -141,6 +144,10 @@ def _digest_roundtrip(coder, name, batch):
     clen = torch.zeros(n, dtype=torch.int32, device="cuda")
     coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=int(l.max()))
     torch.cuda.synchronize()
+    routed = getattr(coder, "variant", "") == "lane3" and lanes is not None
+    if routed:
+        assert coder.last_lane_count() == lanes[0], "encoder fast path hand-off"
+        assert coder.last_exact_count() == 0
     cl = clen.cpu().numpy().astype(np.uint32)
     assert int(cl.sum()) == g["out_bytes"]
     assert fnv_digest(cout.cpu().numpy(), coff.cpu().numpy().astype(np.uint64), cl) == g["digest"]
@@ -149,6 +156,9 @@ def _digest_roundtrip(coder, name, batch):
     dl = torch.zeros(n, dtype=torch.int32, device="cuda")
     coder.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
     torch.cuda.synchronize()
+    if routed:
+        assert coder.last_lane_count() == lanes[1], "decoder fast path hand-off"
+        assert coder.last_exact_count() == 0
     assert torch.equal(dl, dlen)
     assert torch.equal(dout, din)
 
@@ -158,7 +168,8 @@ def test_c1_digest(coder):
 
 
 def test_c2_digest_full_size(coder):
-    _digest_roundtrip(coder, "C2_random_65536x1200", synth.random_batch(65536, 1200))
+    # every C2 packet stays on the fast kernels, both directions
+    _digest_roundtrip(coder, "C2_random_65536x1200", synth.random_batch(65536, 1200), lanes=(0, 0))
 
 
 def test_c3_digest_full_size(coder):
@@ -171,11 +182,41 @@ def test_c4_mixed_sizes_vs_oracle(coder):
     out, oo, cap, ol = ocompress(d, o, l, "port")
     packets = [d[int(o[i]): int(o[i]) + int(l[i])].tobytes() for i in range(len(l))]
     res = _run(coder, False, packets, [int(c) for c in cap])
+    if getattr(coder, "variant", "") == "lane3":                 # random C4 packets: all on the fast encoder
+        assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
     gl = np.array([r[0] for r in res], np.uint32)
     assert np.array_equal(gl, ol)
     blob = np.frombuffer(b"".join(r[1] for r in res), np.uint8)
     goff = np.concatenate([[0], np.cumsum(gl[:-1].astype(np.uint64))]).astype(np.uint64)
     assert fnv_digest(blob, goff, gl) == fnv_digest(out, oo, ol)
+    back = _run(coder, True, [r[1] for r in res], [len(p) for p in packets])
+    if getattr(coder, "variant", "") == "lane3":                 # ... and on the fast decoder
+        assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
+    assert all(b == (len(p), p) for b, p in zip(back, packets))
+
+
+def test_max_len_below_packet_lengths(coder):
+    """A batch's max_len hint below some of its packets' lengths: the
+    encoder's record slots are sized by max_len, so the longer packets must
+    go to the lane kernels (whose arena, also sized by max_len, sends what
+    outgrows it to the exact path) -- never past their slot.  Bit-exact
+    against the oracle, then back with the same kind of hint."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(404)
+    pk = []
+    for i in range(8192):
+        n = int(rng.integers(1, 1900)) if i % 3 else int(rng.integers(1, 300))
+        alpha = int(rng.choice([3, 40, 256]))
+        pk.append(rng.integers(0, alpha, size=n).astype(np.uint8).tobytes())
+    caps = [2 * len(p) + 64 for p in pk]
+    res = _run(coder, False, pk, caps, max_len=300)
+    want = [port.compress(p, out_limit=c) for p, c in zip(pk, caps)]
+    bad = [i for i, (r, w) in enumerate(zip(res, want)) if r != w]
+    assert not bad, bad[:10]
+    back = _run(coder, True, [r[1] for r in res], [len(p) for p in pk], max_len=200)
+    bad = [i for i, (b, p) in enumerate(zip(back, pk)) if b != (len(p), p)]
+    assert not bad, bad[:10]
 
 
 def test_protocol_out_limit_mode(coder):

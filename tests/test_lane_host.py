@@ -1,5 +1,6 @@
-"""Host (CPU) build of the lane kernel's per-lane logic (enet_amd/csrc/rc_lane.hip
-compiled with tests/proto/lane_host_shim.h) against the reference fixtures.
+"""Host (CPU) build of the lane kernels' per-lane logic (enet_amd/csrc/rc_lane3.hip,
+and the bucket-history decoder rc_dec4.hip in front of it, compiled with
+tests/proto/lane_host_shim.h) against the reference fixtures.
 
 The lane kernel is scalar code per lane, so its model and coder logic can be
 exercised here without a GPU; the -m gpu tests then check the real kernel."""
@@ -16,17 +17,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "tests", "proto", "liblanehost.so")
 
 
-# v4: the bucket-history decoder (rc_dec4.hip) in front of the v3 lanes, as on the GPU
-@pytest.fixture(scope="module", params=["v2", "v3", "v4"])
+# v3: the lane kernels alone; v4 / v5: the bucket-history decoder (rc_dec4.hip / the speculative
+# rc_dec5.hip) in front of them, as on the GPU
+@pytest.fixture(scope="module", params=["v3", "v4", "v5"])
 def lane(request):
-    so = SO if request.param == "v2" else SO.replace("liblanehost", "liblanehost" + request.param[1])
+    so = SO.replace("liblanehost", "liblanehost" + request.param[1])
     csrc = os.path.join(ROOT, "enet_amd", "csrc")
     src = [os.path.join(ROOT, "tests", "proto", "lane_host.cpp")] + \
-        [os.path.join(csrc, f) for f in ("rc_lane.hip", "rc_lane3.hip", "rc_dec4.hip", "rc_lane_common.h",
-                                         "rc_root3.h")]
+        [os.path.join(csrc, f) for f in ("rc_lane3.hip", "rc_dec4.hip", "rc_dec5.hip", "rc_bucket4.h",
+                                         "rc_lane_common.h", "rc_root3.h")]
     if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in src):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared"] +
-                              {"v2": [], "v3": ["-DLANE3"], "v4": ["-DLANE3", "-DDEC4"]}[request.param] +
+                              {"v3": [], "v4": ["-DDEC4"], "v5": ["-DDEC5"]}[request.param] +
                               ["-I", csrc, "-I", os.path.join(ROOT, "tests", "proto"), "-o", so, src[0]])
     lib = C.CDLL(so)
     lib.lane_host_run.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
@@ -53,7 +55,7 @@ def test_lane_logic_compress_fixtures(lane):
             continue
         r = lane(0, c["input"], c["out_limit"])
         if r[0] == "exact":      # (allowed only for packets long enough to reach the model reset)
-            assert lane.version != "v2" and len(c["input"]) > 1919
+            assert len(c["input"]) > 1919
             continue
         assert r[0] == c["ret"], (len(c["input"]), c["out_limit"])
         if c["ret"]:
@@ -74,7 +76,7 @@ def test_lane_logic_decompress_fixtures(lane):
         if c["ret"]:
             assert r[1] == c["expect"]
     assert 0 < exact < 2000
-    if lane.version == "v4":     # most fixtures are garbage or low-entropy: those are left to the lanes
+    if lane.version in ("v4", "v5"):     # most fixtures are garbage or low-entropy: those are left to the lanes
         assert 0 < lane.left < len(cases) - 1000, (lane.left, len(cases))
 
 
@@ -82,8 +84,8 @@ def test_dec4_takes_random_packets(lane):
     """The bucket-history decoder decodes random packets up to MTU size itself
     (no bucket reaches its 20 elements) and matches the oracle at every
     output limit edge."""
-    if lane.version != "v4":
-        pytest.skip("dec4 only")
+    if lane.version not in ("v4", "v5"):
+        pytest.skip("bucket-history decoders only")
     from oracle.pyoracle import Coder
     port = Coder("port")
     rng = np.random.default_rng(11)
@@ -102,6 +104,5 @@ def test_lane_logic_region_overflow_routes_exact(lane):
     # (v3 keeps single-symbol order-2 contexts inline, so it needs a small
     # alphabet -- many order-2 contexts with several symbols -- to fill its arena)
     data = np.random.default_rng(3).integers(0, 256, 1200, dtype=np.uint8)
-    if lane.version != "v2":
-        data &= 15
+    data &= 15
     assert lane(0, data.tobytes(), 4096, max_len=16)[0] == "exact"

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Per-phase cycle breakdown of the lane kernels (diagnostic build).
 
-    make -C enet_amd/csrc prof && python tools/lane_prof.py [c2|c3] [packets]
+    make -C enet_amd/csrc prof3 && python tools/lane_prof.py [c2|c3] [packets]
 
-Loads enet_amd/lib/libenet_rc_amd_prof.so (rc_lane.hip compiled with
+Loads enet_amd/lib/libenet_rc_amd_prof3.so (rc_lane3.hip compiled with
 -DRC_PROFILE: s_memtime stamps between the phases of a step, summed per wave)
 and prints, per phase, shader cycles per wave-step (one byte of each of the
 wave's 64 packets).  A stamp waits for outstanding LDS ops, so LDS latency is
@@ -20,13 +20,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ["ENET_RC_LIB"] = os.path.join(ROOT, "enet_amd", "lib",
-                                         os.environ.get("LANE_PROF_LIB", "libenet_rc_amd_prof.so"))
+                                         os.environ.get("LANE_PROF_LIB", "libenet_rc_amd_prof3.so"))
 
 import torch  # noqa: E402
 
 from enet_amd import RangeCoder, compress_batch, decompress_batch, get_lib, synth  # noqa: E402
 
-V3 = "3" in os.environ.get("LANE_PROF_LIB", "")
+V3 = "3" in os.environ.get("LANE_PROF_LIB", "libenet_rc_amd_prof3.so")
 COMP3 = ["top (record decode)", "o2 lookup", "o2 encode", "o1 lookup", "o1 encode", "root", "advance (updates, stores)",
          "input refill", "", "DRAIN (outstanding memory)"]
 DEC3 = ["top (record decode)", "o2 decode", "o1 decode", "root decode", "lookups", "advance (updates, stores)",
