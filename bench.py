@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--no-rccl", action="store_true")
     p.add_argument("--no-dgram", action="store_true", help="skip the datagram-path leg")
     p.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (C3, C4)")
+    p.add_argument("--no-multi", action="store_true", help="skip the multi-GPU C-ABI leg")
     return p.parse_args()
 
 
@@ -256,6 +257,16 @@ def main():
         leg("datagram_path", datagram_path, coder, dev, stream)
         leg("per_datagram_call", per_datagram_call, coder, d, o, l)
 
+    if not args.no_multi:
+        # the single-process multi-GPU C entry (enet_rc_multi_*, rc_multi.c) over
+        # every GPU of the job, driven from rank 0 (the other ranks wait)
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            leg("multi_device_c_abi", multi_device_leg, list(range(world)), din, doff, dlen, max_len, in_bytes)
+        if world > 1:
+            dist.barrier()
+
     if world > 1 and not args.no_rccl:
         try:
             rs = rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank)
@@ -272,6 +283,42 @@ def main():
     coder.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def multi_device_leg(devices, din, doff, dlen, max_len, in_bytes):
+    """enet_rc_multi_{compress,decompress}_batch_device (rc_multi.c): the
+    batch on devices[0], split by payload bytes, the other devices' ranges
+    over the peer links (xGMI), coded, packed, gathered and unpacked back.
+    Each call returns with its results in place; round trips timed on the host."""
+    import torch
+    from enet_amd import MultiCoder
+    m = MultiCoder(devices)
+    n = dlen.numel()
+    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+    coff = torch.zeros(n, dtype=torch.int64, device=din.device)
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+    cout = torch.empty(int(coff[-1] + cap[-1]), dtype=torch.uint8, device=din.device)
+    clen = torch.zeros(n, dtype=torch.int32, device=din.device)
+    dout = torch.empty_like(din)
+    dl = torch.zeros(n, dtype=torch.int32, device=din.device)
+    torch.cuda.synchronize()
+    best_c = best_d = None
+    for it in range(4):
+        t0 = time.perf_counter()
+        m.batch_device(False, din, doff, dlen, cout, coff, cap, clen, max_len=max_len)
+        t1 = time.perf_counter()
+        m.batch_device(True, cout, coff, clen, dout, doff, dlen, dl, max_len=int(clen.max().item()))
+        t2 = time.perf_counter()
+        if it:
+            best_c = min(best_c or 1e9, t1 - t0)
+            best_d = min(best_d or 1e9, t2 - t1)
+    ok = bool(torch.equal(dl, dlen)) and bool(torch.equal(dout, din))
+    m.close()
+    return {"devices": devices, "value": round(in_bytes / (best_c + best_d) / GIB, 4), "unit": "GiB/s",
+            "compress_GiBps": round(in_bytes / best_c / GIB, 4), "decompress_GiBps": round(in_bytes / best_d / GIB, 4),
+            "bit_exact_roundtrip": ok,
+            "note": "one process, one context per device; device pointers on devices[0], other ranges over "
+                    "hipMemcpyPeerAsync (xGMI); includes the offset/length D2H, splits and syncs; best of 3"}
 
 
 def crc32_bench(coder, din, doff, dlen, in_bytes, n, stream):
@@ -492,7 +539,7 @@ def rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank)
         cout = torch.empty(int(coff[-1] + cap[-1]), dtype=torch.uint8, device=dev)
         clen = torch.zeros_like(pln)
         coder.compress_batch(pay, poff, pln, cout, coff, cap, clen, max_len=max_len)
-        res, rl = shard.pack_results(cout, coff, clen)
+        res, rl = shard.pack_results(cout, coff, clen, coder=coder)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         parts = shard.gather_results(dist, res, rl)

@@ -18,7 +18,8 @@ from typing import Optional, Sequence
 
 from ._lib import ENetBuffer, get_lib
 
-__all__ = ["RangeCoder", "compress_batch", "decompress_batch", "get_lib", "ENetBuffer"]
+__all__ = ["RangeCoder", "MultiCoder", "compress_batch", "decompress_batch", "get_lib", "ENetBuffer",
+           "multi_split"]
 
 
 class RangeCoder:
@@ -204,6 +205,57 @@ class RangeCoder:
         """Packets of the last batch the first pass (two-pass encoder or
         bucket-history decoder) left to the lane kernels."""
         return int(self.lib.enet_rc_last_lane_count(self.ctx))
+
+
+def multi_split(in_len, parts: int):
+    """enet_rc_multi_split: device k codes packets [first[k], first[k+1])."""
+    import numpy as np
+    ln = np.ascontiguousarray(in_len, dtype=np.uint32)
+    first = np.zeros(parts + 1, np.uint64)
+    rc = get_lib().enet_rc_multi_split(ln.ctypes.data, len(ln), parts, first.ctypes.data)
+    if rc != 0:
+        raise ValueError("enet_rc_multi_split: bad arguments")
+    return first
+
+
+class MultiCoder:
+    """One process, several GPUs (enet_rc_multi_*, rc_multi.c): a context per
+    listed device; batches split by payload bytes across them."""
+
+    def __init__(self, devices: Sequence[int]):
+        self.lib = lib = get_lib()
+        arr = (C.c_int * len(devices))(*devices)
+        self.ctx = lib.enet_rc_multi_create(arr, len(devices))
+        if not self.ctx:
+            raise RuntimeError(f"enet_rc_multi_create({list(devices)}) failed")
+
+    def close(self):
+        if self.ctx:
+            self.lib.enet_rc_multi_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch_host(self, decompress: bool, data, off, ln, out, out_off, out_cap, out_len):
+        """numpy arrays (uint8, uint64, uint32, uint8, uint64, uint32, uint32)."""
+        fn = self.lib.enet_rc_multi_decompress_batch_host if decompress else self.lib.enet_rc_multi_compress_batch_host
+        p = lambda a: a.ctypes.data  # noqa: E731
+        rc = fn(self.ctx, p(data), p(off), p(ln), len(ln), p(out), p(out_off), p(out_cap), p(out_len))
+        if rc != 0:
+            raise RuntimeError(f"enet_rc_multi host batch failed: HIP error {rc}")
+
+    def batch_device(self, decompress: bool, inp, in_off, in_len, out, out_off, out_cap, out_len, max_len=0):
+        """torch tensors on the first listed device (the batch's dtypes as RangeCoder.compress_batch)."""
+        fn = self.lib.enet_rc_multi_decompress_batch_device if decompress else \
+            self.lib.enet_rc_multi_compress_batch_device
+        rc = fn(self.ctx, inp.data_ptr(), in_off.data_ptr(), in_len.data_ptr(), in_len.numel(), int(max_len),
+                out.data_ptr(), out_off.data_ptr(), out_cap.data_ptr(), out_len.data_ptr())
+        if rc != 0:
+            raise RuntimeError(f"enet_rc_multi device batch failed: HIP error {rc}")
 
 
 def _caps_offsets(caps):

@@ -71,6 +71,23 @@ def _load() -> C.CDLL:
     lib.enet_rc_socket_send_batch.argtypes = [C.c_int, vp, vp, vp, vp, sz]
     lib.enet_rc_crc32.restype = u32
     lib.enet_rc_crc32.argtypes = [C.POINTER(ENetBuffer), sz]
+    lib.enet_rc_multi_create.restype = vp
+    lib.enet_rc_multi_create.argtypes = [vp, sz]
+    lib.enet_rc_multi_destroy.restype = None
+    lib.enet_rc_multi_destroy.argtypes = [vp]
+    lib.enet_rc_multi_devices.restype = sz
+    lib.enet_rc_multi_devices.argtypes = [vp]
+    lib.enet_rc_multi_split.restype = C.c_int
+    lib.enet_rc_multi_split.argtypes = [vp, sz, sz, vp]
+    for name, args in (("enet_rc_multi_compress_batch_host", batch_host),
+                       ("enet_rc_multi_decompress_batch_host", batch_host),
+                       ("enet_rc_multi_compress_batch_device", batch_dev[:-1]),
+                       ("enet_rc_multi_decompress_batch_device", batch_dev[:-1])):
+        f = getattr(lib, name)
+        f.restype = C.c_int
+        f.argtypes = args
+    lib.enet_rc_pack_batch_device.restype = C.c_int
+    lib.enet_rc_pack_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
     lib.enet_rc_last_exact_count.restype = u32
     lib.enet_rc_last_exact_count.argtypes = [vp]
     lib.enet_rc_last_lane_count.restype = u32

@@ -139,6 +139,9 @@ int rc_hip_dgram_launch(int stage, const rc_dgram_dev *g, void *stream);
  * packed (rc_pack.hip); bsum: ceil(n / 1024) + 1 words, bsum[last] = total. */
 int rc_hip_pack(const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len, uint32_t n,
                 uint64_t *bsum, uint8_t *packed, void *stream);
+/* The reverse: packed (back to back) -> out[out_off[i] .. +out_len[i]). */
+int rc_hip_unpack(const uint8_t *packed, uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
+                  uint32_t n, uint64_t *bsum, void *stream);
 
 /* Kernel introspection for bench/profiling. */
 const char *rc_hip_fast_kernel_name(int decompress, uint32_t kernel);

@@ -28,9 +28,9 @@
 // speculative step is checked against the record, so a stale or wrong T entry
 // costs a redo, never a wrong byte.
 //
-// Two records are in flight per lane (the one being verified and the next),
-// alternating between two register sets (the loop is unrolled twice: a
-// copy of a load's destination would wait for it).
+// A step's record load is issued once the step is committed, after its
+// record store, and waited for after the next step's decode: the next step's
+// speculative decode runs in its shadow.
 //
 // Fast path and hand-off as rc_dec4: buckets of at most kCap4 elements, fewer
 // than 4094 nodes, root codes within symbol 255; a lane leaving it lists its
@@ -53,6 +53,15 @@
 namespace {
 
 constexpr uint32_t kWaveBail5 = 16;          // as rc_dec4's kWaveBail
+
+#if defined(RC_LANE_HOST_TEST) && defined(DEC5_STATS)
+}  // namespace
+extern "C" { unsigned long long g_dec5_stats[4]; }   // iterations, commits, redos, redos from a stall
+namespace {
+#define DEC5_STAT(i, c) do { if (c) ++g_dec5_stats[i]; } while (0)
+#else
+#define DEC5_STAT(i, c) do { } while (0)
+#endif
 constexpr uint32_t kTUnknown = 0xFF;
 
 // T entry of a bucket from its order-1 statistics
@@ -154,9 +163,8 @@ DEV void decompress_one5(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
 
     Bucket B;                       // the step's context record when held (redo, or the last step's bucket)
     bk_empty(B, epoch);
-    Raw4 rwA, rwB;                  // records in flight (two register sets, alternating)
-    rwA.q0 = rwA.q1 = rwA.q2 = rwA.q3 = make_uint4(0u, 0u, 0u, 0u);
-    rwB = rwA;
+    Raw4 rw;                        // bucket p in flight (issued by the previous step)
+    rw.q0 = rw.q1 = rw.q2 = rw.q3 = make_uint4(0u, 0u, 0u, 0u);
     Groups S;                       // redo: the groups of B for the step being redone
     S.g2 = S.g1 = S.t2 = S.d2 = S.t1 = S.d1 = 0;
     // (words, not bools: a bool would be an SGPR lane mask)
@@ -166,12 +174,14 @@ DEV void decompress_one5(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     uint32_t order = 0, a = 0, p = 0, nodes = 1;
     bool fail = false, off = false;
 
-    // one iteration: decode step i (speculatively unless redo), issue the
-    // next bucket's load into rout, verify with bucket p (rin, issued by the
-    // previous iteration), commit or roll back.  false: the packet is done.
-    auto step = [&](Raw4& rin, Raw4& rout) -> bool {
+    // One step per iteration: (A) decode the symbol speculatively (unless
+    // redone) -- every code but the step's last; (C) wait for bucket p
+    // (issued by the previous step, a whole decode ago) and check the guess;
+    // then either roll back, or commit: the element into bucket p and its
+    // store, (B) the load of the next step's bucket, the step's last code,
+    // the root's update and the output -- in the shadow of that load.
+    for (;;) {
         src_fill(in, true);
-        sink_flush(o);
         const bool spec = redo == 0;
         const uint32_t s_low = low, s_range = range, s_code = code, s_na = in.na;
         const uint64_t s_la = in.la;
@@ -184,7 +194,7 @@ DEV void decompress_one5(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         int at = -1;
         uint32_t hj = 0, v = 0;
         bool new0 = false, lfail = false, leof = false, loff = false;
-        // order 2 (only a redone step can have its symbols), then order 1
+        // (A) order 2 (only a redone step can have its symbols), then order 1
         if (order >= 2 && !stall && s.t2 > 0) {
             if (sub_decode5(B, s.g2, s.t2, s.d2, rt2, low, code, range, in, v, hj, lfail, spec, stall)) at = 2;
         }
@@ -209,11 +219,7 @@ DEV void decompress_one5(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             }
         }
         const bool have = at >= 0 && !stall && !lfail;
-        // the next step's bucket: this one when v == p, else a load issued now
-        // (unconditional: the scratch record for lanes with none to load)
-        const bool nfwd = have && order >= 1 && v == p;
-        raw4_load(reg, (have && !nfwd) ? kO1Base + v * kRec4 : kDummyRec, rout);
-        // the step's last code: the root's, or a hit's (redo only)
+        // the interval of the step's last code: the root's, or a hit's (redo only)
         uint32_t fu = 1 + under0, fc = 1 + cnt0;
         if (any_lane(have && at != 0)) {
             uint32_t hu, hc;
@@ -221,31 +227,38 @@ DEV void decompress_one5(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             fu = at != 0 ? hu : fu;
             fc = at != 0 ? hc : fc;
         }
-        dec_code5(low, code, range, fu, fc, in, have, spec, stall);
-        // bucket p: the record issued by the previous iteration (the wait for
-        // it is here, a whole step after its load), or B
-        if (spec && !pfwd) bk_from(rin, epoch, B);
+        // (C) bucket p: the record issued by the previous step, or B.  Unpacked
+        // on every path: a load consumed on some paths only stays pending for
+        // the compiler at the merge, and the next write to its registers would
+        // wait for vmcnt(0).
+        {
+            Bucket Bn;
+            bk_from(rw, epoch, Bn);
+            const bool take = spec && !pfwd;
+            B.h = take ? Bn.h : B.h; B.hit = take ? Bn.hit : B.hit;
+            B.nw = take ? Bn.nw : B.nw; B.run = take ? Bn.run : B.run;
+#pragma unroll
+            for (int d = 0; d < 6; ++d) { B.a[d] = take ? Bn.a[d] : B.a[d]; B.v[d] = take ? Bn.v[d] : B.v[d]; }
+        }
         const uint32_t nd = live_dwords(bk_k(B.h));
         Groups g;
         bk_groups(B, nd, a, order >= 2, g);
         // the guess: no order-2 symbols, T[p] = the record's order-1 statistics
         const bool ok = !spec || (!stall && g.t2 == 0 && (order < 1 || (g.t1 == s.t1 && g.d1 == s.d1)));
+        DEC5_STAT(0, true);
+        DEC5_STAT(1, ok && have);
+        DEC5_STAT(2, !ok);
+        DEC5_STAT(3, !ok && stall);
         if (!ok) {
             // roll back and redo the step with its record
             low = s_low; range = s_range; code = s_code; in.na = s_na; in.la = s_la;
             S = g;
             redo = 1;
         }
-        if (ok && lfail) { fail = true; return false; }
-        if (ok && leof) return false;
-        if (ok && loff) { off = true; return false; }
+        if (ok && lfail) { fail = true; break; }
+        if (ok && leof) { dec_code5(low, code, range, 0, 1, in, true, false, stall); break; }   // (EOF)
+        if (ok && loff) { off = true; break; }
         const bool commit = ok && have;
-        if (commit && at == 0) {
-            root3_add<false>(root, R, v, cnt0);
-            rtot = (rtot + kRootDelta) & 0xFFFF;
-            if (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
-            rrt = rcp64(rtot);
-        }
         fail = commit && o.n >= o.cap;                               // compress.c:617
         // the element joins bucket p (compress.c:598-615); nodes as compress.c creates them
         uint32_t lt, le;
@@ -259,12 +272,30 @@ DEV void decompress_one5(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         const bool ins = commit && order >= 1;
         bk_insert(B, nd, le, a, v, (at == 2 ? 1u : 0u) | first, (n2 ? 1u : 0u) | first, lt == le ? 1u : 0u,
                   (1u << 16) + (at == 2 ? (1u << 21) : 0u) + (n1 ? (1u << 26) : 0u), ins && !full);
-        // (the step's last record operation; lanes with nothing to store write the scratch record)
+        // (stored before the next load is issued: a later wait for the store
+        // then never waits for that load; lanes with nothing to store write
+        // the scratch record)
         bk_store(reg, ins ? kO1Base + p * kRec4 : kDummyRec, B);
+        // the output window the previous step completed: also before the load
+        // (what is issued after it -- the input chunk only -- is then what the
+        // next step's wait for it waits for as well)
+        sink_flush(o);
+        // (B) the next step's bucket: this one when v == p, else a load whose
+        // latency the rest of this step and the next step's decode overlap
+        const bool nfwd = commit && order >= 1 && v == p;
+        raw4_load(reg, (commit && !nfwd) ? kO1Base + v * kRec4 : kDummyRec, rw);
         if (ins) tt[p] = static_cast<uint8_t>(t_code(g.t1 + (at != 2 ? 1u : 0u), g.d1 + (n1 ? 1u : 0u)));
+        // the step's last code, the root's update (compress.c:583-595)
+        dec_code5(low, code, range, fu, fc, in, commit, false, stall);
+        if (commit && at == 0) {
+            root3_add<false>(root, R, v, cnt0);
+            rtot = (rtot + kRootDelta) & 0xFFFF;
+            if (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
+            rrt = rcp64(rtot);
+        }
         off = full || (commit && nodes >= kNodeLimit4) || *wbail >= kWaveBail5;
-        if (fail || off) return false;
-        if (!commit) return true;                                    // redo next iteration
+        if (fail || off) break;
+        if (!commit) continue;                                       // redo next iteration
         sink_put(o, v, 1, true);
         src_adv(in);
         tcur = tt[v];
@@ -273,12 +304,6 @@ DEV void decompress_one5(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         a = p;
         p = v;
         order += order < 2 ? 1u : 0u;
-        return true;
-    };
-
-    for (;;) {
-        if (!step(rwA, rwB)) break;
-        if (!step(rwB, rwA)) break;
     }
     if (off && !fail) { atomicAdd(wbail, 1u); bail5(ws, pkt); return; }
     sink_finish(o, !fail);

@@ -22,6 +22,7 @@
 
 #include "enet_rc_amd.h"
 #include "rc_abi_internal.h"
+#include "rc_host_internal.h"
 
 /* ENet's allocator and host hook, resolved from libenet when it is linked
  * (callbacks.c:37-52, host.c:294-304). */
@@ -798,4 +799,53 @@ uint32_t enet_rc_last_exact_count(void *context)
     return v;
 }
 
-const char *enet_rc_version(void) { return "enet_rc_amd 0.1 (gfx950)"; }
+/* ------------------------------------------------------ for rc_multi.c */
+
+int rc_ctx_device(void *context) { return context ? ((rc_ctx *) context)->device : -1; }
+void *rc_ctx_stream(void *context) { return context ? (void *) ((rc_ctx *) context)->stream : NULL; }
+
+int rc_ctx_run_device(void *context, int decompress, const uint8_t *in, const uint64_t *in_off,
+                      const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                      const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len, void *stream)
+{
+    return run_device((rc_ctx *) context, decompress, in, in_off, in_len, n, max_len, 0, out, out_off, out_cap,
+                      out_len, stream);
+}
+
+int rc_ctx_run_host(void *context, int decompress, const uint8_t *in, const uint64_t *in_off,
+                    const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
+                    const uint32_t *out_cap, uint32_t *out_len)
+{
+    return run_host((rc_ctx *) context, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+}
+
+/* The context's block-sum workspace of rc_pack.hip for n packets (device
+ * pointer, ceil(n / 1024) + 1 words; the last holds the packed total). */
+uint64_t *rc_ctx_bsum(void *context, size_t n)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c || hipSetDevice(c->device) != hipSuccess) return NULL;
+    const size_t blocks = (n + 1023) / 1024;
+    if (blocks + 1 > c->d_bsum_cap) {
+        hipDeviceSynchronize();
+        if (c->d_bsum) hipFree(c->d_bsum);
+        c->d_bsum = NULL; c->d_bsum_cap = 0;
+        if (hipMalloc((void **) &c->d_bsum, (blocks + 1) * 8) != hipSuccess) return NULL;
+        c->d_bsum_cap = blocks + 1;
+    }
+    return c->d_bsum;
+}
+
+/* Packs out_len[i] bytes of each packet back to back (rc_pack.hip). */
+int enet_rc_pack_batch_device(void *context, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
+                              size_t n, uint8_t *packed, void *stream)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c || n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    uint64_t *bsum = rc_ctx_bsum(c, n);
+    if (!bsum) return (int) hipErrorOutOfMemory;
+    return rc_hip_pack(out, out_off, out_len, (uint32_t) n, bsum, packed, stream);
+}
+
+const char *enet_rc_version(void) { return "enet_rc_amd 0.3 (gfx950)"; }

@@ -71,9 +71,11 @@ extern "C" __global__ __launch_bounds__(kThreads) void rc_pack_scan(uint64_t* bs
     if (threadIdx.x == 0) bsum[nb] = carry;
 }
 
-extern "C" __global__ __launch_bounds__(kThreads)
-void rc_pack_copy(const uint8_t* out, const uint64_t* out_off, const uint32_t* len, uint32_t n,
-                  const uint64_t* bsum, uint8_t* packed)
+// UNPACK: the reverse, packed[sum of len[<i]] -> out[out_off[i]] (rc_multi.c:
+// results of another device, gathered back to back, into the root's slots)
+template <bool UNPACK>
+__device__ void pack_copy(uint8_t* out, const uint64_t* out_off, const uint32_t* len, uint32_t n,
+                          const uint64_t* bsum, uint8_t* packed)
 {
     __shared__ uint32_t s[kThreads];
     __shared__ uint32_t off[kPer];
@@ -95,8 +97,8 @@ void rc_pack_copy(const uint8_t* out, const uint64_t* out_off, const uint32_t* l
         const uint32_t i = base + k;
         if (i >= n) break;
         const uint32_t m = len[i];
-        const uint8_t* src = out + out_off[i];
-        uint8_t* dst = packed + b0 + off[k];
+        const uint8_t* src = UNPACK ? packed + b0 + off[k] : out + out_off[i];
+        uint8_t* dst = UNPACK ? out + out_off[i] : packed + b0 + off[k];
         if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
             const uint32_t w = m >> 2;
             for (uint32_t j = lane; j < w; j += 64)
@@ -106,6 +108,32 @@ void rc_pack_copy(const uint8_t* out, const uint64_t* out_off, const uint32_t* l
             for (uint32_t j = lane; j < m; j += 64) dst[j] = src[j];
         }
     }
+}
+
+extern "C" __global__ __launch_bounds__(kThreads)
+void rc_pack_copy(const uint8_t* out, const uint64_t* out_off, const uint32_t* len, uint32_t n,
+                  const uint64_t* bsum, uint8_t* packed)
+{
+    pack_copy<false>(const_cast<uint8_t*>(out), out_off, len, n, bsum, packed);
+}
+
+extern "C" __global__ __launch_bounds__(kThreads)
+void rc_unpack_copy(uint8_t* out, const uint64_t* out_off, const uint32_t* len, uint32_t n,
+                    const uint64_t* bsum, const uint8_t* packed)
+{
+    pack_copy<true>(out, out_off, len, n, bsum, const_cast<uint8_t*>(packed));
+}
+
+extern "C" int rc_hip_unpack(const uint8_t* packed, uint8_t* out, const uint64_t* out_off, const uint32_t* out_len,
+                             uint32_t n, uint64_t* bsum, void* stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) return 0;
+    const uint32_t nb = (n + kPer - 1) / kPer;
+    hipLaunchKernelGGL(rc_pack_sums, dim3(nb), dim3(kThreads), 0, st, out_len, n, bsum);
+    hipLaunchKernelGGL(rc_pack_scan, dim3(1), dim3(kThreads), 0, st, bsum, nb);
+    hipLaunchKernelGGL(rc_unpack_copy, dim3(nb), dim3(kThreads), 0, st, out, out_off, out_len, n, bsum, packed);
+    return static_cast<int>(hipGetLastError());
 }
 
 extern "C" int rc_hip_pack(const uint8_t* out, const uint64_t* out_off, const uint32_t* out_len, uint32_t n,

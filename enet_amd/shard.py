@@ -45,92 +45,111 @@ def _offsets(lengths):
     return off
 
 
+def _batch(dist, ops):
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
 def scatter_batch(dist, data, offsets, lengths, root: int = 0, device=None):
     """Scatter a packet batch held by ``root`` (``data``/``offsets``/``lengths``
     tensors; ignored on other ranks) into per-rank shards.  Every rank returns
-    its shard as (data, offsets, lengths) on ``device``."""
+    its shard as (data, offsets, lengths) on ``device``.
+
+    Two grouped rounds: every rank's header at once, then every rank's
+    lengths and payload at once -- the transfers to all ranks run together,
+    one per xGMI link, instead of one rank after another."""
     import torch
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = device if device is not None else (data.device if data is not None else torch.device("cpu"))
-    hdr = torch.zeros(2, dtype=torch.int64, device=dev)
     if rank == root:
         ln_cpu = lengths.to("cpu")
         ranges = shard_ranges(ln_cpu.numpy(), world)
-        ops, keep = [], None
         off_cpu = offsets.to("cpu")
+        hdrs, parts, keep = [], [], None
         for r, (a, b) in enumerate(ranges):
             if a < b:
                 lo = int(off_cpu[a]); hi = int(off_cpu[b - 1] + ln_cpu[b - 1])
             else:
                 lo = hi = 0
-            h = torch.tensor([b - a, hi - lo], dtype=torch.int64, device=dev)
             ln_r = lengths[a:b].to(device=dev, dtype=torch.int32).contiguous()
             pay = data[lo:hi].to(dev).contiguous()
             if r == root:
                 keep = (pay, ln_r)
                 continue
-            dist.send(h, r)
+            hdrs.append(dist.P2POp(dist.isend, torch.tensor([b - a, hi - lo], dtype=torch.int64, device=dev), r))
             if b > a:
-                ops.append(dist.P2POp(dist.isend, ln_r, r))
-                ops.append(dist.P2POp(dist.isend, pay, r))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+                parts += [dist.P2POp(dist.isend, ln_r, r), dist.P2POp(dist.isend, pay, r)]
+        _batch(dist, hdrs)
+        _batch(dist, parts)
         pay, ln_r = keep
         return pay, _offsets(ln_r), ln_r
-    dist.recv(hdr, root)
+    hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+    _batch(dist, [dist.P2POp(dist.irecv, hdr, root)])
     n, nbytes = int(hdr[0]), int(hdr[1])
     ln_r = torch.empty(n, dtype=torch.int32, device=dev)
     pay = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     if n:
-        ops = [dist.P2POp(dist.irecv, ln_r, root), dist.P2POp(dist.irecv, pay, root)]
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+        _batch(dist, [dist.P2POp(dist.irecv, ln_r, root), dist.P2POp(dist.irecv, pay, root)])
     return pay, _offsets(ln_r), ln_r
 
 
-def pack_results(out, out_off, out_len):
+def pack_results(out, out_off, out_len, coder=None):
     """Compacts per-packet results (out[out_off[i] : +out_len[i]]) into one
-    contiguous byte tensor; returns (bytes, lengths)."""
+    contiguous byte tensor; returns (bytes, lengths).  Device tensors go
+    through the library's packing kernel (rc_pack.hip,
+    enet_rc_pack_batch_device: one wavefront per packet, no per-byte index);
+    host tensors (the CPU tests) are sliced on the host."""
     import torch
     n = out_len.numel()
     if n == 0:
         return torch.empty(0, dtype=torch.uint8, device=out.device), out_len
     ln = out_len.to(torch.int64)
-    dst = _offsets(ln)
-    total = int((dst[-1] + ln[-1]).item())
-    idx = torch.repeat_interleave(out_off.to(torch.int64) - dst, ln) + torch.arange(total, device=out.device)
-    return out[idx], out_len
+    total = int(ln.sum().item())
+    packed = torch.empty(max(total, 1), dtype=torch.uint8, device=out.device)
+    if out.is_cuda:
+        if coder is None:
+            raise ValueError("pack_results on device tensors needs a RangeCoder (the packing kernel)")
+        oo = out_off.to(torch.int64).contiguous()
+        ol = out_len.to(torch.int32).contiguous()
+        stream = torch.cuda.current_stream(out.device)
+        rc = coder.lib.enet_rc_pack_batch_device(coder.ctx, out.data_ptr(), oo.data_ptr(), ol.data_ptr(), n,
+                                                 packed.data_ptr(), stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"enet_rc_pack_batch_device failed: HIP error {rc}")
+        return packed[:total], out_len
+    o, l = out_off.numpy(), out_len.numpy()
+    src = out.numpy()
+    if total:
+        packed.numpy()[:total] = np.concatenate([src[int(o[i]): int(o[i]) + int(l[i])] for i in range(n)])
+    return packed[:total], out_len
 
 
 def gather_results(dist, payload, lengths, root: int = 0):
     """Gather each rank's packed results (bytes + int32 lengths) to ``root``.
-    Returns on root a list of (payload, lengths) in rank order; None elsewhere."""
+    Returns on root a list of (payload, lengths) in rank order; None elsewhere.
+    Two grouped rounds as in scatter_batch: all headers, then all payloads."""
     import torch
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = payload.device
-    hdr = torch.tensor([lengths.numel(), payload.numel()], dtype=torch.int64, device=dev)
     if rank != root:
-        dist.send(hdr, root)
+        hdr = torch.tensor([lengths.numel(), payload.numel()], dtype=torch.int64, device=dev)
+        _batch(dist, [dist.P2POp(dist.isend, hdr, root)])
         if lengths.numel():
-            ops = [dist.P2POp(dist.isend, lengths.to(torch.int32).contiguous(), root),
-                   dist.P2POp(dist.isend, payload.contiguous(), root)]
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            _batch(dist, [dist.P2POp(dist.isend, lengths.to(torch.int32).contiguous(), root),
+                          dist.P2POp(dist.isend, payload.contiguous(), root)])
         return None
+    hdrs = {r: torch.zeros(2, dtype=torch.int64, device=dev) for r in range(world) if r != root}
+    _batch(dist, [dist.P2POp(dist.irecv, h, r) for r, h in hdrs.items()])
     parts = [None] * world
     parts[root] = (payload, lengths)
-    for r in range(world):
-        if r == root:
-            continue
-        h = torch.zeros(2, dtype=torch.int64, device=dev)
-        dist.recv(h, r)
+    ops = []
+    for r, h in hdrs.items():
         n, nb = int(h[0]), int(h[1])
         ln = torch.empty(n, dtype=torch.int32, device=dev)
         pay = torch.empty(nb, dtype=torch.uint8, device=dev)
         if n:
-            ops = [dist.P2POp(dist.irecv, ln, r), dist.P2POp(dist.irecv, pay, r)]
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            ops += [dist.P2POp(dist.irecv, ln, r), dist.P2POp(dist.irecv, pay, r)]
         parts[r] = (pay, ln)
+    _batch(dist, ops)
     return parts

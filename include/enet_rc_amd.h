@@ -192,6 +192,49 @@ int enet_rc_socket_receive_batch(int socket, uint8_t *buf, size_t slot_bytes, si
 int enet_rc_socket_send_batch(int socket, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
                               const ENetAddress *addresses, size_t n);
 
+/* ================================================================ multi-GPU
+ * One process, several GPUs (no reference counterpart).  Packets
+ * are independent (compress.c:252-265): a batch is split into contiguous
+ * packet ranges of about equal payload bytes, one per device, and every
+ * device codes its range with its own context, concurrently.  Results are
+ * exactly those of the single-device calls.
+ *
+ * enet_rc_multi_create binds one context per listed device (devices[0] is
+ * the root of the device-pointer calls; a device may be listed twice, which
+ * only makes sense for testing).  NULL on failure. */
+void *enet_rc_multi_create(const int *devices, size_t n_devices);
+void enet_rc_multi_destroy(void *multi);
+size_t enet_rc_multi_devices(void *multi);
+/* The split: device k gets packets [first[k], first[k + 1]) (first has
+ * parts + 1 entries); the smallest index whose prefix sum of in_len reaches
+ * k / parts of the total.  0, or -1 on bad arguments.  Host-only. */
+int enet_rc_multi_split(const uint32_t *in_len, size_t n, size_t parts, uint64_t *first);
+/* HOST pointers, as enet_rc_*_batch_host: one host thread per device copies
+ * its range in, codes it and copies it out; returns with the results. */
+int enet_rc_multi_compress_batch_host(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                      const uint32_t *in_len, size_t n, uint8_t *out,
+                                      const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
+int enet_rc_multi_decompress_batch_host(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                        const uint32_t *in_len, size_t n, uint8_t *out,
+                                        const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
+/* DEVICE pointers on devices[0]: every other device's range is copied to it
+ * over the peer link (hipMemcpyPeerAsync, xGMI), coded there, packed back to
+ * back and copied back, then unpacked into the root's slots (only bytes
+ * [out_off[i], +out_len[i]) are written).  Waits for the root device before
+ * starting and returns with the results in place. */
+int enet_rc_multi_compress_batch_device(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                        const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                                        const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
+int enet_rc_multi_decompress_batch_device(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                          const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                                          const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
+
+/* Packs out_len[i] bytes of each packet (at out_off[i]) back to back into
+ * packed, on the device (the gather of a batch's results before a copy);
+ * packed holds at least the sum of out_len.  Device pointers, on `stream`. */
+int enet_rc_pack_batch_device(void *context, const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
+                              size_t n, uint8_t *packed, void *stream);
+
 /* ============================================================ introspection */
 /* Number of packets of the last batch that took the exact (binary-tree) path. */
 uint32_t enet_rc_last_exact_count(void *context);

@@ -1,0 +1,104 @@
+"""One process, several GPUs through the C ABI (enet_rc_multi_*, rc_multi.c;
+SURVEY.md §8e).  CPU: the split against enet_amd/shard.py's ranges.  GPU:
+bit-exact results against the oracle with the device lists [0] (one device)
+and [0, 0, 0] (three contexts on the one GPU of the test box: the non-root
+ranges take the whole scatter / code / pack / gather / unpack path of a
+multi-GPU node, over a same-device "peer" copy)."""
+import numpy as np
+import pytest
+
+from enet_amd import multi_split, shard, synth
+
+
+@pytest.mark.parametrize("n,parts", [(0, 3), (1, 4), (7, 8), (1000, 1), (1000, 3), (65536, 8), (100000, 5)])
+def test_split_matches_shard_ranges(n, parts):
+    rng = np.random.default_rng(n + parts)
+    ln = rng.integers(0, 1400, size=n).astype(np.uint32)
+    first = multi_split(ln, parts)
+    want = shard.shard_ranges(ln, parts)
+    assert [int(x) for x in first[:-1]] == [a for a, _ in want]
+    assert int(first[-1]) == n
+    assert all(first[k] <= first[k + 1] for k in range(parts))
+    if n and ln.sum():
+        per = [int(ln[int(first[k]): int(first[k + 1])].sum()) for k in range(parts)]
+        assert max(per) - min(per) <= 2 * 1400         # balanced by payload bytes within a packet or two
+
+
+def test_split_bad_arguments():
+    with pytest.raises(ValueError):
+        multi_split(np.zeros(4, np.uint32), 0)
+    with pytest.raises(ValueError):
+        multi_split(np.zeros(4, np.uint32), 65)
+
+
+def _oracle(d, o, l):
+    from oracle.pyoracle import compress_batch as ocompress
+    return ocompress(d, o, l, "port")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_host_batches_vs_oracle(devices):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from enet_amd import MultiCoder
+    from oracle.pyoracle import fnv_digest
+    d, o, l = synth.mixed_batch(20000, seed=0x4D554C54)
+    want, wo, wcap, wl = _oracle(d, o, l)
+    n = len(l)
+    ln = l.astype(np.uint32)
+    cap = (2 * ln.astype(np.int64) + 64).astype(np.uint32)
+    coff = np.zeros(n, np.uint64)
+    coff[1:] = np.cumsum(cap[:-1].astype(np.uint64) + 5)          # gapped slots
+    cout = np.zeros(int(coff[-1] + cap[-1]) + 16, np.uint8)
+    clen = np.zeros(n, np.uint32)
+    m = MultiCoder(devices)
+    m.batch_host(False, d, o, ln, cout, coff, cap, clen)
+    assert np.array_equal(clen, wl)
+    assert fnv_digest(cout, coff, clen) == fnv_digest(want, wo, wl)
+    dout = np.zeros(d.size + 16, np.uint8)
+    dlen = np.zeros(n, np.uint32)
+    m.batch_host(True, cout, coff, clen, dout, o, ln, dlen)
+    assert np.array_equal(dlen, ln)
+    assert np.array_equal(dout[: d.size], d)
+    m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_device_batches_vs_oracle(devices):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from enet_amd import MultiCoder
+    from oracle.pyoracle import fnv_digest
+    d, o, l = synth.mixed_batch(20000, seed=0x4D554C55)
+    want, wo, wcap, wl = _oracle(d, o, l)
+    n = len(l)
+    dev = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
+    din, doff, dlen = dev(d, torch.uint8), dev(o, torch.int64), dev(l, torch.int32)
+    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+    gap = 7
+    coff = torch.zeros(n, dtype=torch.int64, device="cuda")
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64) + gap, 0)
+    total = int(coff[-1] + cap[-1]) + gap
+    cout = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    m = MultiCoder(devices)
+    m.batch_device(False, din, doff, dlen, cout, coff, cap, clen, max_len=int(l.max()))
+    cl = clen.cpu().numpy().astype(np.uint32)
+    assert np.array_equal(cl, wl)
+    cb, co = cout.cpu().numpy(), coff.cpu().numpy().astype(np.uint64)
+    assert fnv_digest(cb, co, cl) == fnv_digest(want, wo, wl)
+    # nothing written outside [out_off, out_off + out_len)
+    mask = np.ones(total, bool)
+    for i in range(n):
+        mask[int(co[i]): int(co[i]) + int(cl[i])] = False
+    assert (cb[mask] == 0xA5).all()
+    dout = torch.zeros_like(din)
+    dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    m.batch_device(True, cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
+    assert torch.equal(dl, dlen)
+    assert torch.equal(dout, din)
+    m.close()
