@@ -52,9 +52,8 @@ typedef struct {
     void     *enc2_stream;  /* NULL: the encoder is off (ENET_RC_ENC2=0) or not allocated yet */
     uint64_t  enc2_cap;     /* bytes */
     uint32_t *enc2_list;    /* [n_cap] */
-    /* bucket-history decoder in front of the v3 lane decoder: 5 = rc_dec5.hip (speculative
-       steps), 4 = rc_dec4.hip, 0 = off (ENET_RC_DEC=5|4|0; ENET_RC_DEC4=0: off); the packets it
-       leaves go to enc2_list / counters[3] */
+    /* bucket-history decoder (rc_dec4.hip) in front of the v3 lane decoder; the packets it
+       leaves go to enc2_list / counters[3] (ENET_RC_DEC4=0: off) */
     uint32_t  dec4;
     /* test switch (ENET_RC_ENC2_SLOW=1): the scan takes its slow paths (every position
        exceptional, every bucket sorted and re-walked) */
@@ -87,9 +86,6 @@ int rc_hip_enc2_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *
  * regions; packets off its fast path are listed in ws->enc2_list, count in
  * ws->counters[3]. */
 int rc_hip_dec4_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
-/* The same model with speculative steps (rc_dec5.hip): the record of a step
- * is waited for after the step is decoded, and verifies it. */
-int rc_hip_dec5_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
 uint32_t rc_hip_lane3_region_bytes(uint32_t max_len);

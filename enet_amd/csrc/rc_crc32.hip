@@ -5,21 +5,27 @@
 // complement, returned in network byte order (ENET_HOST_TO_NET_32).
 // protocol.c:1709-1718 (send) and :1075-1091 (receive) are the call sites.
 //
-// One wavefront per packet, HBM-bound:
-//   * The packet is cut into 1 KiB blocks aligned to its END (a raw CRC with a
-//     zero register ignores leading zero bytes, so the first block is padded
-//     at the front for free).  Each lane owns 16 bytes of a block: one aligned
-//     16-B load per lane, wave-uniform funnel shift for the packet's alignment.
+// Sixteen lanes per packet (four packets per wavefront), HBM-bound:
+//   * The packet is cut into 256-B rounds aligned to its END (a raw CRC with
+//     a zero register ignores leading zero bytes, so the first round is
+//     padded at the front for free).  Lane s of the packet's 16 owns bytes
+//     [16 s, 16 s + 16) of every round: one aligned 16-B load per lane and
+//     round, a funnel shift (with the next lane's granule) for the packet's
+//     alignment.
 //   * A lane's raw CRC of its 16 bytes is a slice-by-16 lookup (16 independent
-//     LDS reads, tables T_k[b] = CRC of b followed by k zero bytes).
-//   * Lanes are combined in a 6-level xor tree: crc(A||B) = shift(crc(A), |B|)
-//     ^ crc(B), where shift(v, n) -- n zero bytes through the register -- is
-//     linear in v, i.e. four 256-entry lookups per level (n = 16 << level).
-//     Blocks chain with the n = 1024 tables.
+//     LDS reads, tables T_k[b] = CRC of b followed by k zero bytes), folded
+//     into the lane's running value across rounds: acc = shift(acc, 256) ^
+//     crc16 -- the lane's interleaved stream, 256 B apart.
+//   * The 16 running values are combined once per packet in a 4-level xor
+//     tree: crc(A||B) = shift(crc(A), |B|) ^ crc(B), where shift(v, n) -- n
+//     zero bytes through the register -- is linear in v, i.e. four 256-entry
+//     lookups (n = 16 << level).
 //   * The 0xFFFFFFFF preset is folded in by complementing the first four
 //     message bytes (identical for packets of >= 4 bytes); shorter packets add
 //     shift(0xFFFFFFFF, L) directly.
-// Tables (44 KiB) are built on the host once per context and staged into LDS
+// Per byte: about one table lookup (round 2 used 2.75 plus the padding of a
+// 1-KiB block per packet: 1200-B packets ran 2048 B of lookups).
+// Tables (36 KiB) are built on the host once per context and staged into LDS
 // by each workgroup of a persistent grid.
 
 #include <hip/hip_runtime.h>
@@ -30,9 +36,10 @@
 namespace {
 
 constexpr uint32_t kSlice = 16;                 // slice-by-16 tables
-constexpr uint32_t kLevels = 7;                 // shift tables for 16 << 0..6 bytes
+constexpr uint32_t kLevels = 5;                 // shift tables for 16 << 0..4 bytes (tree levels 0..3, rounds)
 constexpr uint32_t kTableWords = (kSlice + 4 * kLevels) * 256;
-constexpr uint32_t kBlock = 1024;               // bytes per wave pass (64 lanes x 16 B)
+constexpr uint32_t kLanesPer = 16;              // lanes per packet
+constexpr uint32_t kRound = 16 * kLanesPer;     // bytes per round (256)
 constexpr uint32_t kWavesPerGroup = 4;
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t k) { return (w >> (8 * k)) & 0xFFu; }
@@ -77,38 +84,48 @@ void rc_crc32_batch(const uint8_t* __restrict__ in, const uint64_t* __restrict__
     for (uint32_t i = threadIdx.x; i < kTableWords / 4; i += blockDim.x)
         reinterpret_cast<uint4*>(tab)[i] = reinterpret_cast<const uint4*>(tables)[i];
     __syncthreads();
-    const uint32_t* sh = tab + kSlice * 256;    // shift tables, level-major
-
+    const uint32_t* sh = tab + kSlice * 256;    // shift tables, level-major: 16, 32, 64, 128, 256 bytes
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerGroup + (threadIdx.x >> 6));
-    const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+    const uint32_t s = lane & (kLanesPer - 1);  // lane within the packet's 16
+    const uint32_t q = lane / kLanesPer;        // the wavefront's packet slot
+    const uint32_t wave = blockIdx.x * kWavesPerGroup + (threadIdx.x >> 6);
+    const uint32_t stride = gridDim.x * kWavesPerGroup * 4;
     const uint64_t base = reinterpret_cast<uint64_t>(in);
-    for (uint32_t p = wave; p < n; p += nwaves) {
-        // everything per packet is wave-uniform; addresses are absolute
-        const uint64_t start = base + in_off[p];
-        const uint32_t len = in_len[p];
+    for (uint32_t p0 = wave * 4; p0 < n; p0 += stride) {
+        const uint32_t p = p0 + q;
+        const bool live = p < n;
+        const uint64_t start = base + (live ? in_off[p] : 0);
+        const uint32_t len = live ? in_len[p] : 0u;
         const uint64_t end = start + len;
-        const uint32_t nb = (len + kBlock - 1) / kBlock;
+        const uint32_t rounds = (len + kRound - 1) / kRound;
         const uint32_t mis = static_cast<uint32_t>(end & 15);
         const uint32_t dq = mis >> 2, bs = mis & 3;
-        uint32_t run = 0;
-        for (uint32_t b = 0; b < nb; ++b) {
-            // this lane's 16 bytes: [c, c + 16) (may start before the packet in block 0)
-            const uint64_t c = end - static_cast<uint64_t>(kBlock) * (nb - b) + 16 * lane;
-            const uint64_t a = c - mis;                                 // aligned granule holding byte c
+        // the wavefront loops over its longest packet's rounds; a packet's
+        // rounds are the last ones (the shuffles below need every lane)
+        uint32_t rmax = rounds;
+#pragma unroll
+        for (uint32_t m = 16; m < 64; m <<= 1) rmax = max(rmax, static_cast<uint32_t>(__shfl_xor(rmax, m)));
+        rmax = __builtin_amdgcn_readfirstlane(rmax);
+        uint32_t acc = 0;
+        for (uint32_t r = 0; r < rmax; ++r) {
+            const bool on = r + rounds >= rmax;                 // this packet's round r - (rmax - rounds)
+            const uint32_t rr = r + rounds - rmax;
+            // this lane's 16 bytes: [c, c + 16) (may start before the packet in the first round)
+            const uint64_t c = end - static_cast<uint64_t>(kRound) * (rounds - rr) + 16 * s;
+            const uint64_t a = c - mis;                         // aligned granule holding byte c
             uint4 w0 = make_uint4(0, 0, 0, 0), w1;
-            if (a + 16 > start) w0 = gload16(a);   // granule overlaps the packet
-            // next granule: the neighbour's; lane 63 loads its own (only when misaligned)
+            if (on && a + 16 > start) w0 = gload16(a);          // granule overlaps the packet
+            // next granule: the neighbour's; the packet's last lane loads its own (only when misaligned)
             w1.x = __shfl_down(w0.x, 1); w1.y = __shfl_down(w0.y, 1);
             w1.z = __shfl_down(w0.z, 1); w1.w = __shfl_down(w0.w, 1);
-            if (lane == 63 && mis) w1 = gload16(a + 16);
+            if (on && s == kLanesPer - 1 && mis) w1 = gload16(a + 16);
             // funnel-shift the 32 bytes (w0, w1) right by mis -> 16 bytes d[0..3]
-            const uint32_t q[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+            const uint32_t qq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
             uint32_t d[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint32_t lo = dq == 0 ? q[k] : dq == 1 ? q[k + 1] : dq == 2 ? q[k + 2] : q[k + 3];
-                const uint32_t hi = dq == 0 ? q[k + 1] : dq == 1 ? q[k + 2] : dq == 2 ? q[k + 3] : q[k + 4];
+                const uint32_t lo = dq == 0 ? qq[k] : dq == 1 ? qq[k + 1] : dq == 2 ? qq[k + 2] : qq[k + 3];
+                const uint32_t hi = dq == 0 ? qq[k + 1] : dq == 1 ? qq[k + 2] : dq == 2 ? qq[k + 3] : qq[k + 4];
                 d[k] = funnel(lo, hi, bs);
             }
             // zero the bytes before the packet; complement its first four (register preset)
@@ -119,28 +136,29 @@ void rc_crc32_batch(const uint8_t* __restrict__ in, const uint64_t* __restrict__
                 d[k] &= keep;
                 if (len >= 4) d[k] ^= keep & ~bytes_from(lead + 4, k);
             }
-            // raw CRC of the 16 bytes (slice-by-16)
+            // raw CRC of the 16 bytes (slice-by-16), folded into the lane's stream
             uint32_t v = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) v ^= tab[(15 - (4 * k + j)) * 256 + byte_of(d[k], j)];
-            // xor tree over the 64 lanes (lane order = message order)
-#pragma unroll
-            for (uint32_t lv = 0; lv < 6; ++lv) {
-                const uint32_t m = 1u << lv;
-                const uint32_t s = shift_by(sh + lv * 1024, v);
-                const uint32_t os = __shfl_xor(s, m), ov = __shfl_xor(v, m);
-                v = (lane & m) ? (os ^ v) : (s ^ ov);
-            }
-            run = shift_by(sh + 6 * 1024, run) ^ v;
+            const uint32_t nacc = shift_by(sh + 4 * 1024, acc) ^ v;
+            acc = on ? nacc : acc;
         }
-        if (lane == 0) {
-            uint32_t crc = run;
+        // xor tree over the packet's 16 lanes (lane order = message order)
+#pragma unroll
+        for (uint32_t lv = 0; lv < 4; ++lv) {
+            const uint32_t m = 1u << lv;
+            const uint32_t t = shift_by(sh + lv * 1024, acc);
+            const uint32_t ot = __shfl_xor(t, m), oa = __shfl_xor(acc, m);
+            acc = (s & m) ? (ot ^ acc) : (t ^ oa);
+        }
+        if (live && s == 0) {
+            uint32_t crc = acc;
             if (len < 4) {                       // preset through len bytes, zero data
-                uint32_t r = 0xFFFFFFFFu;
-                for (uint32_t k = 0; k < len; ++k) r = (r >> 8) ^ tab[r & 0xFF];
-                crc ^= r;
+                uint32_t rg = 0xFFFFFFFFu;
+                for (uint32_t k = 0; k < len; ++k) rg = (rg >> 8) ^ tab[rg & 0xFF];
+                crc ^= rg;
             }
             crc_out[p] = __builtin_bswap32(~crc);
         }
@@ -181,8 +199,8 @@ extern "C" int rc_hip_crc32(const uint8_t* in, const uint64_t* in_off, const uin
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    uint32_t groups = (n + kWavesPerGroup - 1) / kWavesPerGroup;
-    const uint32_t cap = static_cast<uint32_t>(cus) * 3;        // 44 KiB LDS -> 3 groups per CU
+    uint32_t groups = (n + 4 * kWavesPerGroup - 1) / (4 * kWavesPerGroup);
+    const uint32_t cap = static_cast<uint32_t>(cus) * 4;        // 36 KiB LDS -> 4 groups per CU
     if (groups > cap) groups = cap;
     hipLaunchKernelGGL(rc_crc32_batch, dim3(groups), dim3(64 * kWavesPerGroup), 0,
                        static_cast<hipStream_t>(stream), in, in_off, in_len, n, crc_out, tables);

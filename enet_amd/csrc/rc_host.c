@@ -31,9 +31,6 @@ extern void enet_free(void *) __attribute__((weak));
 extern void enet_host_compress(ENetHost *, const ENetCompressor *) __attribute__((weak));
 
 #define EXACT_SLOTS 256u            /* concurrent exact-path packets (64 KiB pool each) */
-#ifndef ENET_RC_DEC_DEFAULT
-#define ENET_RC_DEC_DEFAULT 4u      /* the bucket-history decoder: rc_dec4.hip (4) or rc_dec5.hip (5) */
-#endif
 
 typedef struct {
     int device;
@@ -196,10 +193,8 @@ void *enet_range_coder_create(void)
         c->ws.cus = (uint32_t) cus;
         const char *e2 = getenv("ENET_RC_ENC2");
         c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
-        const char *d4 = getenv("ENET_RC_DEC4"), *dv = getenv("ENET_RC_DEC");
-        c->ws.dec4 = ENET_RC_DEC_DEFAULT;
-        if (dv && (strcmp(dv, "4") == 0 || strcmp(dv, "5") == 0 || strcmp(dv, "0") == 0)) c->ws.dec4 = (uint32_t) atoi(dv);
-        if (d4 && strcmp(d4, "0") == 0) c->ws.dec4 = 0;
+        const char *d4 = getenv("ENET_RC_DEC4");
+        c->ws.dec4 = !(d4 && strcmp(d4, "0") == 0);
         const char *es = getenv("ENET_RC_ENC2_SLOW");
         c->ws.enc2_slow = (es && strcmp(es, "1") == 0) ? 1u : 0u;
         const char *sl = getenv("ENET_RC_SLOTS");

@@ -136,10 +136,9 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
         w.sub_count = ws->counters + 3;
     }
     if (decompress && ws->dec4) {
-        // the bucket-history decoder takes what it can (rc_dec5.hip, or
-        // rc_dec4.hip with ENET_RC_DEC=4); the lanes decode only the packets it lists
-        const int rc = ws->dec4 == 4 ? rc_hip_dec4_launch(b, &w, blocks, stream)
-                                     : rc_hip_dec5_launch(b, &w, blocks, stream);
+        // the bucket-history decoder takes what it can (rc_dec4.hip); the
+        // lanes decode only the packets it lists
+        const int rc = rc_hip_dec4_launch(b, &w, blocks, stream);
         if (rc != 0) return rc;
         w.sub_list = ws->enc2_list;
         w.sub_count = ws->counters + 3;

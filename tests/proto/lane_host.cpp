@@ -1,6 +1,5 @@
 // TEST ONLY: host build of the lane kernels' per-lane compress/decompress
-// (rc_lane3.hip) and, with -DDEC4 / -DDEC5, the bucket-history decoders
-// (rc_dec4.hip, rc_dec5.hip).
+// (rc_lane3.hip) and, with -DDEC4, the bucket-history decoder (rc_dec4.hip).
 #define RC_LANE_HOST_TEST 1
 #include <stdlib.h>
 #include <string.h>
@@ -8,9 +7,7 @@
 #ifdef DEC4
 #include "../../enet_amd/csrc/rc_dec4.hip"
 #endif
-#ifdef DEC5
-#include "../../enet_amd/csrc/rc_dec5.hip"
-#endif
+
 #define REGION_BYTES rc_hip_lane3_region_bytes
 #define COMPRESS_ONE compress_one3
 #define DECOMPRESS_ONE decompress_one3
@@ -44,15 +41,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
         if (!counters[3]) return 0;
     }
 #endif
-#ifdef DEC5
-    // the speculative bucket-history decoder first, likewise
-    if (decompress) {
-        static uint8_t g_t[256];
-        uint32_t wbail = 0;
-        decompress_one5(b, ws, 0, region, g_root, g_t, &wbail);
-        if (!counters[3]) return 0;
-    }
-#endif
+
     if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root);
     else COMPRESS_ONE(b, ws, 0, region, g_root COMPRESS_ARGS);
     return counters[0] ? 1 : (counters[3] ? 2 : 0);   // 1 = routed to the exact path, 2 = left by dec4
