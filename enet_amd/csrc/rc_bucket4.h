@@ -1,5 +1,5 @@
-// rc_bucket4.h -- the bucket-history model of the decoders (rc_dec4.hip,
-// rc_dec5.hip): one 64-B record per previous byte p listing the positions
+// rc_bucket4.h -- the bucket-history model of the decoder (rc_dec4.hip):
+// one 64-B record per previous byte p listing the positions
 // decoded so far with x[j-1] = p (compress.c:159-199, :536-615; see
 // rc_dec4.hip for the algebra).  Include after rc_lane_common.h / rc_root3.h.
 #pragma once

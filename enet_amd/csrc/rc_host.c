@@ -12,6 +12,7 @@
  * There is no CPU coder in this library: if no HIP device is usable,
  * enet_range_coder_create() returns NULL and the batch calls fail.
  */
+#define _POSIX_C_SOURCE 200809L
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
 
@@ -19,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <time.h>
 
 #include "enet_rc_amd.h"
 #include "rc_abi_internal.h"
@@ -311,7 +313,7 @@ static void *copy_worker(void *p)
     return NULL;
 }
 
-#define COPY_THREADS 8
+#define COPY_THREADS 16          /* the GPU box gives a process 16 CPUs */
 #define COPY_MIN_BYTES (4u << 20)
 
 static void par_run(copy_job *jobs, int k)
@@ -378,17 +380,54 @@ static int pack_reserve(rc_ctx *c, size_t bytes, size_t blocks)
  * H2D, the device path, then the results packed back to back on the device
  * (rc_pack.hip) so that only the produced bytes cross PCIe, and scattered to
  * out_off on the host. */
+/* Page-locks [p, p + bytes) for direct DMA (hipHostRegister: ~0.35 ms for
+ * 80 MB the first time, microseconds after), so that a host batch skips the
+ * copy through pinned staging.  1: registered here (host_unpin after the
+ * transfers), 0: not usable (already registered by someone else, or the call
+ * failed) -- the staging path then. */
+static int host_pin(const void *p, size_t bytes)
+{
+    static int off = -1;
+    if (off < 0) off = getenv("ENET_RC_NO_HOST_PIN") != NULL;
+    if (off || bytes < (1u << 20)) return 0;
+    const uintptr_t a = (uintptr_t) p & ~(uintptr_t) 4095, e = ((uintptr_t) p + bytes + 4095) & ~(uintptr_t) 4095;
+    if (hipHostRegister((void *) a, e - a, hipHostRegisterDefault) == hipSuccess) return 1;
+    (void) hipGetLastError();
+    return 0;
+}
+
+static void host_unpin(const void *p, int pinned)
+{
+    if (pinned == 1) hipHostUnregister((void *) ((uintptr_t) p & ~(uintptr_t) 4095));
+}
+
+/* ENET_RC_HOST_PROFILE=1: phase times of run_host on stderr (diagnostic) */
+static double now_ms(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+
 static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
                     const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
-                    const uint32_t *out_cap, uint32_t *out_len)
+                    const uint32_t *out_cap, uint32_t *out_len, int allow_pin)
 {
+    static int prof = -1;
+    if (prof < 0) prof = getenv("ENET_RC_HOST_PROFILE") != NULL;
+    double tp[8] = {0};
+    if (prof) tp[0] = now_ms();
     if (!c) return (int) hipErrorInvalidValue;
     if (n == 0) return 0;
-    uint64_t in_bytes = 0, out_bytes = 0;
+    /* the input as it goes to the device: packed back to back (a batch whose
+     * packets sit in gapped slots -- the compressed side of a round trip --
+     * moves only its bytes); a batch that already is back to back is one range */
+    uint64_t in_bytes = 0, out_bytes = 0, in_lo = in_off[0];
     uint32_t max_len = 0, max_cap = 0;
+    int packed_in = 1;
     for (size_t i = 0; i < n; ++i) {
-        uint64_t e = in_off[i] + in_len[i];
-        if (e > in_bytes) in_bytes = e;
+        if (in_off[i] != in_lo + in_bytes) packed_in = 0;
+        in_bytes += in_len[i];
         uint64_t f = out_off[i] + out_cap[i];
         if (f > out_bytes) out_bytes = f;
         if (in_len[i] > max_len) max_len = in_len[i];
@@ -407,25 +446,43 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     const size_t blocks = (n + 1023) / 1024;
     if (pack_reserve(c, out_bytes + 16, blocks) != 0) return (int) hipErrorOutOfMemory;
     uint8_t *h = c->h_stage, *d = c->d_stage;
-    memcpy(h + a_ioff, in_off, n * 8);
+    uint64_t *hio = (uint64_t *) (h + a_ioff);
+    {
+        uint64_t acc = 0;
+        for (size_t i = 0; i < n; ++i) { hio[i] = acc; acc += in_len[i]; }
+    }
     memcpy(h + a_ilen, in_len, n * 4);
     memcpy(h + a_ooff, out_off, n * 8);
     memcpy(h + a_ocap, out_cap, n * 4);
     hipError_t err = hipMemcpyAsync(d + a_ioff, h + a_ioff, a_olen - a_ioff, hipMemcpyHostToDevice, c->stream);
     if (err != hipSuccess) return (int) err;
-    /* the payload in chunks: the staging copy of chunk k+1 overlaps the DMA of chunk k */
-    const size_t chunk = in_bytes >= (16u << 20) ? (in_bytes + 3) / 4 : in_bytes;
-    for (size_t lo = 0; lo < in_bytes; lo += chunk) {
-        const size_t m = in_bytes - lo < chunk ? in_bytes - lo : chunk;
-        par_memcpy(h + a_in + lo, in + lo, m);
-        err = hipMemcpyAsync(d + a_in + lo, h + a_in + lo, m, hipMemcpyHostToDevice, c->stream);
+    /* the payload: straight from the caller's memory when it is one range and
+     * can be page-locked; else in four packet groups through pinned staging,
+     * the staging copy of group k+1 overlapping the DMA of group k */
+    const int pin_in = packed_in && allow_pin ? host_pin(in + in_lo, in_bytes) : 0;
+    if (pin_in) err = hipMemcpyAsync(d + a_in, in + in_lo, in_bytes, hipMemcpyHostToDevice, c->stream);
+    if (err != hipSuccess) { host_unpin(in + in_lo, pin_in); return (int) err; }
+    const int ig = pin_in ? 0 : in_bytes >= (16u << 20) ? 4 : 1;
+    for (int g = 0; g < ig; ++g) {
+        const size_t lo = n * (size_t) g / (size_t) ig, hi = n * (size_t) (g + 1) / (size_t) ig;
+        if (hi <= lo) continue;
+        const uint64_t b0 = hio[lo], b1 = hio[hi - 1] + in_len[hi - 1];
+        if (packed_in) par_memcpy(h + a_in + b0, in + in_lo + b0, b1 - b0);
+        else par_scatter(h + a_in, hio, in, in_off, in_len, lo, hi, b1 - b0);
+        if (b1 > b0) err = hipMemcpyAsync(d + a_in + b0, h + a_in + b0, b1 - b0, hipMemcpyHostToDevice, c->stream);
         if (err != hipSuccess) return (int) err;
     }
+    if (prof) { tp[1] = now_ms(); hipStreamSynchronize(c->stream); tp[2] = now_ms(); }
     int rc = run_device(c, decompress, d + a_in, (const uint64_t *) (d + a_ioff),
                         (const uint32_t *) (d + a_ilen), n, max_len, max_cap, d + a_out,
                         (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_ocap),
                         (uint32_t *) (d + a_olen), (void *) c->stream);
+    if (pin_in) {               /* the input DMA is behind the kernels on the stream */
+        hipStreamSynchronize(c->stream);
+        host_unpin(in + in_lo, pin_in);
+    }
     if (rc != 0) return rc;
+    if (prof) { hipStreamSynchronize(c->stream); tp[3] = now_ms(); }
     if (out_bytes <= (1u << 20)) {
         /* small batches (the per-datagram drop-in calls): one D2H of the slots,
          * fewer launches and syncs than packing */
@@ -438,15 +495,46 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
             if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
         return 0;
     }
+    /* the results: straight into the caller's slots when they are back to
+     * back and every packet filled its slot exactly (a decompress batch with
+     * out_cap = the packet lengths) -- one DMA writes exactly the results;
+     * else packed on the device (rc_pack.hip), copied, scattered on the host */
+    int contig_out = 1;
+    for (size_t i = 1; i < n && contig_out; ++i) contig_out = out_off[i] == out_off[i - 1] + out_cap[i - 1];
+    err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess && contig_out) err = hipStreamSynchronize(c->stream);
+    if (err != hipSuccess) return (int) err;
+    if (contig_out) {
+        const uint32_t *ol = (const uint32_t *) (h + a_olen);
+        int full = 1;
+        for (size_t i = 0; i < n && full; ++i) full = ol[i] == out_cap[i];
+        const uint64_t span = out_off[n - 1] + out_cap[n - 1] - out_off[0];
+        const int pin_out = full && allow_pin ? host_pin(out + out_off[0], span) : 0;
+        if (pin_out) {
+            err = hipMemcpyAsync(out + out_off[0], d + a_out + out_off[0], span, hipMemcpyDeviceToHost, c->stream);
+            if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+            host_unpin(out + out_off[0], pin_out);
+            if (err != hipSuccess) return (int) err;
+            memcpy(out_len, ol, n * 4);
+            if (prof) {
+                tp[5] = now_ms();
+                fprintf(stderr, "enet_rc host %s n=%zu in=%.1f MB out=%.1f MB (direct): stage+H2D enqueue %.3f, "
+                        "H2D drain %.3f, kernels %.3f, D2H %.3f, total %.3f ms\n", decompress ? "dec" : "enc", n,
+                        in_bytes / 1e6, span / 1e6, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[5] - tp[3],
+                        tp[5] - tp[0]);
+            }
+            return 0;
+        }
+    }
     rc = rc_hip_pack(d + a_out, (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_olen), (uint32_t) n,
                      c->d_bsum, c->d_pack, (void *) c->stream);
     if (rc != 0) return rc;
     uint64_t packed = 0;
-    err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(&packed, c->d_bsum + blocks, 8, hipMemcpyDeviceToHost, c->stream);
+    err = hipMemcpyAsync(&packed, c->d_bsum + blocks, 8, hipMemcpyDeviceToHost, c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     if (err != hipSuccess) return (int) err;
+    if (prof) tp[4] = now_ms();
     if (packed > out_bytes) return (int) hipErrorUnknown;
     memcpy(out_len, h + a_olen, n * 4);
     uint64_t *poff = (uint64_t *) malloc((n + 1) * sizeof(uint64_t));
@@ -474,6 +562,13 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     }
     for (int g = 0; g < nev; ++g) hipEventDestroy(ev[g]);
     free(poff);
+    if (prof) {
+        tp[5] = now_ms();
+        fprintf(stderr, "enet_rc host %s n=%zu in=%.1f MB out=%.1f MB: stage+H2D enqueue %.3f, H2D drain %.3f, "
+                "kernels %.3f, pack+lens %.3f, D2H+scatter %.3f, total %.3f ms\n", decompress ? "dec" : "enc", n,
+                in_bytes / 1e6, packed / 1e6, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3],
+                tp[5] - tp[4], tp[5] - tp[0]);
+    }
     return err == hipSuccess ? 0 : (int) err;
 }
 
@@ -481,14 +576,14 @@ int enet_rc_compress_batch_host(void *context, const uint8_t *in, const uint64_t
                                 const uint32_t *in_len, size_t n, uint8_t *out,
                                 const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return run_host((rc_ctx *) context, 0, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+    return run_host((rc_ctx *) context, 0, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1);
 }
 
 int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
                                   const uint32_t *in_len, size_t n, uint8_t *out,
                                   const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+    return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1);
 }
 
 /* --------------------------------------------------- datagram framing (§8f) */
@@ -811,7 +906,9 @@ int rc_ctx_run_host(void *context, int decompress, const uint8_t *in, const uint
                     const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
                     const uint32_t *out_cap, uint32_t *out_len)
 {
-    return run_host((rc_ctx *) context, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len);
+    /* (no page-locking of the caller's memory: the devices' ranges share
+     * boundary pages, and one range's unregister would unpin another's) */
+    return run_host((rc_ctx *) context, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 0);
 }
 
 /* The context's block-sum workspace of rc_pack.hip for n packets (device

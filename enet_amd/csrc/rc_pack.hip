@@ -3,10 +3,10 @@
 // slot of out_cap[i] bytes, e.g. 2N + 64) go to packed[sum of out_len[<i]].
 // PCIe then carries the compressed bytes, not the slot capacities.
 //
-// Three launches: per-block sums of out_len (1024 packets per block), one
-// block scanning those sums (also writing the total), and per block a local
-// scan plus the copies (one wavefront per packet, 4-B words where both ends
-// are aligned, bytes otherwise).
+// Three launches: per-segment sums of out_len (1024 packets per segment), one
+// block scanning those sums (also writing the total), and the copies: 16
+// workgroups per segment, one wavefront per packet, aligned dword stores
+// assembled from the source with alignbyte (copy_bytes).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -71,42 +71,70 @@ extern "C" __global__ __launch_bounds__(kThreads) void rc_pack_scan(uint64_t* bs
     if (threadIdx.x == 0) bsum[nb] = carry;
 }
 
+// One packet's bytes [src, src + m) -> [dst, dst + m) by one wavefront, any
+// alignment on either side: every destination dword inside the range is one
+// aligned store assembled from two aligned source dwords (alignbyte); the
+// bytes of the range's first and last partial dwords are stored singly (a
+// neighbouring packet owns the rest of those dwords).
+__device__ __forceinline__ void copy_bytes(const uint8_t* src, uint8_t* dst, uint32_t m, uint32_t lane)
+{
+    if (m == 0) return;
+    const uintptr_t d0 = reinterpret_cast<uintptr_t>(dst), d1 = d0 + m;
+    const uintptr_t b0 = (d0 + 3) & ~static_cast<uintptr_t>(3), b1 = d1 & ~static_cast<uintptr_t>(3);
+    if (b0 >= b1) {                                      // no whole dword inside
+        if (lane < m) dst[lane] = src[lane];
+        return;
+    }
+    const uint32_t head = static_cast<uint32_t>(b0 - d0), tail = static_cast<uint32_t>(d1 - b1);
+    if (lane < head) dst[lane] = src[lane];
+    if (lane < tail) dst[m - tail + lane] = src[m - tail + lane];
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(src) + head;   // source of the first whole dword
+    const uint32_t sh = static_cast<uint32_t>(s0 & 3);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(s0 & ~static_cast<uintptr_t>(3));
+    uint32_t* dw = reinterpret_cast<uint32_t*>(b0);
+    const uint32_t nw = static_cast<uint32_t>((b1 - b0) >> 2);
+    for (uint32_t k = lane; k < nw; k += 64) {
+        const uint32_t lo = sw[k];
+        const uint32_t hi = sh ? sw[k + 1] : 0u;          // (only read when the source is misaligned)
+        dw[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    }
+}
+
+constexpr uint32_t kPerBlock = 64;          // packets per copy workgroup (16 per wavefront)
+
 // UNPACK: the reverse, packed[sum of len[<i]] -> out[out_off[i]] (rc_multi.c:
-// results of another device, gathered back to back, into the root's slots)
+// results of another device, gathered back to back, into the root's slots).
+// Workgroup (segment s, part q) copies packets [1024 s + 64 q, +64): their
+// offsets are the segment's base (bsum) plus the lengths before them.
 template <bool UNPACK>
 __device__ void pack_copy(uint8_t* out, const uint64_t* out_off, const uint32_t* len, uint32_t n,
                           const uint64_t* bsum, uint8_t* packed)
 {
     __shared__ uint32_t s[kThreads];
-    __shared__ uint32_t off[kPer];
-    const uint32_t base = blockIdx.x * kPer;
-    // local exclusive offsets: each thread owns 4 consecutive packets
-    uint32_t l4[4], v = 0;
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t i = base + 4 * threadIdx.x + k;
-        l4[k] = i < n ? len[i] : 0u;
-        v += l4[k];
-    }
+    __shared__ uint32_t off[kPerBlock];
+    const uint32_t seg = blockIdx.x / (kPer / kPerBlock), part = blockIdx.x % (kPer / kPerBlock);
+    const uint32_t base = seg * kPer, first = base + part * kPerBlock;
+    // lengths of the segment's packets before this part
+    uint32_t v = 0;
+    for (uint32_t i = base + threadIdx.x; i < first; i += kThreads) v += i < n ? len[i] : 0u;
+    uint32_t before;
+    block_excl_scan(s, v, before);
+    // exclusive offsets of this part's packets
+    const uint32_t t = threadIdx.x;
+    const uint32_t mine = (t < kPerBlock && first + t < n) ? len[first + t] : 0u;
     uint32_t total;
-    uint32_t ex = block_excl_scan(s, v, total);
-    for (uint32_t k = 0; k < 4; ++k) { off[4 * threadIdx.x + k] = ex; ex += l4[k]; }
+    const uint32_t ex = block_excl_scan(s, mine, total);
+    if (t < kPerBlock) off[t] = ex;
     __syncthreads();
-    const uint64_t b0 = bsum[blockIdx.x];
+    const uint64_t b0 = bsum[seg] + before;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t k = wave; k < kPer; k += kThreads / 64) {
-        const uint32_t i = base + k;
+    for (uint32_t k = wave; k < kPerBlock; k += kThreads / 64) {
+        const uint32_t i = first + k;
         if (i >= n) break;
-        const uint32_t m = len[i];
-        const uint8_t* src = UNPACK ? packed + b0 + off[k] : out + out_off[i];
-        uint8_t* dst = UNPACK ? out + out_off[i] : packed + b0 + off[k];
-        if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
-            const uint32_t w = m >> 2;
-            for (uint32_t j = lane; j < w; j += 64)
-                reinterpret_cast<uint32_t*>(dst)[j] = reinterpret_cast<const uint32_t*>(src)[j];
-            for (uint32_t j = 4 * w + lane; j < m; j += 64) dst[j] = src[j];
-        } else {
-            for (uint32_t j = lane; j < m; j += 64) dst[j] = src[j];
-        }
+        uint8_t* pk = packed + b0 + off[k];
+        uint8_t* sl = out + out_off[i];
+        if (UNPACK) copy_bytes(pk, sl, len[i], lane);
+        else copy_bytes(sl, pk, len[i], lane);
     }
 }
 
@@ -132,7 +160,8 @@ extern "C" int rc_hip_unpack(const uint8_t* packed, uint8_t* out, const uint64_t
     const uint32_t nb = (n + kPer - 1) / kPer;
     hipLaunchKernelGGL(rc_pack_sums, dim3(nb), dim3(kThreads), 0, st, out_len, n, bsum);
     hipLaunchKernelGGL(rc_pack_scan, dim3(1), dim3(kThreads), 0, st, bsum, nb);
-    hipLaunchKernelGGL(rc_unpack_copy, dim3(nb), dim3(kThreads), 0, st, out, out_off, out_len, n, bsum, packed);
+    hipLaunchKernelGGL(rc_unpack_copy, dim3(nb * (kPer / kPerBlock)), dim3(kThreads), 0, st, out, out_off, out_len, n,
+                       bsum, packed);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -144,6 +173,7 @@ extern "C" int rc_hip_pack(const uint8_t* out, const uint64_t* out_off, const ui
     const uint32_t nb = (n + kPer - 1) / kPer;
     hipLaunchKernelGGL(rc_pack_sums, dim3(nb), dim3(kThreads), 0, st, out_len, n, bsum);
     hipLaunchKernelGGL(rc_pack_scan, dim3(1), dim3(kThreads), 0, st, bsum, nb);
-    hipLaunchKernelGGL(rc_pack_copy, dim3(nb), dim3(kThreads), 0, st, out, out_off, out_len, n, bsum, packed);
+    hipLaunchKernelGGL(rc_pack_copy, dim3(nb * (kPer / kPerBlock)), dim3(kThreads), 0, st, out, out_off, out_len, n,
+                       bsum, packed);
     return static_cast<int>(hipGetLastError());
 }
