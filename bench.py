@@ -504,9 +504,10 @@ def pcie_inclusive(coder, d, o, l, args):
     nb = float(l.sum(dtype=np.uint64))
     return {"value": round(nb / (best_c + best_d) / GIB, 4), "unit": "GiB/s",
             "compress_GiBps": round(nb / best_c / GIB, 4), "decompress_GiBps": round(nb / best_d / GIB, 4),
-            "bit_exact": ok, "note": "enet_rc_*_batch_host: threaded copy into pinned staging overlapped with chunked H2D, "
-                    "kernels, outputs packed on the device, chunked D2H of the produced bytes overlapped "
-                    "with the threaded scatter; best of 3"}
+            "bit_exact": ok, "note": "enet_rc_*_batch_host: a back-to-back input DMA'd from the page-locked caller "
+                    "buffer (else gathered into pinned staging on a thread pool, overlapped with chunked H2D), "
+                    "kernels, outputs that fill their slots DMA'd into place (else packed on the device, "
+                    "chunked D2H of the produced bytes overlapped with the pooled scatter); best of 3"}
 
 
 def rccl_scatter_gather(dist, dev, coder, din, doff, dlen, max_len, world, rank):

@@ -40,7 +40,7 @@ constexpr uint32_t kLevels = 5;                 // shift tables for 16 << 0..4 b
 constexpr uint32_t kTableWords = (kSlice + 4 * kLevels) * 256;
 constexpr uint32_t kLanesPer = 16;              // lanes per packet
 constexpr uint32_t kRound = 16 * kLanesPer;     // bytes per round (256)
-constexpr uint32_t kWavesPerGroup = 4;
+constexpr uint32_t kWavesPerGroup = 16;             // 1024-thread workgroups: the 36-KiB table staging per workgroup is read once per 16 wavefronts
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t k) { return (w >> (8 * k)) & 0xFFu; }
 
@@ -200,7 +200,7 @@ extern "C" int rc_hip_crc32(const uint8_t* in, const uint64_t* in_off, const uin
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
     uint32_t groups = (n + 4 * kWavesPerGroup - 1) / (4 * kWavesPerGroup);
-    const uint32_t cap = static_cast<uint32_t>(cus) * 4;        // 36 KiB LDS -> 4 groups per CU
+    const uint32_t cap = static_cast<uint32_t>(cus) * 2;        // 2 x 16 wavefronts per CU (the wave limit), 72 KiB LDS
     if (groups > cap) groups = cap;
     hipLaunchKernelGGL(rc_crc32_batch, dim3(groups), dim3(64 * kWavesPerGroup), 0,
                        static_cast<hipStream_t>(stream), in, in_off, in_len, n, crc_out, tables);

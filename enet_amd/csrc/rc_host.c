@@ -313,19 +313,78 @@ static void *copy_worker(void *p)
     return NULL;
 }
 
-#define COPY_THREADS 16          /* the GPU box gives a process 16 CPUs */
+#define COPY_THREADS 8
 #define COPY_MIN_BYTES (4u << 20)
+
+/* A persistent pool of COPY_THREADS - 1 workers (created on first use):
+ * creating threads per copy group cost ~1-3 ms per host batch.  One caller
+ * at a time uses it; a concurrent caller (several contexts driven from
+ * several threads, rc_multi.c) runs its jobs on its own thread. */
+static struct {
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    copy_job *jobs;
+    int k, next, pending;
+} pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, NULL, 0, 0, 0};
+static pthread_mutex_t pool_user = PTHREAD_MUTEX_INITIALIZER;
+static pthread_once_t pool_once = PTHREAD_ONCE_INIT;
+static int pool_workers;
+
+static void *pool_worker(void *unused)
+{
+    (void) unused;
+    pthread_mutex_lock(&pool.mu);
+    for (;;) {
+        while (pool.next >= pool.k) pthread_cond_wait(&pool.go, &pool.mu);
+        copy_job *j = &pool.jobs[pool.next++];
+        pthread_mutex_unlock(&pool.mu);
+        copy_worker(j);
+        pthread_mutex_lock(&pool.mu);
+        if (--pool.pending == 0) pthread_cond_signal(&pool.done);
+    }
+    return NULL;
+}
+
+static void pool_start(void)
+{
+    for (int i = 1; i < COPY_THREADS; ++i) {
+        pthread_t t;
+        if (pthread_create(&t, NULL, pool_worker, NULL) != 0) break;
+        pthread_detach(t);
+        ++pool_workers;
+    }
+}
 
 static void par_run(copy_job *jobs, int k)
 {
-    pthread_t t[COPY_THREADS];
-    int started[COPY_THREADS] = {0};
-    for (int i = 1; i < k; ++i) started[i] = pthread_create(&t[i], NULL, copy_worker, &jobs[i]) == 0;
-    copy_worker(&jobs[0]);
-    for (int i = 1; i < k; ++i) {
-        if (started[i]) pthread_join(t[i], NULL);
-        else copy_worker(&jobs[i]);
+    pthread_once(&pool_once, pool_start);
+    if (k <= 1 || pool_workers == 0 || pthread_mutex_trylock(&pool_user) != 0) {
+        for (int i = 0; i < k; ++i) copy_worker(&jobs[i]);
+        return;
     }
+    pthread_mutex_lock(&pool.mu);
+    pool.jobs = jobs;
+    pool.next = 1;                  /* job 0 runs here */
+    pool.pending = k - 1;
+    pool.k = k;
+    pthread_cond_broadcast(&pool.go);
+    pthread_mutex_unlock(&pool.mu);
+    copy_worker(&jobs[0]);
+    pthread_mutex_lock(&pool.mu);
+    while (pool.pending > 0) {
+        if (pool.next < pool.k) {   /* help with what is left */
+            copy_job *j = &pool.jobs[pool.next++];
+            pthread_mutex_unlock(&pool.mu);
+            copy_worker(j);
+            pthread_mutex_lock(&pool.mu);
+            --pool.pending;
+            continue;
+        }
+        pthread_cond_wait(&pool.done, &pool.mu);
+    }
+    pool.k = pool.next = 0;
+    pthread_mutex_unlock(&pool.mu);
+    pthread_mutex_unlock(&pool_user);
 }
 
 static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
