@@ -67,6 +67,13 @@ __device__ __forceinline__ uint4 gload16(uint64_t a)
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// the value of lane + 1 within the lane's row of 16 (DPP row_shl:1; 0 for
+// the row's last lane)
+__device__ __forceinline__ uint32_t row_next(uint32_t x)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x101, 0xF, 0xF, true));
+}
+
 __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh)
 {
     // bytes sh.. of the 8-byte little-endian pair (lo, hi), sh in 0..3
@@ -106,6 +113,7 @@ void rc_crc32_batch(const uint8_t* __restrict__ in, const uint64_t* __restrict__
 #pragma unroll
         for (uint32_t m = 16; m < 64; m <<= 1) rmax = max(rmax, static_cast<uint32_t>(__shfl_xor(rmax, m)));
         rmax = __builtin_amdgcn_readfirstlane(rmax);
+        const bool any_misaligned = __builtin_amdgcn_ballot_w64(mis != 0) != 0;
         uint32_t acc = 0;
         for (uint32_t r = 0; r < rmax; ++r) {
             const bool on = r + rounds >= rmax;                 // this packet's round r - (rmax - rounds)
@@ -113,28 +121,34 @@ void rc_crc32_batch(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             // this lane's 16 bytes: [c, c + 16) (may start before the packet in the first round)
             const uint64_t c = end - static_cast<uint64_t>(kRound) * (rounds - rr) + 16 * s;
             const uint64_t a = c - mis;                         // aligned granule holding byte c
-            uint4 w0 = make_uint4(0, 0, 0, 0), w1;
+            uint4 w0 = make_uint4(0, 0, 0, 0);
             if (on && a + 16 > start) w0 = gload16(a);          // granule overlaps the packet
-            // next granule: the neighbour's; the packet's last lane loads its own (only when misaligned)
-            w1.x = __shfl_down(w0.x, 1); w1.y = __shfl_down(w0.y, 1);
-            w1.z = __shfl_down(w0.z, 1); w1.w = __shfl_down(w0.w, 1);
-            if (on && s == kLanesPer - 1 && mis) w1 = gload16(a + 16);
-            // funnel-shift the 32 bytes (w0, w1) right by mis -> 16 bytes d[0..3]
-            const uint32_t qq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-            uint32_t d[4];
+            uint32_t d[4] = {w0.x, w0.y, w0.z, w0.w};
+            if (any_misaligned) {
+                // next granule: the neighbour's (a DPP row shift: the rows of 16
+                // lanes are the packets); the packet's last lane loads its own
+                uint4 w1;
+                w1.x = row_next(w0.x); w1.y = row_next(w0.y); w1.z = row_next(w0.z); w1.w = row_next(w0.w);
+                if (on && s == kLanesPer - 1 && mis) w1 = gload16(a + 16);
+                // funnel-shift the 32 bytes (w0, w1) right by mis -> 16 bytes d[0..3]
+                const uint32_t qq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t lo = dq == 0 ? qq[k] : dq == 1 ? qq[k + 1] : dq == 2 ? qq[k + 2] : qq[k + 3];
-                const uint32_t hi = dq == 0 ? qq[k + 1] : dq == 1 ? qq[k + 2] : dq == 2 ? qq[k + 3] : qq[k + 4];
-                d[k] = funnel(lo, hi, bs);
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t lo = dq == 0 ? qq[k] : dq == 1 ? qq[k + 1] : dq == 2 ? qq[k + 2] : qq[k + 3];
+                    const uint32_t hi = dq == 0 ? qq[k + 1] : dq == 1 ? qq[k + 2] : dq == 2 ? qq[k + 3] : qq[k + 4];
+                    d[k] = funnel(lo, hi, bs);
+                }
             }
-            // zero the bytes before the packet; complement its first four (register preset)
+            // zero the bytes before the packet; complement its first four
+            // (register preset): only the chunks at a packet's start
             const int lead = static_cast<int>(static_cast<int64_t>(start - c));   // packet byte 0 in chunk
+            if (__builtin_amdgcn_ballot_w64(on && lead > -4) != 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t keep = bytes_from(lead, k);
-                d[k] &= keep;
-                if (len >= 4) d[k] ^= keep & ~bytes_from(lead + 4, k);
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t keep = bytes_from(lead, k);
+                    d[k] &= keep;
+                    if (len >= 4) d[k] ^= keep & ~bytes_from(lead + 4, k);
+                }
             }
             // raw CRC of the 16 bytes (slice-by-16), folded into the lane's stream
             uint32_t v = 0;
