@@ -195,3 +195,173 @@ def compress(p: bytes, out_limit: int):
     if r is None:
         return None
     return code(p, r[0], r[1], out_limit)
+
+
+# ---------------------------------------------------------------- wide mode
+#
+# Packets with a bucket over 64 positions (low-entropy data such as game
+# state) can rescale their sub-contexts (compress.c:90-112, :313-314), so the
+# closed-form statistics above no longer hold for them.  The wide scan
+# (rc_enc2.hip, rc_enc2_wscan) still derives every order-2/order-1 interval
+# from the packet, as explicit (under, count, total) triples:
+#   - buckets of <= 64 positions: the closed form, one lane per bucket;
+#   - bigger buckets: their elements sorted (stably) by a = x[i-2] into runs,
+#     one run per order-2 context; runs of <= DENSE_MIN visits by the closed
+#     form (no rescale before 127 visits), longer runs by a dense walk; then
+#     the bucket's order-1 visits (elements order 2 did not find, in position
+#     order) the same way.
+# A dense walk keeps the context's counts in a table and takes its visits 64
+# at a time (one per lane): a visit's count and under are the table's plus
+# the contributions of the earlier lanes of the round; the first lane whose
+# visit triggers a rescale ends the round (later lanes are redone after it).
+#
+# Wide record of position i: (A, B, root) with A the order-2 code, B the
+# order-1 code (None or (under, count, total)), root whether the root codes.
+
+DENSE_MIN = 32
+WAVE = 64
+
+
+def _closed_form(vals, found):
+    """Codes of a run of visits (values in visit order) with no rescale;
+    found[k] is set for visits that found their symbol."""
+    codes = []
+    for j, v in enumerate(vals):
+        t = j
+        same = sum(1 for k in range(j) if vals[k] == v)
+        less = sum(1 for k in range(j) if vals[k] < v)
+        dist = sum(1 for k in range(j) if not found[k])
+        esc, tot = 5 * dist, 5 * dist + 2 * t
+        if same:
+            codes.append((esc + 2 * less, 2 * same, tot))
+            found[j] = True
+        else:
+            codes.append((0, esc, tot) if esc > 0 else None)
+            found[j] = False
+    return codes
+
+
+def _dense_walk(vals, found):
+    """The same codes, rescales included, in rounds of WAVE visits."""
+    cnt = [0] * 256
+    esc = tot = 0
+    codes = [None] * len(vals)
+    base = 0
+    while base < len(vals):
+        lanes = vals[base: base + WAVE]
+        c = [cnt[v] + 2 * sum(1 for k in range(l) if lanes[k] == v) for l, v in enumerate(lanes)]
+        under = [sum(cnt[:v]) + 2 * sum(1 for k in range(l) if lanes[k] < v) for l, v in enumerate(lanes)]
+        new = [x == 0 for x in c]
+        jstar, rescale = len(lanes), False
+        out = []
+        for l, v in enumerate(lanes):
+            nb = sum(new[:l])
+            e_l, t_l = esc + 5 * nb, tot + 2 * l + 5 * nb
+            out.append((e_l + under[l], c[l], t_l) if c[l] else ((0, e_l, t_l) if e_l > 0 else None))
+            if c[l] > 251 or t_l + 2 + 5 * new[l] > 65280:     # compress.c:313-314
+                jstar, rescale = l + 1, True
+                break
+        for l in range(jstar):
+            codes[base + l] = out[l]
+            found[base + l] = not new[l]
+            cnt[lanes[l]] += 2
+            esc += 5 * new[l]
+            tot += 2 + 5 * new[l]
+        if rescale:                                            # compress.c:90-112
+            cnt = [x - (x >> 1) for x in cnt]
+            esc -= esc >> 1
+            tot = sum(cnt) + esc
+        base += jstar
+    return codes
+
+
+def _walk(vals, found):
+    if len(vals) <= DENSE_MIN:
+        return _closed_form(vals, found)
+    return _dense_walk(vals, found)
+
+
+def scan_wide(p: bytes):
+    """Wide-mode pass 1: one (A, B, root) record per position, or None for a
+    packet the wide scan does not take (empty, or long enough for a model
+    reset)."""
+    n = len(p)
+    if n == 0 or n > MAX_LEN:
+        return None
+    recs = [None] * n
+    recs[0] = (None, None, True)
+    buckets = defaultdict(list)
+    for i in range(1, n):
+        buckets[p[i - 1]].append(i)
+    for lst in buckets.values():
+        A = {}
+        f2 = {i: False for i in lst}
+        if len(lst) <= MAX_BUCKET:
+            runs = defaultdict(list)
+            for i in lst:
+                if i >= 2:
+                    runs[p[i - 2]].append(i)
+            for run in runs.values():
+                found = [False] * len(run)
+                for i, cd, fd in zip(run, _closed_form([p[i] for i in run], found), found):
+                    A[i], f2[i] = cd, fd
+        else:
+            # stable sort by a; position 1 (no order-2 context) apart
+            order = sorted((i for i in lst if i >= 2), key=lambda i: p[i - 2])
+            k = 0
+            while k < len(order):
+                e = k
+                while e < len(order) and p[order[e] - 2] == p[order[k] - 2]:
+                    e += 1
+                run = order[k:e]
+                found = [False] * len(run)
+                codes = _walk([p[i] for i in run], found)
+                for i, cd, fd in zip(run, codes, found):
+                    A[i], f2[i] = cd, fd
+                k = e
+        vis1 = [i for i in lst if not f2[i]]
+        found = [False] * len(vis1)
+        codes = _walk([p[i] for i in vis1], found) if len(lst) > MAX_BUCKET else _closed_form([p[i] for i in vis1], found)
+        B = {i: (cd, fd) for i, cd, fd in zip(vis1, codes, found)}
+        for i in lst:
+            if f2[i]:
+                recs[i] = (A.get(i), None, False)
+            else:
+                cd, fd = B[i]
+                recs[i] = (A.get(i), cd, not fd)
+    return recs
+
+
+def code_wide(p: bytes, recs, out_limit: int):
+    """Pass 2 over wide records: as code(), with explicit intervals."""
+    enc = _Enc(out_limit)
+    cnt = [0] * 256
+    rtot = 257
+    for i, v in enumerate(p):
+        a, b, root = recs[i]
+        for op in (a, b):
+            if op is not None:
+                enc.code(*op)
+        if root:
+            under = v + sum(cnt[:v])
+            c = 1 + cnt[v]
+            enc.code(1 + under, c, rtot)
+            cnt[v] += 3
+            rtot += 3
+            if c > 250 or rtot > 65280:
+                for u in range(256):
+                    cnt[u] -= cnt[u] >> 1
+                rtot = sum(cnt) + 1 + 256
+        if not enc.ok:
+            return 0, b""
+    enc.flush()
+    if not enc.ok:
+        return 0, b""
+    return len(enc.out), bytes(enc.out)
+
+
+def compress_wide(p: bytes, out_limit: int):
+    r = scan_wide(p)
+    if r is None:
+        return None
+    return code_wide(p, r, out_limit)

@@ -75,3 +75,53 @@ def test_fast_path_limits():
     assert twopass.scan(bytes(65)) is not None                # 64: still fast
     rnd = synth.random_bytes(1919, 7).tobytes()
     assert twopass.scan(rnd) is not None
+
+
+# ---- wide mode (rc_enc2_wscan / rc_enc2_wcode): packets with big buckets,
+# rescales included
+
+def _wide_packets():
+    rng = np.random.default_rng(5)
+    d, o, l = synth.gamestate_batch(6, 1200)
+    pk = [d[int(o[i]): int(o[i]) + 1200].tobytes() for i in range(6)]
+    pk += [bytes(n) for n in (1, 2, 3, 100, 300, 1000, 1919)]           # one context, rescales
+    pk += [bytes([7]) * n for n in (257, 1000)]
+    pk += [rng.choice([0, 0, 0, 1, 2], size=n).astype(np.uint8).tobytes() for n in (200, 800, 1919)]
+    pk += [(np.arange(n) % 2).astype(np.uint8).tobytes() for n in (500, 1919)]
+    pk += [np.where(rng.random(n) < 0.8, 0, rng.integers(0, 256, n)).astype(np.uint8).tobytes() for n in (400, 1919)]
+    pk += [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in (1, 5, 300)]
+    return pk
+
+
+@pytest.mark.parametrize("dense_min,max_bucket", [(32, 64), (0, 64), (0, 0), (1000, 0)])
+def test_wide_model_vs_oracle(port, monkeypatch, dense_min, max_bucket):
+    """Default thresholds, dense walks for every big-bucket run, the big-bucket
+    path for every bucket; (1000, 0): closed form everywhere, which must be
+    exact on exactly the packets with no rescale."""
+    monkeypatch.setattr(twopass, "DENSE_MIN", dense_min)
+    monkeypatch.setattr(twopass, "MAX_BUCKET", max_bucket)
+    closed_only = dense_min >= 1000
+    n_ok = 0
+    for p in _wide_packets():
+        for lim in (2 * len(p) + 64, len(p)):
+            r = twopass.compress_wide(p, lim)
+            ref = port.compress(p, out_limit=lim)
+            if closed_only:
+                n_ok += r == ref
+                continue
+            assert r == ref, (len(p), lim)
+    if closed_only:
+        assert 0 < n_ok < 2 * len(_wide_packets())       # rescales exist in the set
+
+
+def test_wide_model_golden_fixtures():
+    n = 0
+    for c in golden_io.compress_cases():
+        if c["in_limit"] != len(c["input"]) or not 0 < len(c["input"]) <= twopass.MAX_LEN:
+            continue
+        r = twopass.compress_wide(c["input"], c["out_limit"])
+        assert r[0] == c["ret"]
+        if c["ret"]:
+            assert r[1] == c["expect"]
+        n += 1
+    assert n > 100
