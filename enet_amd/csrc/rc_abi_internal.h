@@ -32,9 +32,10 @@ typedef struct {
 /* Device workspace owned by a coder context. */
 typedef struct {
     uint32_t *flag_list;    /* [n_cap] packets routed to the exact path */
-    uint32_t *counters;     /* [4]: 0 = flagged count, 1 = work queue head (fast), 2 = exact queue head,
+    uint32_t *counters;     /* [8]: 0 = flagged count, 1 = work queue head (fast), 2 = exact queue head,
                                3 = packets the two-pass encoder (compress) or the bucket-history
-                               decoder (decompress) leaves to the lane kernels */
+                               decoder (decompress) leaves to the lane kernels, 4 = packets the
+                               encoder's scan lists for its wide mode (per chunk) */
     void     *exact_pool;   /* exact_slots * RC_EXACT_POOL_BYTES */
     uint32_t  exact_slots;
     uint32_t  n_cap;
@@ -52,6 +53,11 @@ typedef struct {
     void     *enc2_stream;  /* NULL: the encoder is off (ENET_RC_ENC2=0) or not allocated yet */
     uint64_t  enc2_cap;     /* bytes */
     uint32_t *enc2_list;    /* [n_cap] */
+    /* its wide mode (packets with a bucket over 64 positions): 16-B records per position,
+       one slot per packet listed in enc2_wlist (count counters[4]); NULL: off (ENET_RC_ENC2_WIDE=0) */
+    void     *enc2_wide;
+    uint64_t  enc2_wide_cap;  /* bytes */
+    uint32_t *enc2_wlist;     /* [n_cap] */
     /* bucket-history decoder (rc_dec4.hip) in front of the v3 lane decoder; the packets it
        leaves go to enc2_list / counters[3] (ENET_RC_DEC4=0: off) */
     uint32_t  dec4;
@@ -80,6 +86,7 @@ int rc_hip_decompress(const rc_batch_dev *b, const rc_workspace_dev *ws, void *s
  * packets off its fast path are listed in ws->enc2_list, count in
  * ws->counters[3]). */
 uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len);
+uint64_t rc_hip_enc2_wide_slot_bytes(uint32_t max_len);
 int rc_hip_enc2_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
 
 /* Bucket-history decoder (rc_dec4.hip): one packet per lane over the lane

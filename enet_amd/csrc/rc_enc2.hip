@@ -61,7 +61,7 @@
 // Diagnostic build only (-DE2_PROF, tools/enc2_prof.py): per-phase cycles of
 // the scan pass, summed over wavefronts.  The product build has no stamps.
 #ifdef E2_PROF
-__device__ unsigned long long g_e2prof[16];
+__device__ unsigned long long g_e2prof[32];
 #define E2P_DECL unsigned long long e2p_t = __builtin_amdgcn_s_memtime(), e2p_acc[8] = {0};
 #define E2P(k) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
                  e2p_acc[k] += t_ - e2p_t; e2p_t = t_; __builtin_amdgcn_sched_barrier(0); }
@@ -71,7 +71,17 @@ struct E2Prof { unsigned long long t, acc[8]; };
 #define E2Q(k) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
                  pf.acc[k] += t_ - pf.t; pf.t = t_; __builtin_amdgcn_sched_barrier(0); }
 #define E2Q_FLUSH { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_e2prof[8 + k_], pf.acc[k_]); }
+// the wide scan: per-phase stamps into g_e2prof[16..27]
+struct W2Prof { unsigned long long t, acc[12]; };
+#define W2P(k) { __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+                 wp.acc[k] += t_ - wp.t; wp.t = t_; __builtin_amdgcn_sched_barrier(0); }
+#define W2P_INIT { wp.t = __builtin_amdgcn_s_memtime(); for (int k_ = 0; k_ < 12; ++k_) wp.acc[k_] = 0; }
+#define W2P_FLUSH { if ((threadIdx.x & 63) == 0) for (int k_ = 0; k_ < 12; ++k_) atomicAdd(&g_e2prof[16 + k_], wp.acc[k_]); }
 #else
+struct W2Prof {};
+#define W2P(k)
+#define W2P_INIT
+#define W2P_FLUSH
 struct E2Prof {};
 #define E2Q(k)
 #define E2Q_FLUSH
@@ -87,6 +97,7 @@ constexpr uint32_t kE2Bucket = 64;            // statistics <= 63
 constexpr uint32_t kScanThreads = 64;         // one wavefront per packet, four buckets per lane
 constexpr uint32_t kSkipFallback = 0xFFFFFFFFu;   // first word of a slot: lane kernels
 constexpr uint32_t kSkipDone = 0xFFFFFFFEu;       // empty packet, out_len already 0
+constexpr uint32_t kSkipWide = 0xFFFFFFFDu;       // the wide kernels (the smallest marker)
 
 struct E2Params {
     uint8_t*        stream;     // record stream, one slot per packet of the chunk
@@ -100,6 +111,12 @@ struct E2Params {
     uint32_t        act;        // pass 2: packets per wavefront (64 or 32)
     uint8_t*        dummy;      // pass 2: 1 MB, 16 B per lane, the target of stores with nothing to store
     uint32_t        slow;       // test switch (ENET_RC_ENC2_SLOW=1): every position exceptional, every bucket re-walked
+    // wide mode (below): packets with a bucket over kE2Bucket positions
+    uint8_t*        wide;       // wide record stream, one slot per listed packet, or null (off)
+    uint64_t        wslot_bytes;
+    uint32_t*       wlist;      // listed packets (batch indices), count *wcount, at most wcap slots
+    uint32_t*       wcount;
+    uint32_t        wcap;
 };
 
 // the last element slot: buckets of 1918 positions, each padded to 4, end
@@ -128,6 +145,8 @@ struct ScanLds {
     uint8_t  xlist[256];              // buckets with one
     uint32_t fb[32];                  // packets for the lane kernels, not yet listed
     uint32_t nfb;
+    uint32_t wb[32];                  // packets for the wide kernels (batch indices), not yet listed
+    uint32_t nwb;
 };
 
 // element word: pos (0-10) | v (11-18) | a | 256 (19-27, 0 for position 1) |
@@ -135,15 +154,29 @@ struct ScanLds {
 //               exceptional (31).  A plain position has flags 0.
 constexpr uint32_t kF2 = 1u << 28, kNV1 = 1u << 29, kF1 = 1u << 30, kExc = 1u << 31;
 
+// inclusive prefix sum over the wavefront's lanes: DPP row shifts within
+// rows of 16, then the row broadcasts (no LDS round trips)
 DEV uint32_t wave_incl_scan(uint32_t x)
 {
-    const int l = static_cast<int>(threadIdx.x & 63);
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        x += l >= d ? y : 0u;
-    }
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);   // row_bcast:31
     return x;
+}
+
+// the maximum over the wavefront's lanes (the same network, max for +)
+DEV uint32_t wave_max(uint32_t x)
+{
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false)));
+    return __builtin_amdgcn_readlane(x, 63);
 }
 
 DEV bool bit_at(const uint32_t* m, uint32_t i) { return (m[i >> 5] >> (i & 31)) & 1; }
@@ -194,6 +227,48 @@ DEV void fb_add(ScanLds& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uin
     }
     wave_sync();
     if (s.nfb == 32) fb_flush(s, e, t);
+}
+
+// The wavefront's packets for the wide kernels, 32 per global atomic as
+// above; a packet past the wide stream's capacity goes to the lane kernels.
+DEV void wb_flush(ScanLds& s, const E2Params& e, uint32_t t)
+{
+    wave_sync();
+    const uint32_t k = s.nwb;
+    if (k == 0) return;
+    uint32_t base = 0;
+    if (t == 0) base = atomicAdd(e.wcount, k);
+    base = __shfl(base, 0, 64);
+    if (t < k) {
+        const uint32_t idx = s.wb[t];
+        uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
+        if (base + t < e.wcap) {
+            slot[0] = kSkipWide;
+            e.wlist[base + t] = idx;
+        } else {
+            slot[0] = kSkipFallback;
+            e.list[atomicAdd(e.count, 1u)] = packet_of(e, idx);
+        }
+    }
+    wave_sync();
+    if (t == 0) s.nwb = 0;
+    wave_sync();
+}
+
+// a packet with a bucket over kE2Bucket positions: the wide kernels, or the
+// lane kernels when wide mode is off
+DEV void big_add(ScanLds& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uint32_t idx, uint32_t t)
+{
+    if (!e.wide) {
+        fb_add(s, e, slot, pkt, t);
+        return;
+    }
+    if (t == 0) {
+        s.wb[s.nwb] = idx;
+        s.nwb = s.nwb + 1;
+    }
+    wave_sync();
+    if (s.nwb == 32) wb_flush(s, e, t);
 }
 
 // one predecessor u of an element (v, akey): SWAR accumulators
@@ -391,7 +466,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
 #else
     const bool ordered = false;
 #endif
-    if (t == 0) s.nfb = 0;
+    if (t == 0) { s.nfb = 0; s.nwb = 0; }
     ScanPf pf = scan_prefetch(b, e, e.lo + blockIdx.x);
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const ScanPf cur = pf;
@@ -464,7 +539,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
         const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
         if (any_lane(mx > kE2Bucket)) {
-            fb_add(s, e, slot, pkt, t);
+            big_add(s, e, slot, pkt, idx, t);
             pf = scan_prefetch(b, e, idx + gridDim.x);
             continue;
         }
@@ -543,7 +618,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             if (m1) s.xlist[o++] = static_cast<uint8_t>(4 * t + 1);
             if (m2) s.xlist[o++] = static_cast<uint8_t>(4 * t + 2);
             if (m3) s.xlist[o++] = static_cast<uint8_t>(4 * t + 3);
-            const uint32_t nx = __shfl(incl, 63, 64);
+            const uint32_t nx = __builtin_amdgcn_readlane(incl, 63);
             wave_sync();
 #pragma unroll 1
             for (uint32_t q = t; q < nx; q += kScanThreads) {
@@ -572,6 +647,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
         E2P(5)
     }
     fb_flush(s, e, t);
+    wb_flush(s, e, t);
     E2P_FLUSH
 }
 
@@ -822,7 +898,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     if (idx >= e.hi) return;
     const uintptr_t base = reinterpret_cast<uintptr_t>(e.stream) + static_cast<size_t>(idx - e.lo) * e.slot_bytes;
     uint4 c0 = gload16(base);
-    if (c0.x >= kSkipDone) return;                    // lane kernels / empty
+    if (c0.x >= kSkipWide) return;                    // lane kernels / wide kernels / empty
     uint4 c1 = gload16(base + 16), c2 = gload16(base + 32);
     // (a wavefront's dummies are 1 KB contiguous: every store is one coalesced
     // 1-KB write to lines that stay in L2; a dummy per lane in its own line
@@ -1054,7 +1130,7 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     const uint32_t idx = e.lo + blockIdx.x * 256 + lane;
     const uintptr_t base = reinterpret_cast<uintptr_t>(e.stream) + static_cast<size_t>(min(idx, e.hi - 1) - e.lo) * e.slot_bytes;
     const uintptr_t slot_last = base + e.slot_bytes - 16;
-    const bool live = idx < e.hi && gload16(base).x < kSkipDone;   // (else: lane kernels / empty / past the chunk)
+    const bool live = idx < e.hi && gload16(base).x < kSkipWide;   // (else: lane / wide kernels, empty, past the chunk)
     const uint32_t pkt = packet_of(e, min(idx, e.hi - 1));
     const uint32_t len = live ? b.in_len[pkt] : 0u;
     __syncthreads();
@@ -1148,15 +1224,684 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     if (live) b.out_len[pkt] = ok ? o.n : 0u;
 }
 
+// ------------------------------------------------------------------ wide mode
+//
+// Packets with a bucket over kE2Bucket positions (low-entropy data: game
+// state) can rescale their sub-contexts (compress.c:90-112, :313-314), which
+// the closed form of pass 1 does not model.  rc_enc2_scan lists them (up to
+// slot_len bytes) for these two kernels instead of the lane kernels:
+//
+//   rc_enc2_wscan (wavefront per listed packet, LDS): every position's
+//     order-2 and order-1 codes as explicit (under, count, total) intervals.
+//     Buckets of <= kE2Bucket positions: the closed form, one lane per bucket.
+//     Bigger buckets, one at a time with the whole wavefront: the elements
+//     sorted (stably) by a = x[i-2] into runs, one per order-2 context; runs of
+//     <= kWideDense visits by the closed form (no rescale before a symbol's
+//     127th visit), longer ones by a dense walk; then the bucket's order-1
+//     visits (the elements order 2 did not find, in position order) the same
+//     way.  A dense walk keeps the context's counts in an LDS table and takes
+//     its visits 64 at a time, one per lane: a visit's count and under are the
+//     table's plus twice the earlier lanes' visits of the same / smaller
+//     symbols, its escapes and total the running ones plus the earlier lanes'
+//     new symbols; the first lane whose visit rescales ends the round, and the
+//     lanes after it are redone in the next round on the rescaled table.
+//   rc_enc2_wcode (lane per listed packet): the root and the range coder over
+//     the explicit records, as rc_enc2_code.
+//
+// Wide record of position i (16 B, in the wide stream, slot = list position):
+//   x = underA | countA << 16    the order-2 code, (0, 1, 1) when none
+//   y = totalA | v << 16
+//   z = underB | countB << 16    the order-1 code
+//   w = totalB | B coded << 16 | root codes << 17
+// (an absent code is the identity interval, which the coder passes through).
+// tests/proto/twopass.py (scan_wide, code_wide) restates both kernels.
+
+constexpr uint32_t kWideDense = 32;             // runs longer than this take a dense walk
+
+struct WScanLds {
+    uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i]; then a big bucket's run sizes / starts
+    uint32_t cnt[256];                // bucket sizes, then fill pointers
+    uint32_t start[256];              // bucket starts (4-aligned)
+    uint32_t e[2048 + 768];           // elements in bucket order (element word as in pass 1)
+    uint32_t sw[2048];                // a big bucket's element words by a, then its order-1 visits
+    uint32_t f2bits[64];              // positions found at order 2 (big buckets)
+    uint32_t tab[64];                 // dense walk: a round's updated counts (256 bytes); rank counts
+    uint32_t runs[64];                // a big bucket's long runs (a keys)
+    uint32_t nruns;
+};
+
+DEV uint32_t lane_id() { return threadIdx.x & 63; }
+DEV uint64_t below_mask() { return (1ull << lane_id()) - 1ull; }
+DEV uint32_t popc64(uint64_t m) { return static_cast<uint32_t>(__builtin_popcountll(m)); }
+
+// The lanes of `act` whose 8-bit key equals this lane's, from eight ballots
+// (one per key bit: at each bit, keep the lanes that agree with this lane);
+// lt: how many lanes below this one (of `act`) hold a smaller key (counted at
+// the highest bit where they differ).  No LDS, no atomics, any number of
+// distinct keys.
+DEV uint64_t match8(uint32_t key, uint64_t act, uint32_t& lt)
+{
+    const uint64_t below = below_mask();
+    uint64_t e = act;
+    lt = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const bool one = (key >> b) & 1u;
+        const uint64_t B = __builtin_amdgcn_ballot_w64(one);
+        lt += one ? popc64(e & ~B & below) : 0u;
+        e &= one ? B : ~B;
+    }
+    return e;
+}
+
+// cnt[key] += 1 for every lane with ok: one LDS atomic per distinct key (its
+// lowest lane adds the group's size).  RET: returns the lane's slot, the old
+// value plus its rank among the lanes with its key (lane order).
+template <bool RET>
+DEV uint32_t group_add(uint32_t* cnt, uint32_t key, bool ok)
+{
+    const uint32_t t = lane_id();
+    uint32_t lt;
+    const uint64_t e = match8(key, __builtin_amdgcn_ballot_w64(ok), lt);
+    const uint32_t ld = e ? static_cast<uint32_t>(__builtin_ctzll(e)) : t;
+    uint32_t old = 0;
+    if (ok && t == ld) {
+        if (RET) old = atomicAdd(&cnt[key], popc64(e));
+        else atomicAdd(&cnt[key], popc64(e));
+    }
+    if (!RET) return 0;
+    return __shfl(old, static_cast<int>(ld), 64) + popc64(e & below_mask());
+}
+
+// the identity interval: a code that changes nothing
+constexpr uint32_t kNoCodeLo = 1u << 16;        // under 0, count 1
+constexpr uint32_t kNoCodeTot = 1u;
+constexpr uint32_t kPadWord = 0xFFFFFFFFu;      // bucket padding in WScanLds::e
+
+// explicit interval of a sub-context visit from its statistics (t earlier
+// visits, dist of them new, same / less earlier visits of this / a smaller
+// symbol; no rescale): (lo = under | count << 16, total), or the identity
+DEV uint2 closed_code(uint32_t t, uint32_t dist, uint32_t same, uint32_t less)
+{
+    const uint32_t esc = kSubEscDelta * dist, tot = esc + kSubDelta * t;
+    if (same) return make_uint2((esc + kSubDelta * less) | (kSubDelta * same) << 16, tot);
+    if (esc) return make_uint2(esc << 16, tot);
+    return make_uint2(kNoCodeLo, kNoCodeTot);
+}
+
+DEV uint32_t akey_of(uint32_t w) { return (w & (256u << 19)) ? (w >> 19) & 511 : 1024u; }   // 1024: none (position 1)
+
+// Buckets of <= kE2Bucket elements, element-parallel (a lane per element,
+// over its bucket predecessors, eight per two LDS reads), in three passes over
+// the list of their elements (s.sw: element index | bucket start << 16):
+// (0) found at order 2 (an earlier element of the bucket with the same a and
+// v); (1) the order-2 statistics -> record half A, and found at order 1 (an
+// earlier order-1 visitor with the same v); (2) the order-1 statistics of the
+// order-1 visitors -> record half B.  Each pass reads only flags the previous
+// ones wrote.
+template <uint32_t pass>
+DEV void wide_small_pass(WScanLds& s, uint32_t ns, uint2* wrec)
+{
+    const uint32_t t = lane_id();
+#pragma unroll 1
+    for (uint32_t base = 0; base < ns; base += 64) {
+        const uint32_t li = base + t;
+        const uint32_t ent = s.sw[li < ns ? li : ns - 1];
+        const uint32_t ei = ent & 0xFFFF, bs = ent >> 16;
+        const uint32_t w = s.e[ei];
+        const uint32_t v = (w >> 11) & 255, akey = akey_of(w);
+        const bool f2 = (w & kF2) != 0;
+        const bool act = li < ns && !(pass == 2 && f2);
+        const uint32_t nq = act ? ei - bs : 0u;
+        uint32_t acc2 = 0, acc1 = 0;                  // t | same << 8 | less << 16 | dist << 24
+        bool hit = false;
+#pragma unroll 1
+        for (uint32_t q = 0; q < nq; q += 8) {
+            const uint4 ua = *reinterpret_cast<const uint4*>(&s.e[bs + q]);
+            const uint4 ub = *reinterpret_cast<const uint4*>(&s.e[bs + q + 4]);
+#pragma unroll
+            for (uint32_t c = 0; c < 8; ++c) {
+                const uint32_t u = pick4(c & 3, c < 4 ? ua : ub);
+                const bool in = q + c < nq;
+                const uint32_t uv = (u >> 11) & 255;
+                const uint32_t one = 1u | (uv == v ? 0x100u : 0u) | (uv < v ? 0x10000u : 0u);
+                if constexpr (pass == 0) {
+                    hit = hit || (in && ((u >> 19) & 511) == akey && uv == v);
+                } else if constexpr (pass == 1) {
+                    const bool m2 = in && ((u >> 19) & 511) == akey;
+                    acc2 += m2 ? (one | ((u & kF2) ? 0u : 0x1000000u)) : 0u;
+                    hit = hit || (in && !f2 && (u & kF2) == 0 && uv == v);
+                } else {
+                    const bool m1 = in && (u & kF2) == 0;
+                    acc1 += m1 ? (one | ((u & kF1) ? 0u : 0x1000000u)) : 0u;
+                }
+            }
+        }
+        if (!act) continue;
+        const uint32_t pos = w & 2047;
+        if constexpr (pass == 0) {
+            if (hit) s.e[ei] = w | kF2;
+        } else if constexpr (pass == 1) {
+            const uint2 a = closed_code(acc2 & 255, acc2 >> 24, (acc2 >> 8) & 255, (acc2 >> 16) & 255);
+            wrec[2 * pos] = make_uint2(a.x, a.y | v << 16);
+            if (f2) wrec[2 * pos + 1] = make_uint2(kNoCodeLo, kNoCodeTot);
+            else if (hit) s.e[ei] = w | kF1;
+        } else {
+            const uint2 bq = closed_code(acc1 & 255, acc1 >> 24, (acc1 >> 8) & 255, (acc1 >> 16) & 255);
+            const bool coded = bq.y != kNoCodeTot || bq.x != kNoCodeLo;
+            wrec[2 * pos + 1] = make_uint2(bq.x, bq.y | (coded ? 1u << 16 : 0u) | ((w & kF1) ? 0u : 1u << 17));
+        }
+    }
+}
+
+// A big bucket's short order-2 runs (<= kWideDense visits: no rescale),
+// element-parallel over their sorted words sw[0, ks) (short runs first):
+// (0) found (an earlier element of the run with the same v); (1) the
+// statistics -> record half A, and the position's order-2 hit bit.
+template <uint32_t pass>
+DEV void wide_run_pass(WScanLds& s, uint32_t ks, const uint32_t* hist, const uint32_t* rend, uint2* wrec)
+{
+    const uint32_t t = lane_id();
+#pragma unroll 1
+    for (uint32_t base = 0; base < ks; base += 64) {
+        const uint32_t j = base + t;
+        const bool act = j < ks;
+        const uint32_t w = s.sw[act ? j : ks - 1];
+        const uint32_t a = (w >> 19) & 255;
+        const uint32_t rs = rend[a] - hist[a];
+        const uint32_t v = (w >> 11) & 255;
+        const uint32_t q0 = rs & ~3u;
+        const uint32_t nq = act ? j - q0 : 0u;
+        uint32_t acc = 0;
+        bool hit = false;
+#pragma unroll 1
+        for (uint32_t q = 0; q < nq; q += 8) {
+            const uint4 ua = *reinterpret_cast<const uint4*>(&s.sw[q0 + q]);
+            const uint4 ub = *reinterpret_cast<const uint4*>(&s.sw[q0 + q + 4]);
+#pragma unroll
+            for (uint32_t c = 0; c < 8; ++c) {
+                const uint32_t u = pick4(c & 3, c < 4 ? ua : ub);
+                const bool in = q + c < nq && q0 + q + c >= rs;
+                const uint32_t uv = (u >> 11) & 255;
+                if constexpr (pass == 0) {
+                    hit = hit || (in && uv == v);
+                } else {
+                    const uint32_t one = 1u | (uv == v ? 0x100u : 0u) | (uv < v ? 0x10000u : 0u);
+                    acc += in ? (one | ((u & kF2) ? 0u : 0x1000000u)) : 0u;
+                }
+            }
+        }
+        if (!act) continue;
+        const uint32_t pos = w & 2047;
+        if constexpr (pass == 0) {
+            if (hit) s.sw[j] = w | kF2;
+        } else {
+            const uint2 c = closed_code(acc & 255, acc >> 24, (acc >> 8) & 255, (acc >> 16) & 255);
+            wrec[2 * pos] = make_uint2(c.x, c.y | v << 16);
+            if (w & kF2) {
+                wrec[2 * pos + 1] = make_uint2(kNoCodeLo, kNoCodeTot);
+                atomicOr(&s.f2bits[pos >> 5], 1u << (pos & 31));
+            }
+        }
+    }
+}
+
+// bytes of x that are not zero, as 0xFF bytes
+DEV uint32_t nonzero_bytes(uint32_t x)
+{
+    const uint32_t y = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+    return ((y >> 7) & 0x01010101u) * 0xFFu;
+}
+
+// The dense walk of one context's visits (element words list[0..m), visit
+// order), the whole wavefront, compress.c:286-316 with rescales (see the
+// section header).  The context's 256 counts live in registers, four per
+// lane (lane l: symbols 4l .. 4l+3), with the counts below each lane's four
+// (a wave prefix sum); a visit reads its symbol's dword and prefix from the
+// owning lane (ds_bpermute).  order2: record half A, a hit sets the
+// position's order-2 hit bit and closes half B; else half B with the root
+// flag.
+DEV void wide_dense_walk(WScanLds& s, const uint32_t* list, uint32_t m, bool order2, uint2* wrec)
+{
+    const uint32_t t = lane_id();
+    uint8_t* sc = reinterpret_cast<uint8_t*>(s.tab);   // a round's final counts of its symbols (0: untouched)
+    uint32_t tabr = 0, pre = 0;
+    uint32_t esc = 0, tot = 0;                        // (wave-uniform)
+    s.tab[t] = 0;
+    wave_sync();
+#pragma unroll 1
+    for (uint32_t base = 0; base < m;) {
+        const uint32_t j = base + t;
+        const bool act = j < m;
+        const uint32_t w = list[act ? j : m - 1];
+        const uint32_t pos = w & 2047, v = (w >> 11) & 255;
+        const uint32_t dw = __shfl(tabr, static_cast<int>(v >> 2), 64);
+        const uint32_t pd = __shfl(pre, static_cast<int>(v >> 2), 64);
+        const uint32_t sh = 8 * (v & 3);
+        const uint32_t c0 = (dw >> sh) & 255;
+        // lanes of this round with the same symbol; earlier ones with a smaller one
+        uint32_t lt;
+        const uint64_t m_mine = match8(v, __builtin_amdgcn_ballot_w64(act), lt);
+        const uint32_t eq = popc64(m_mine & below_mask());
+        const uint32_t c = c0 + kSubDelta * eq;
+        const uint32_t under = pd + sad(dw & ((1u << sh) - 1u), 0u) + kSubDelta * lt;
+        const bool isnew = act && c == 0;
+        const uint64_t nm = __builtin_amdgcn_ballot_w64(isnew);
+        const uint32_t nb = popc64(nm & below_mask());
+        const uint32_t esc_l = esc + kSubEscDelta * nb;
+        const uint32_t tot_l = tot + kSubDelta * t + kSubEscDelta * nb;
+        const bool resc = act && (c > 0xFF - 2 * kSubDelta ||
+                                  tot_l + kSubDelta + (isnew ? kSubEscDelta : 0u) > kTotalLimit);
+        const uint64_t rm = __builtin_amdgcn_ballot_w64(resc);
+        const uint32_t jstar = rm ? static_cast<uint32_t>(__builtin_ctzll(rm)) : 64u;
+        const bool commit = act && t <= jstar;
+        const bool hit = c != 0;
+        uint2 code;
+        if (hit) code = make_uint2((esc_l + under) | c << 16, tot_l);
+        else if (esc_l) code = make_uint2(esc_l << 16, tot_l);
+        else code = make_uint2(kNoCodeLo, kNoCodeTot);
+        if (commit) {
+            if (order2) {
+                wrec[2 * pos] = make_uint2(code.x, code.y | v << 16);
+                if (hit) {
+                    wrec[2 * pos + 1] = make_uint2(kNoCodeLo, kNoCodeTot);
+                    atomicOr(&s.f2bits[pos >> 5], 1u << (pos & 31));
+                }
+            } else {
+                const bool coded = hit || esc_l != 0;
+                wrec[2 * pos + 1] = make_uint2(code.x, code.y | (coded ? 1u << 16 : 0u) | (hit ? 0u : 1u << 17));
+            }
+        }
+        // the table: the last committed visit of each symbol posts its count,
+        // the owning lanes merge them
+        const uint64_t cm = __builtin_amdgcn_ballot_w64(commit);
+        const uint64_t later = t == 63 ? 0ull : (m_mine & cm) >> (t + 1);
+        if (commit && later == 0) sc[v] = static_cast<uint8_t>(c + kSubDelta);
+        wave_sync();
+        const uint32_t nw = s.tab[t];
+        s.tab[t] = 0;
+        tabr = (tabr & ~nonzero_bytes(nw)) | nw;
+        const uint32_t ncm = popc64(cm), nnew = popc64(nm & cm);
+        esc += kSubEscDelta * nnew;
+        tot += kSubDelta * ncm + kSubEscDelta * nnew;
+        if (jstar < 64) {
+            // rescale after visit jstar (compress.c:90-112): halve every count
+            // (rounding up), escapes likewise, total = counts + escapes
+            tabr = tabr - ((tabr >> 1) & 0x7F7F7F7Fu);
+            esc -= esc >> 1;
+        }
+        const uint32_t bsum = sad(tabr, 0u);
+        const uint32_t incl = wave_incl_scan(bsum);
+        pre = incl - bsum;
+        if (jstar < 64) {
+            tot = __builtin_amdgcn_readlane(incl, 63) + esc;
+            base += jstar + 1;
+        } else {
+            base += 64;
+        }
+    }
+    wave_sync();
+}
+
+// a big bucket of a wide packet (> kE2Bucket elements, [bs, bs + k) in
+// position order), the whole wavefront
+DEV void wide_big_bucket(WScanLds& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp)
+{
+    const uint32_t t = lane_id();
+    uint32_t* hist = reinterpret_cast<uint32_t*>(s.x);          // [256] run sizes by a
+    uint32_t* rst = hist + 256;                                  // [256] run starts, then run ends
+    *reinterpret_cast<uint4*>(&hist[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
+    if (t == 0) s.nruns = 0;
+    wave_sync();
+    // order 2: the elements' a (position 1 has none: its record half A is the identity)
+#pragma unroll 1
+    for (uint32_t q = 0; q < k; q += 64) {
+        const bool ok0 = q + t < k;
+        const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
+        const bool has = (w & (256u << 19)) != 0;
+        group_add<false>(hist, (w >> 19) & 255, ok0 && has);
+        if (ok0 && !has) wrec[2 * (w & 2047)] = make_uint2(kNoCodeLo, kNoCodeTot | ((w >> 11) & 255) << 16);
+    }
+    wave_sync();
+    uint32_t ks;
+    {
+        // run starts: the short runs first (sw[0, ks)), then the long ones
+        const uint4 h = *reinterpret_cast<const uint4*>(&hist[4 * t]);
+        const uint4 hs = make_uint4(h.x <= kWideDense ? h.x : 0u, h.y <= kWideDense ? h.y : 0u,
+                                    h.z <= kWideDense ? h.z : 0u, h.w <= kWideDense ? h.w : 0u);
+        const uint4 hl = make_uint4(h.x - hs.x, h.y - hs.y, h.z - hs.z, h.w - hs.w);
+        const uint32_t ms = hs.x + hs.y + hs.z + hs.w, ml = hl.x + hl.y + hl.z + hl.w;
+        const uint32_t is = wave_incl_scan(ms), il = wave_incl_scan(ml);
+        ks = __builtin_amdgcn_readlane(is, 63);
+        const uint32_t ss = is - ms, sl = ks + il - ml;
+        *reinterpret_cast<uint4*>(&rst[4 * t]) =
+            make_uint4(h.x <= kWideDense ? ss : sl,
+                       h.y <= kWideDense ? ss + hs.x : sl + hl.x,
+                       h.z <= kWideDense ? ss + hs.x + hs.y : sl + hl.x + hl.y,
+                       h.w <= kWideDense ? ss + hs.x + hs.y + hs.z : sl + hl.x + hl.y + hl.z);
+    }
+    wave_sync();
+    // stable scatter of the element words by a into sw (run starts become run ends)
+#pragma unroll 1
+    for (uint32_t q = 0; q < k; q += 64) {
+        const bool ok0 = q + t < k;
+        const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
+        const bool has = ok0 && (w & (256u << 19)) != 0;
+        const uint32_t rk = group_add<true>(rst, (w >> 19) & 255, has);
+        if (has) s.sw[rk] = w;
+    }
+    wave_sync();
+    W2P(5)
+    // short runs: the closed form, element-parallel; long runs: dense walks
+    wide_run_pass<0>(s, ks, hist, rst, wrec);
+    wave_sync();
+    wide_run_pass<1>(s, ks, hist, rst, wrec);
+#pragma unroll 1
+    for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t a = 4 * t + r;
+        if (hist[a] > kWideDense) s.runs[atomicAdd(&s.nruns, 1u)] = a;
+    }
+    wave_sync();
+    W2P(6)
+    const uint32_t nr = s.nruns;
+#pragma unroll 1
+    for (uint32_t r = 0; r < nr; ++r) {
+        const uint32_t a = s.runs[r];
+        const uint32_t len = hist[a], st = rst[a] - len;
+        wide_dense_walk(s, s.sw + st, len, true, wrec);
+    }
+    wave_sync();
+    W2P(7)
+    // order 1: the elements order 2 did not find, in position order (a dense walk)
+    uint32_t m1 = 0;
+#pragma unroll 1
+    for (uint32_t q = 0; q < k; q += 64) {
+        const bool ok0 = q + t < k;
+        const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
+        const uint32_t pos = w & 2047;
+        const bool vis = ok0 && !bit_at(s.f2bits, pos);
+        const uint64_t vm = __builtin_amdgcn_ballot_w64(vis);
+        if (vis) s.sw[m1 + popc64(vm & below_mask())] = w;
+        m1 += popc64(vm);
+    }
+    wave_sync();
+    W2P(8)
+    wide_dense_walk(s, s.sw, m1, false, wrec);
+    wave_sync();
+    W2P(9)
+}
+
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_wscan(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) WScanLds s;
+    const uint32_t t = threadIdx.x;
+    const uint32_t nw = min(*e.wcount, e.wcap);
+    W2Prof wp;
+    W2P_INIT
+    for (uint32_t q = blockIdx.x; q < nw; q += gridDim.x) {
+        const uint32_t idx = e.wlist[q];
+        const uint32_t pkt = packet_of(e, idx);
+        const uint32_t n = b.in_len[pkt];             // (1 <= n <= slot_len: rc_enc2_scan)
+        uint2* wrec = reinterpret_cast<uint2*>(e.wide + static_cast<size_t>(q) * e.wslot_bytes);
+        const uintptr_t src = reinterpret_cast<uintptr_t>(b.in + b.in_off[pkt]);
+        const uintptr_t a16 = src & ~static_cast<uintptr_t>(15);
+        const uint32_t mis = static_cast<uint32_t>(src & 15);
+        const uint32_t last = (mis + n - 1) >> 4;
+        const uint4 r0 = gload16(a16 + 16 * min(t, last));
+        const uint4 r1 = gload16(a16 + 16 * min(t + kScanThreads, last));
+        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
+        if (t < 16) *reinterpret_cast<uint4*>(&s.f2bits[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = r0;
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = r1;
+        wave_sync();
+        W2P(0)
+        const uint32_t q0 = 16 + mis;
+        // bucket sizes
+#pragma unroll 1
+        for (uint32_t i = 1 + t; i < n + t; i += kScanThreads) {
+            const bool ok = i < n;
+            const uint32_t p = s.x[q0 + (ok ? i : 1) - 1];
+            group_add<false>(s.cnt, p, ok);
+        }
+        wave_sync();
+        W2P(1)
+        const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
+        const uint32_t a0 = (c4.x + 3) & ~3u, a1 = (c4.y + 3) & ~3u, a2 = (c4.z + 3) & ~3u, a3 = (c4.w + 3) & ~3u;
+        const uint32_t mine = a0 + a1 + a2 + a3;
+        const uint32_t incl = wave_incl_scan(mine);
+        const uint32_t st = incl - mine;
+        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        const uint4 s4 = make_uint4(st, st + a0, st + a0 + a1, st + a0 + a1 + a2);
+        *reinterpret_cast<uint4*>(&s.start[4 * t]) = s4;
+        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
+        // the buckets' padding (to 4) marked, for the element-parallel passes
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t e0 = pick4(r, s4) + pick4(r, c4), e1 = pick4(r, s4) + ((pick4(r, c4) + 3) & ~3u);
+            for (uint32_t j = e0; j < e1; ++j) s.e[j] = kPadWord;
+        }
+        wave_sync();
+        W2P(2)
+        // scatter into buckets, position order (two positions per lane and iteration)
+#pragma unroll 1
+        for (uint32_t i = 1 + t; i < n + t; i += 2 * kScanThreads) {
+            uint32_t w[2], p[2];
+            bool ok[2];
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t i2 = i + h * kScanThreads;
+                ok[h] = i2 < n;
+                const uint32_t ii = ok[h] ? i2 : 1u;
+                const uint32_t b3 = bytes3(s.x, q0 + max(ii, 2u));   // (position 1: its a byte unused)
+                p[h] = s.x[q0 + ii - 1];
+                const uint32_t v = s.x[q0 + ii];
+                w[h] = ii | v << 11 | (ii >= 2 ? ((b3 & 255) | 256u) << 19 : 0u);
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t slot = group_add<true>(s.cnt, p[h], ok[h]);
+                if (ok[h]) s.e[slot] = w[h];
+            }
+        }
+        const uint32_t x0 = s.x[q0];
+        wave_sync();
+        W2P(3)
+        // buckets of <= kE2Bucket elements, element-parallel over the list of
+        // their elements (in s.sw: element index | bucket start << 16),
+        // ordered by rank in the bucket, highest first: a lane's work is its
+        // rank, and a round costs its longest lane
+        uint32_t* rfill = reinterpret_cast<uint32_t*>(s.tab);        // [64] rank counts, then fill pointers
+        s.tab[t] = 0;
+        wave_sync();
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t kk = pick4(r, c4);
+            if (kk && kk <= kE2Bucket) {
+                atomicAdd(&rfill[0], 1u);                             // ranks 0 .. kk - 1: a range add
+                if (kk < 64) atomicSub(&rfill[kk], 1u);
+            }
+        }
+        wave_sync();
+        uint32_t ns;
+        {
+            const uint32_t cr = wave_incl_scan(s.tab[t]);             // elements of rank t
+            const uint32_t above = wave_incl_scan(__shfl(cr, static_cast<int>(63 - t), 64));   // ranks > 63 - t, incl.
+            ns = __builtin_amdgcn_readlane(above, 63);
+            // rank t starts after every element of a higher rank
+            const uint32_t start_t = __shfl(above - __shfl(cr, static_cast<int>(63 - t), 64), static_cast<int>(63 - t), 64);
+            wave_sync();
+            s.tab[t] = start_t;
+        }
+        wave_sync();
+#pragma unroll 1
+        for (uint32_t base = 0; base < total; base += 64) {
+            const uint32_t ei = base + t;
+            const uint32_t w = ei < total ? s.e[ei] : kPadWord;
+            bool sm = w != kPadWord;
+            uint32_t bs = 0;
+            if (sm) {
+                const uint32_t p = s.x[q0 + (w & 2047) - 1];
+                bs = s.start[p];
+                sm = s.cnt[p] - bs <= kE2Bucket;
+            }
+            if (sm) s.sw[atomicAdd(&rfill[ei - bs], 1u)] = ei | bs << 16;
+        }
+        wave_sync();
+        if (ns) {
+            wide_small_pass<0>(s, ns, wrec);
+            wave_sync();
+            wide_small_pass<1>(s, ns, wrec);
+            wave_sync();
+            wide_small_pass<2>(s, ns, wrec);
+            wave_sync();
+        }
+        W2P(4)
+        // big ones: the wavefront, one at a time
+        uint32_t bigm = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) bigm |= pick4(r, c4) > kE2Bucket ? 1u << r : 0u;
+        uint64_t bl = __builtin_amdgcn_ballot_w64(bigm != 0);
+        while (bl != 0) {
+            const uint32_t ld = static_cast<uint32_t>(__builtin_ctzll(bl));
+            const uint32_t bm = __builtin_amdgcn_readlane(bigm, ld);
+#pragma unroll 1
+            for (uint32_t r = 0; r < 4; ++r) {
+                if (!((bm >> r) & 1u)) continue;
+                const uint32_t bk = 4 * ld + r;
+                wide_big_bucket(s, s.start[bk], s.cnt[bk] - s.start[bk], wrec, wp);
+            }
+            bl &= bl - 1;
+        }
+        if (t == 0) {                                 // position 0: root only
+            wrec[0] = make_uint2(kNoCodeLo, kNoCodeTot | x0 << 16);
+            wrec[1] = make_uint2(kNoCodeLo, kNoCodeTot | 1u << 17);
+        }
+        wave_sync();
+        W2P(10)
+    }
+    W2P_FLUSH
+}
+
+// ---- wide code pass: rc_enc2_code over explicit records
+DEV Pre prep_wide(const uint4& r, bool en)
+{
+    Pre p;
+    p.u1 = en ? r.x & 0xFFFF : 0u;
+    p.c1 = en ? r.x >> 16 : 1u;
+    p.r1 = rcp64(en ? r.y & 0xFFFF : 1u);
+    p.v = (r.y >> 16) & 255;
+    p.e2 = en && ((r.w >> 16) & 1u);
+    p.e0 = en && ((r.w >> 17) & 1u);
+    p.u2 = p.e2 ? r.z & 0xFFFF : 0u;
+    p.c2 = p.e2 ? r.z >> 16 : 1u;
+    p.r2 = rcp64(p.e2 ? r.w & 0xFFFF : 1u);
+    return p;
+}
+
+// code_step with the next position's wide record
+DEV void wcode_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, const uint8_t* itab, Pre& p,
+                    const uint4& nx, bool enn, uintptr_t dummy)
+{
+    const uint32_t n0 = o.n;
+    uint32_t under0, cnt0;
+    root3_lookup(root, mtab, p.v, under0, cnt0);
+    const RootAddPre ra = root3_add_read(root, itab, p.v);
+    const Pre q = prep_wide(nx, enn);
+    const uint32_t rtot1 = p.e0 ? ((k.rtot + kRootDelta) & 0xFFFF) : k.rtot;
+    double rrt1 = rcp64(rtot1);
+    code(k.low, k.range, p.u1, p.c1, p.r1, o);
+    if (any_lane(p.e2)) code(k.low, k.range, p.u2, p.c2, p.r2, o);
+    code(k.low, k.range, p.e0 ? 1 + under0 : 0u, p.e0 ? 1 + cnt0 : 1u, p.e0 ? k.rrt : 1.0, o);
+    if (p.e0) root3_add_write(root, p.v, cnt0, ra);
+    k.rtot = rtot1;
+    const bool rs0 = p.e0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
+    if (any_lane(rs0)) {
+        if (rs0) { Root R; k.rtot = root3_rescale<true>(root, R); }
+        rrt1 = rcp64(k.rtot);
+    }
+    k.rrt = rrt1;
+    ring_store(o);
+    ring_chunk(o, n0, dummy);
+    p = q;
+}
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void rc_enc2_wcode(rc_batch_dev b, E2Params e)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint8_t* mtab = smem + kCodeMtab;
+    const uint8_t* itab = smem + kCodeItab;
+    if (threadIdx.x < 16) root3_mask_init(smem + kCodeMtab, threadIdx.x);
+    if (threadIdx.x < 16) root3_inc_init(smem + kCodeItab, threadIdx.x);
+    __syncthreads();
+    const uint32_t nw = min(*e.wcount, e.wcap);
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x * 256 >= nw) return;               // (wave-uniform for whole blocks)
+    const bool live = q < nw;
+    const uint32_t pkt = live ? packet_of(e, e.wlist[q]) : 0u;
+    const uint32_t len = live ? b.in_len[pkt] : 0u;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(e.wide) + static_cast<size_t>(live ? q : 0u) * e.wslot_bytes;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(e.dummy) + ((blockIdx.x * 256u + threadIdx.x) & 65535u) * 16u;
+    uint8_t* root = smem + threadIdx.x * kCodeLds;
+    Ring o;
+    o.r = root + kRingAt;
+    o.lo = reinterpret_cast<uintptr_t>(b.out + (live ? b.out_off[pkt] : 0));
+    o.n = 0;
+    o.cap = live ? b.out_cap[pkt] : 0u;
+    o.ch = make_uint4(0u, 0u, 0u, 0u);
+    o.ca = dummy;
+    CodeState k;
+    {
+        Root R;
+        root3_clear<true>(root, R);
+    }
+    k.rtot = 1 + 256; k.low = 0; k.range = ~0u;
+    k.rrt = rcp64(k.rtot);
+    // one 16-B record per position; four registers, each reloaded (four
+    // positions ahead) right after its position is prepared
+    uint4 c0 = gload16(base), c1 = gload16(base + 16), c2 = gload16(base + 32), c3 = gload16(base + 48);
+    __builtin_amdgcn_s_waitcnt(0);
+    Pre p = prep_wide(c0, 0 < len);
+    c0 = gload16(base + 64);
+    uintptr_t a = base + 80;
+    for (uint32_t i = 0; any_lane(i < len && o.n <= o.cap); i += 4, a += 64) {
+        wcode_step(k, o, root, mtab, itab, p, c1, i + 1 < len, dummy);
+        c1 = gload16(a);
+        wcode_step(k, o, root, mtab, itab, p, c2, i + 2 < len, dummy);
+        c2 = gload16(a + 16);
+        wcode_step(k, o, root, mtab, itab, p, c3, i + 3 < len, dummy);
+        c3 = gload16(a + 32);
+        wcode_step(k, o, root, mtab, itab, p, c0, i + 4 < len, dummy);
+        c0 = gload16(a + 48);
+    }
+    ring_store(o);
+    ring_chunk(o, o.n, dummy);
+    bool ok = live && o.n <= o.cap;
+    uint32_t low = k.low;
+    while (any_lane(ok && low != 0)) {
+        const bool more = ok && low != 0;
+        const bool full = more && o.n >= o.cap;
+        ok = ok && !full;
+        const uint32_t n0 = o.n;
+        ring_put(o, low, 1, more && !full);
+        low = (more && !full) ? low << 8 : low;
+        ring_chunk(o, n0, dummy);
+        ring_store(o);
+    }
+    ring_finish(o, ok);
+    if (live) b.out_len[pkt] = ok ? o.n : 0u;
+}
+
 }  // namespace
 
 #ifdef E2_PROF
 extern "C" int rc_enc2_prof_read(unsigned long long* out, int reset)
 {
     hipError_t err = hipDeviceSynchronize();
-    if (err == hipSuccess) err = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_e2prof), sizeof(unsigned long long) * 16);
+    if (err == hipSuccess) err = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_e2prof), sizeof(unsigned long long) * 32);
     if (err == hipSuccess && reset) {
-        static const unsigned long long zero[16] = {0};
+        static const unsigned long long zero[32] = {0};
         err = hipMemcpyToSymbol(HIP_SYMBOL(g_e2prof), zero, sizeof zero);
     }
     return static_cast<int>(err);
@@ -1170,8 +1915,17 @@ extern "C" uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len)
     return ((8 * l + 15) & ~15ull) + 96;              // 8 B per position, + the chunks read ahead
 }
 
+// bytes of one wide-mode slot (16-B records, rc_enc2_wcode reads 4 ahead)
+extern "C" uint64_t rc_hip_enc2_wide_slot_bytes(uint32_t max_len)
+{
+    const uint64_t l = max_len < kE2MaxLen ? max_len : kE2MaxLen;
+    return 16 * l + 256;
+}
+
 // Both passes over the batch, in chunks that fit the record stream; packets
 // off the fast path end up in ws->enc2_list / counters[3] for the lane kernels.
+// Per chunk: rc_enc2_scan, rc_enc2_code2 (narrow packets), then the wide
+// kernels over the packets the scan listed for them (counters[4]).
 extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1192,6 +1946,12 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     e.bins = ws->bins;
     e.list = ws->enc2_list;
     e.count = ws->counters + 3;
+    e.wslot_bytes = rc_hip_enc2_wide_slot_bytes(ml);
+    e.wide = ws->enc2_wide && ws->enc2_wide_cap >= e.wslot_bytes ? static_cast<uint8_t*>(ws->enc2_wide) : nullptr;
+    e.wlist = ws->enc2_wlist;
+    e.wcount = ws->counters + 4;
+    const uint64_t wcap = e.wide ? ws->enc2_wide_cap / e.wslot_bytes : 0;
+    e.wcap = static_cast<uint32_t>(wcap < 0xFFFFFFFFull ? wcap : 0xFFFFFFFFull);
     const uint32_t scan_blocks_max = ws->cus * 16;
     static const char* lanes = getenv("ENET_RC_ENC2_LANES");      // experiment: 32 packets per wavefront
     e.act = (lanes && atoi(lanes) == 32) ? 32u : 64u;
@@ -1201,6 +1961,10 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         e.lo = static_cast<uint32_t>(lo);
         e.hi = static_cast<uint32_t>(hi);
         const uint32_t cnt = static_cast<uint32_t>(hi - lo);
+        if (lo > 0 && e.wide) {                        // (the batch's memset cleared it for the first chunk)
+            const hipError_t err = hipMemsetAsync(e.wcount, 0, sizeof(uint32_t), st);
+            if (err != hipSuccess) return static_cast<int>(err);
+        }
         hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
                            0, st, *b, e);
         static const char* one = getenv("ENET_RC_ENC2_CODE1");        // the one-wavefront code pass (A/B)
@@ -1209,6 +1973,11 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
                                *b, e);
         else
             hipLaunchKernelGGL(rc_enc2_code2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
+        if (e.wide) {
+            hipLaunchKernelGGL(rc_enc2_wscan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
+                               0, st, *b, e);
+            hipLaunchKernelGGL(rc_enc2_wcode, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
+        }
     }
     return static_cast<int>(hipGetLastError());
 }

@@ -46,6 +46,9 @@ typedef struct {
     uint32_t last_exact;
     uint32_t max_slots;             /* lanes with a model region (ENET_RC_SLOTS) */
     int enc2_on;                    /* compress batches on the two-pass encoder (ENET_RC_ENC2=0: off) */
+    int enc2_wide_on;               /* ... and its wide mode (ENET_RC_ENC2_WIDE=0: off) */
+    uint64_t enc2_stream_max;       /* record-stream caps, read when the context is created */
+    uint64_t enc2_wide_max;
     uint32_t *crc_tables;           /* device: slice-by-16 + shift tables (rc_crc32.hip) */
     /* datagram framing workspace (rc_dgram.hip): per-datagram arrays + checksum scratch */
     uint8_t *dg_arrays;
@@ -67,19 +70,24 @@ static int ws_reserve(rc_ctx *c, size_t n)
     if (n <= c->ws.n_cap) return 0;
     size_t cap = c->ws.n_cap ? c->ws.n_cap : 1024;
     while (cap < n) cap *= 2;
-    uint32_t *fl = NULL, *ord = NULL, *el = NULL;
+    uint32_t *fl = NULL, *ord = NULL, *el = NULL, *wl = NULL;
     if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) return -1;
     if (hipMalloc((void **) &ord, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(fl); return -1; }
     if (hipMalloc((void **) &el, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(fl); hipFree(ord); return -1; }
+    if (hipMalloc((void **) &wl, cap * sizeof(uint32_t)) != hipSuccess) {
+        hipFree(fl); hipFree(ord); hipFree(el); return -1;
+    }
     if (c->ws.flag_list) {
         hipDeviceSynchronize();
         hipFree(c->ws.flag_list);
         hipFree(c->ws.order);
         hipFree(c->ws.enc2_list);
+        hipFree(c->ws.enc2_wlist);
     }
     c->ws.flag_list = fl;
     c->ws.order = ord;
     c->ws.enc2_list = el;
+    c->ws.enc2_wlist = wl;
     c->ws.n_cap = (uint32_t) cap;
     return 0;
 }
@@ -116,26 +124,51 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 
 /* Record stream of the two-pass encoder (rc_enc2.hip): one slot per packet,
  * at most ENC2_STREAM_MAX bytes (larger batches run in whole code-pass rounds
- * of chunks; ENET_RC_ENC2_STREAM_MB=m caps it lower).  Reserved only for
- * batches that take the lane path (run_device). */
+ * of chunks; ENET_RC_ENC2_STREAM_MB=m caps it lower).  Its wide mode has a
+ * stream of 16-B records for as many packets as a chunk holds (at most
+ * ENC2_WIDE_MAX bytes, ENET_RC_ENC2_WIDE_MB=m caps it lower: packets past it
+ * take the lane kernels; ENET_RC_ENC2_WIDE=0 turns the mode off).  Reserved
+ * only for batches that take the lane path (run_device). */
 #define ENC2_STREAM_MAX (1ull << 30)
+#define ENC2_WIDE_MAX (3ull << 30)
+
+static uint64_t env_mb_cap(const char *name, uint64_t cap)
+{
+    const char *mb = getenv(name);
+    if (mb && atol(mb) > 0 && (uint64_t) atol(mb) << 20 < cap) cap = (uint64_t) atol(mb) << 20;
+    return cap;
+}
 
 static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
 {
     if (!c->enc2_on || c->ws.kernel != RC_KERNEL_LANE3) return 0;
-    const uint64_t slot = rc_hip_enc2_slot_bytes(max_len ? max_len : 4096);
-    uint64_t cap = ENC2_STREAM_MAX;
-    const char *mb = getenv("ENET_RC_ENC2_STREAM_MB");
-    if (mb && atol(mb) > 0 && (uint64_t) atol(mb) << 20 < cap) cap = (uint64_t) atol(mb) << 20;
+    const uint32_t ml = max_len ? max_len : 4096;
+    const uint64_t slot = rc_hip_enc2_slot_bytes(ml);
+    const uint64_t cap = c->enc2_stream_max;
     uint64_t want = (uint64_t) n * slot;
     if (want > cap) want = cap > slot ? cap : slot;
-    if (want <= c->ws.enc2_cap) return 0;
-    hipDeviceSynchronize();
-    if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
-    c->ws.enc2_stream = NULL; c->ws.enc2_cap = 0;
-    /* + 1 MB past the stream: the code pass's dummy store targets (rc_enc2.hip) */
-    if (hipMalloc(&c->ws.enc2_stream, want + (1u << 20)) != hipSuccess) return -1;
-    c->ws.enc2_cap = want;
+    if (want > c->ws.enc2_cap) {
+        hipDeviceSynchronize();
+        if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
+        c->ws.enc2_stream = NULL; c->ws.enc2_cap = 0;
+        /* + 1 MB past the stream: the code pass's dummy store targets (rc_enc2.hip) */
+        if (hipMalloc(&c->ws.enc2_stream, want + (1u << 20)) != hipSuccess) return -1;
+        c->ws.enc2_cap = want;
+    }
+    if (c->enc2_wide_on) {
+        /* a slot per packet of a chunk */
+        const uint64_t wslot = rc_hip_enc2_wide_slot_bytes(ml);
+        uint64_t wwant = (want / slot) * wslot;
+        const uint64_t wcap = c->enc2_wide_max;
+        if (wwant > wcap) wwant = wcap > wslot ? wcap : wslot;
+        if (wwant > c->ws.enc2_wide_cap) {
+            hipDeviceSynchronize();
+            if (c->ws.enc2_wide) hipFree(c->ws.enc2_wide);
+            c->ws.enc2_wide = NULL; c->ws.enc2_wide_cap = 0;
+            if (hipMalloc(&c->ws.enc2_wide, wwant) != hipSuccess) return -1;
+            c->ws.enc2_wide_cap = wwant;
+        }
+    }
     return 0;
 }
 
@@ -163,7 +196,7 @@ void *enet_range_coder_create(void)
     memset(c, 0, sizeof *c);
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) goto fail;
-    if (hipMalloc((void **) &c->ws.counters, 16) != hipSuccess) goto fail;
+    if (hipMalloc((void **) &c->ws.counters, 32) != hipSuccess) goto fail;
     if (hipMalloc((void **) &c->ws.bins, (RC_LEN_BINS + 1) * sizeof(uint32_t)) != hipSuccess) goto fail;
     c->ws.exact_slots = EXACT_SLOTS;
     if (hipMalloc(&c->ws.exact_pool, (size_t) EXACT_SLOTS * RC_EXACT_POOL_BYTES) != hipSuccess) goto fail;
@@ -195,6 +228,10 @@ void *enet_range_coder_create(void)
         c->ws.cus = (uint32_t) cus;
         const char *e2 = getenv("ENET_RC_ENC2");
         c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
+        const char *ew = getenv("ENET_RC_ENC2_WIDE");
+        c->enc2_wide_on = !(ew && strcmp(ew, "0") == 0);
+        c->enc2_stream_max = env_mb_cap("ENET_RC_ENC2_STREAM_MB", ENC2_STREAM_MAX);
+        c->enc2_wide_max = env_mb_cap("ENET_RC_ENC2_WIDE_MB", ENC2_WIDE_MAX);
         const char *d4 = getenv("ENET_RC_DEC4");
         c->ws.dec4 = !(d4 && strcmp(d4, "0") == 0);
         const char *es = getenv("ENET_RC_ENC2_SLOW");
@@ -220,6 +257,8 @@ void enet_range_coder_destroy(void *context)
     if (c->ws.order) hipFree(c->ws.order);
     if (c->ws.enc2_list) hipFree(c->ws.enc2_list);
     if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
+    if (c->ws.enc2_wlist) hipFree(c->ws.enc2_wlist);
+    if (c->ws.enc2_wide) hipFree(c->ws.enc2_wide);
     if (c->ws.bins) hipFree(c->ws.bins);
     if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);

@@ -145,7 +145,7 @@ def _digest_roundtrip(coder, name, batch, lanes=None):
     coder.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=int(l.max()))
     torch.cuda.synchronize()
     routed = getattr(coder, "variant", "") == "lane3" and lanes is not None
-    if routed:
+    if routed and lanes[0] is not None:
         assert coder.last_lane_count() == lanes[0], "encoder fast path hand-off"
         assert coder.last_exact_count() == 0
     cl = clen.cpu().numpy().astype(np.uint32)
@@ -156,7 +156,7 @@ def _digest_roundtrip(coder, name, batch, lanes=None):
     dl = torch.zeros(n, dtype=torch.int32, device="cuda")
     coder.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
     torch.cuda.synchronize()
-    if routed:
+    if routed and lanes[1] is not None:
         assert coder.last_lane_count() == lanes[1], "decoder fast path hand-off"
         assert coder.last_exact_count() == 0
     assert torch.equal(dl, dlen)
@@ -173,7 +173,9 @@ def test_c2_digest_full_size(coder):
 
 
 def test_c3_digest_full_size(coder):
-    _digest_roundtrip(coder, "C3_gamestate_65536x1200", synth.gamestate_batch(65536, 1200))
+    # game state: every packet on the encoder's wide mode; the decoder hands
+    # them all to the lane kernels (buckets over its capacity)
+    _digest_roundtrip(coder, "C3_gamestate_65536x1200", synth.gamestate_batch(65536, 1200), lanes=(0, 65536))
 
 
 def test_c4_mixed_sizes_vs_oracle(coder):

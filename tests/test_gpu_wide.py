@@ -1,0 +1,151 @@
+"""The two-pass encoder's wide mode on the GPU (rc_enc2_wscan / rc_enc2_wcode,
+rc_enc2.hip): packets with a bucket over 64 positions, whose sub-contexts
+rescale (compress.c:90-112, :313-314).  Bit-exact against the oracle, through
+the C ABI, on batches large enough for the lane path (small batches run on the
+wave kernel).  The model the kernels follow is tests/proto/twopass.py
+(scan_wide), checked on the CPU in tests/test_twopass_model.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from enet_amd import synth
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _coder(**env):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from enet_amd import RangeCoder
+    env = {"ENET_RC_KERNEL": "lane3", "ENET_RC_SMALL_BATCH": "0", **env}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return RangeCoder()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _wide_packets(n, seed):
+    """Low-entropy packets of every shape the wide path has to get right:
+    single-byte runs (one context, rescales every 127 visits), alternations,
+    small alphabets, mostly-zero with random bytes, game state, lengths up to
+    1919 B (the longest without a model reset)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = i % 7
+        ln = int(rng.integers(66, 1920))
+        if k == 0:
+            p = np.full(ln, rng.integers(0, 256), np.uint8)
+        elif k == 1:
+            per = int(rng.integers(2, 5))
+            p = np.resize(rng.integers(0, 256, per).astype(np.uint8), ln)
+        elif k == 2:
+            alpha = rng.integers(0, 256, int(rng.integers(2, 9))).astype(np.uint8)
+            p = alpha[rng.integers(0, len(alpha), ln)]
+        elif k == 3:
+            p = np.where(rng.random(ln) < rng.uniform(0.5, 0.95), 0, rng.integers(0, 256, ln)).astype(np.uint8)
+        elif k == 4:
+            # a long run, then random bytes (dense walks, then small buckets)
+            cut = int(rng.integers(1, ln))
+            p = np.concatenate([np.zeros(cut, np.uint8), rng.integers(0, 256, ln - cut).astype(np.uint8)])
+        elif k == 5:
+            # two interleaved heavy contexts in one bucket: (0, 0) and (5, 0)
+            p = np.resize(np.array([0, 0, 5, 0], np.uint8), ln)
+            flip = rng.random(ln) < 0.05
+            p[flip] = rng.integers(0, 256, int(flip.sum()))
+        else:
+            # skewed symbols inside one heavy context: many distinct values per round
+            p = np.where(np.arange(ln) % 2 == 0, 0, rng.geometric(0.05, ln) % 256).astype(np.uint8)
+        out.append(p.tobytes())
+    return out
+
+
+def _check(coder, packets, cap_fn):
+    from oracle.pyoracle import compress_batch as ocompress
+    d, o, l = synth.pack(packets)
+    ref, roff, cap, rlen = ocompress(d, o, l, "port", cap_fn=cap_fn)
+    n = len(l)
+    din = torch.from_numpy(d).cuda()
+    doff = torch.from_numpy(o.astype(np.int64)).cuda()
+    dlen = torch.from_numpy(l.astype(np.int32)).cuda()
+    coff = torch.from_numpy(roff.astype(np.int64)).cuda()
+    ccap = torch.from_numpy(cap.astype(np.int32)).cuda()
+    cout = torch.zeros(int(cap.sum()) + 1, dtype=torch.uint8, device="cuda")
+    clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    coder.compress_batch(din, doff, dlen, cout, coff, ccap, clen, max_len=int(l.max()))
+    torch.cuda.synchronize()
+    gl = clen.cpu().numpy().astype(np.uint32)
+    bad = np.nonzero(gl != rlen)[0]
+    assert bad.size == 0, [(int(i), int(l[i]), int(gl[i]), int(rlen[i])) for i in bad[:8]]
+    go = cout.cpu().numpy()
+    for i in range(n):
+        a, b = int(roff[i]), int(roff[i]) + int(rlen[i])
+        assert np.array_equal(go[a:b], ref[a:b]), (i, int(l[i]))
+
+
+def test_wide_packets_vs_oracle():
+    c = _coder()
+    pk = _wide_packets(3000, 11)
+    _check(c, pk, lambda n: 2 * n + 64)
+    assert c.last_lane_count() == 0                   # every packet on the wide path
+    _check(c, pk, lambda n: n)                        # protocol mode: outLimit = N (overflows included)
+    c.close()
+
+
+def test_wide_gamestate_and_random_mixed():
+    c = _coder()
+    d, o, l = synth.gamestate_batch(2048, 1200)
+    pk = [d[int(o[i]): int(o[i]) + 1200].tobytes() for i in range(2048)]
+    rng = np.random.default_rng(3)
+    pk += [rng.integers(0, 256, int(rng.integers(1, 1920)), dtype=np.uint8).tobytes() for _ in range(1024)]
+    rng.shuffle(pk)
+    _check(c, pk, lambda n: 2 * n + 64)
+    assert c.last_lane_count() == 0
+    c.close()
+
+
+def test_wide_slow_path_full_peeling():
+    """ENET_RC_ENC2_SLOW=1: no reliance on lane-ordered LDS atomics (every
+    key peeled with ballots)."""
+    c = _coder(ENET_RC_ENC2_SLOW="1")
+    _check(c, _wide_packets(1500, 12), lambda n: 2 * n + 64)
+    c.close()
+
+
+def test_wide_stream_overflow_goes_to_lanes():
+    """A wide stream for only a few packets (ENET_RC_ENC2_WIDE_MB=1): the rest
+    of the listed packets take the lane kernels, still bit-exact."""
+    c = _coder(ENET_RC_ENC2_WIDE_MB="1")
+    d, o, l = synth.gamestate_batch(3000, 1200)
+    pk = [d[int(o[i]): int(o[i]) + 1200].tobytes() for i in range(3000)]
+    _check(c, pk, lambda n: 2 * n + 64)
+    assert 0 < c.last_lane_count() < 3000
+    c.close()
+
+
+def test_wide_across_stream_chunks():
+    """Record-stream chunks (ENET_RC_ENC2_STREAM_MB=8): the wide list is per
+    chunk."""
+    c = _coder(ENET_RC_ENC2_STREAM_MB="8")
+    pk = _wide_packets(2500, 13)
+    _check(c, pk, lambda n: 2 * n + 64)
+    assert c.last_lane_count() == 0
+    c.close()
+
+
+def test_wide_off_takes_lanes():
+    c = _coder(ENET_RC_ENC2_WIDE="0")
+    d, o, l = synth.gamestate_batch(2048, 1200)
+    pk = [d[int(o[i]): int(o[i]) + 1200].tobytes() for i in range(2048)]
+    _check(c, pk, lambda n: 2 * n + 64)
+    assert c.last_lane_count() == 2048
+    c.close()

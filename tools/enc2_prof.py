@@ -19,7 +19,7 @@ d, o, l = (synth.gamestate_batch if len(sys.argv) > 2 and sys.argv[2] == "c3" el
 din = torch.from_numpy(d).cuda()
 doff = torch.from_numpy(o.astype("int64")).cuda()
 dlen = torch.from_numpy(l.astype("int32")).cuda()
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 32)()
 with RangeCoder() as rc:
     compress_batch(rc, din, doff, dlen, max_len=1200)
     torch.cuda.synchronize()
@@ -44,3 +44,12 @@ print(f"code {'total':22s} {ctot / steps:8.0f} cycles/wave-step")
 parts = (n // 64) * 1200 / 4
 print(f"code2 helper work {buf[8] / parts:7.0f}  barrier wait {buf[9] / parts:7.0f} cycles/wave-part")
 print(f"code2 coder  work {buf[10] / parts:7.0f}  barrier wait {buf[11] / parts:7.0f} cycles/wave-part")
+
+# the wide scan (rc_enc2_wscan): cycles per packet it took
+wnames = ["load+zero", "bucket sizes", "starts+pad", "scatter", "small buckets", "big: sort",
+          "big: short runs", "big: dense o2", "big: o1 list", "big: dense o1", "end", "-"]
+wtot = sum(buf[16 + k] for k in range(12))
+if wtot:
+    for k, nm in enumerate(wnames):
+        print(f"wide {nm:16s} {buf[16 + k] / n:10.0f} cycles/packet  {100.0 * buf[16 + k] / wtot:5.1f} %")
+    print(f"wide {'total':16s} {wtot / n:10.0f} cycles/packet")
