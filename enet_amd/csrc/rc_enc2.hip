@@ -1294,6 +1294,29 @@ DEV uint64_t match8(uint32_t key, uint64_t act, uint32_t& lt)
     return e;
 }
 
+// match8 against ballots taken once (B[b] = lanes with key bit b set):
+// several matches on the same key share them
+struct KeyBits { uint64_t b[8]; };
+DEV KeyBits key_bits(uint32_t key)
+{
+    KeyBits k;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) k.b[b] = __builtin_amdgcn_ballot_w64((key >> b) & 1u);
+    return k;
+}
+DEV uint64_t match_bits(uint32_t key, const KeyBits& kb, uint64_t e, uint32_t& lt)
+{
+    const uint64_t below = below_mask();
+    lt = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const bool one = (key >> b) & 1u;
+        lt += one ? popc64(e & ~kb.b[b] & below) : 0u;
+        e &= one ? kb.b[b] : ~kb.b[b];
+    }
+    return e;
+}
+
 // cnt[key] += 1 for every lane with ok: one LDS atomic per distinct key (its
 // lowest lane adds the group's size).  RET: returns the lane's slot, the old
 // value plus its rank among the lanes with its key (lane order).
@@ -1331,118 +1354,117 @@ DEV uint2 closed_code(uint32_t t, uint32_t dist, uint32_t same, uint32_t less)
 
 DEV uint32_t akey_of(uint32_t w) { return (w & (256u << 19)) ? (w >> 19) & 511 : 1024u; }   // 1024: none (position 1)
 
-// Buckets of <= kE2Bucket elements, element-parallel (a lane per element,
-// over its bucket predecessors, eight per two LDS reads), in three passes over
-// the list of their elements (s.sw: element index | bucket start << 16):
-// (0) found at order 2 (an earlier element of the bucket with the same a and
-// v); (1) the order-2 statistics -> record half A, and found at order 1 (an
-// earlier order-1 visitor with the same v); (2) the order-1 statistics of the
-// order-1 visitors -> record half B.  Each pass reads only flags the previous
-// ones wrote.
-template <uint32_t pass>
-DEV void wide_small_pass(WScanLds& s, uint32_t ns, uint2* wrec)
+// Buckets of <= kE2Bucket elements, whole buckets per round: a window of 64
+// element slots starting at a bucket start takes every bucket that ends inside
+// it (the next window starts at the first one that does not; big buckets are
+// skipped).  With a bucket's elements side by side in the lanes, every
+// statistic is a count of lanes (compress.c:159-199, :286-316): with
+// match(key) = the lanes of a set whose key equals this lane's,
+//   order 2: C = match(a) in my bucket, t2 = |C below me|, same2 / less2 from
+//            match(v) in C, found2 = same2 > 0, dist2 = |C below me, not found2|;
+//   order 1 (not found2): the bucket's lanes not found2, likewise.
+// found2 of every lane is known at once (an earlier lane with the same a and
+// v), so nothing runs lane after lane.
+DEV void wide_small_buckets(WScanLds& s, uint32_t q0, uint32_t total, uint2* wrec)
 {
     const uint32_t t = lane_id();
+    const uint64_t below = below_mask();
 #pragma unroll 1
-    for (uint32_t base = 0; base < ns; base += 64) {
-        const uint32_t li = base + t;
-        const uint32_t ent = s.sw[li < ns ? li : ns - 1];
-        const uint32_t ei = ent & 0xFFFF, bs = ent >> 16;
-        const uint32_t w = s.e[ei];
-        const uint32_t v = (w >> 11) & 255, akey = akey_of(w);
-        const bool f2 = (w & kF2) != 0;
-        const bool act = li < ns && !(pass == 2 && f2);
-        const uint32_t nq = act ? ei - bs : 0u;
-        uint32_t acc2 = 0, acc1 = 0;                  // t | same << 8 | less << 16 | dist << 24
-        bool hit = false;
-#pragma unroll 1
-        for (uint32_t q = 0; q < nq; q += 8) {
-            const uint4 ua = *reinterpret_cast<const uint4*>(&s.e[bs + q]);
-            const uint4 ub = *reinterpret_cast<const uint4*>(&s.e[bs + q + 4]);
-#pragma unroll
-            for (uint32_t c = 0; c < 8; ++c) {
-                const uint32_t u = pick4(c & 3, c < 4 ? ua : ub);
-                const bool in = q + c < nq;
-                const uint32_t uv = (u >> 11) & 255;
-                const uint32_t one = 1u | (uv == v ? 0x100u : 0u) | (uv < v ? 0x10000u : 0u);
-                if constexpr (pass == 0) {
-                    hit = hit || (in && ((u >> 19) & 511) == akey && uv == v);
-                } else if constexpr (pass == 1) {
-                    const bool m2 = in && ((u >> 19) & 511) == akey;
-                    acc2 += m2 ? (one | ((u & kF2) ? 0u : 0x1000000u)) : 0u;
-                    hit = hit || (in && !f2 && (u & kF2) == 0 && uv == v);
+    for (uint32_t W = 0; W < total;) {
+        const uint32_t ei = W + t;
+        const uint32_t w = ei < total ? s.e[ei] : kPadWord;
+        const bool pad = w == kPadWord;
+        uint32_t bs = 0, be = 0, p = 0;
+        if (!pad) {
+            p = s.x[q0 + (w & 2047) - 1];
+            bs = s.start[p];
+            be = s.cnt[p];
+        }
+        const bool small = !pad && be - bs <= kE2Bucket;
+        const bool act = small && be <= W + 64;
+        // the next window: the first lane not taken (a big bucket: past its end)
+        const uint64_t nt = __builtin_amdgcn_ballot_w64(!pad && !act);
+        uint32_t nextW = W + 64;
+        if (nt) {
+            const uint32_t ld = static_cast<uint32_t>(__builtin_ctzll(nt));
+            const uint32_t lbs = __builtin_amdgcn_readlane(bs, ld), lbe = __builtin_amdgcn_readlane(be, ld);
+            const uint32_t lsm = __builtin_amdgcn_readlane(small ? 1u : 0u, ld);
+            nextW = lsm ? lbs : (lbe + 3) & ~3u;
+            nextW = max(nextW, W + (ld ? 0u : 4u));  // (progress: a first lane never taken is a big bucket's)
+        }
+        const uint64_t am = __builtin_amdgcn_ballot_w64(act);
+        if (am) {
+            const uint32_t v = (w >> 11) & 255, a = (w >> 19) & 255;
+            const bool has = (w & (256u << 19)) != 0;
+            uint32_t lt;
+            const KeyBits kp = key_bits(p), ka = key_bits(a), kv = key_bits(v);
+            const uint64_t mine = act ? match_bits(p, kp, am, lt) : 0ull;          // my bucket
+            const uint64_t hm = __builtin_amdgcn_ballot_w64(has);
+            const uint64_t ctx2 = has ? match_bits(a, ka, mine & hm, lt) : 0ull;   // my order-2 context
+            uint32_t less2;
+            const uint64_t same2m = match_bits(v, kv, ctx2, less2);
+            const bool f2 = act && (same2m & below) != 0;
+            const uint64_t F2 = __builtin_amdgcn_ballot_w64(f2);
+            const uint32_t t2 = popc64(ctx2 & below), same2 = popc64(same2m & below);
+            const uint32_t dist2 = popc64(ctx2 & below & ~F2);
+            const uint64_t vis1 = mine & ~F2;                                      // the bucket's order-1 visitors
+            uint32_t less1;
+            const uint64_t same1m = match_bits(v, kv, vis1, less1);
+            const bool f1 = act && !f2 && (same1m & below) != 0;
+            const uint64_t F1 = __builtin_amdgcn_ballot_w64(f1);
+            if (act) {
+                const uint32_t pos = w & 2047;
+                const uint2 ca = closed_code(t2, dist2, same2, less2);
+                wrec[2 * pos] = make_uint2(ca.x, ca.y | v << 16);
+                if (f2) {
+                    wrec[2 * pos + 1] = make_uint2(kNoCodeLo, kNoCodeTot);
                 } else {
-                    const bool m1 = in && (u & kF2) == 0;
-                    acc1 += m1 ? (one | ((u & kF1) ? 0u : 0x1000000u)) : 0u;
+                    const uint2 cb = closed_code(popc64(vis1 & below), popc64(vis1 & below & ~F1),
+                                                 popc64(same1m & below), less1);
+                    const bool coded = cb.y != kNoCodeTot || cb.x != kNoCodeLo;
+                    wrec[2 * pos + 1] = make_uint2(cb.x, cb.y | (coded ? 1u << 16 : 0u) | (f1 ? 0u : 1u << 17));
                 }
             }
         }
-        if (!act) continue;
-        const uint32_t pos = w & 2047;
-        if constexpr (pass == 0) {
-            if (hit) s.e[ei] = w | kF2;
-        } else if constexpr (pass == 1) {
-            const uint2 a = closed_code(acc2 & 255, acc2 >> 24, (acc2 >> 8) & 255, (acc2 >> 16) & 255);
-            wrec[2 * pos] = make_uint2(a.x, a.y | v << 16);
-            if (f2) wrec[2 * pos + 1] = make_uint2(kNoCodeLo, kNoCodeTot);
-            else if (hit) s.e[ei] = w | kF1;
-        } else {
-            const uint2 bq = closed_code(acc1 & 255, acc1 >> 24, (acc1 >> 8) & 255, (acc1 >> 16) & 255);
-            const bool coded = bq.y != kNoCodeTot || bq.x != kNoCodeLo;
-            wrec[2 * pos + 1] = make_uint2(bq.x, bq.y | (coded ? 1u << 16 : 0u) | ((w & kF1) ? 0u : 1u << 17));
-        }
+        W = nextW;
     }
 }
 
-// A big bucket's short order-2 runs (<= kWideDense visits: no rescale),
-// element-parallel over their sorted words sw[0, ks) (short runs first):
-// (0) found (an earlier element of the run with the same v); (1) the
-// statistics -> record half A, and the position's order-2 hit bit.
-template <uint32_t pass>
-DEV void wide_run_pass(WScanLds& s, uint32_t ks, const uint32_t* hist, const uint32_t* rend, uint2* wrec)
+// A big bucket's short order-2 runs (<= kWideDense visits: no rescale) in
+// windows of whole runs over their sorted words sw[0, ks) (short runs first),
+// counted over lanes as in wide_small_buckets: record half A, and the
+// position's order-2 hit bit.
+DEV void wide_short_runs(WScanLds& s, uint32_t ks, const uint32_t* hist, const uint32_t* rend, uint2* wrec)
 {
     const uint32_t t = lane_id();
+    const uint64_t below = below_mask();
 #pragma unroll 1
-    for (uint32_t base = 0; base < ks; base += 64) {
-        const uint32_t j = base + t;
-        const bool act = j < ks;
-        const uint32_t w = s.sw[act ? j : ks - 1];
-        const uint32_t a = (w >> 19) & 255;
-        const uint32_t rs = rend[a] - hist[a];
-        const uint32_t v = (w >> 11) & 255;
-        const uint32_t q0 = rs & ~3u;
-        const uint32_t nq = act ? j - q0 : 0u;
-        uint32_t acc = 0;
-        bool hit = false;
-#pragma unroll 1
-        for (uint32_t q = 0; q < nq; q += 8) {
-            const uint4 ua = *reinterpret_cast<const uint4*>(&s.sw[q0 + q]);
-            const uint4 ub = *reinterpret_cast<const uint4*>(&s.sw[q0 + q + 4]);
-#pragma unroll
-            for (uint32_t c = 0; c < 8; ++c) {
-                const uint32_t u = pick4(c & 3, c < 4 ? ua : ub);
-                const bool in = q + c < nq && q0 + q + c >= rs;
-                const uint32_t uv = (u >> 11) & 255;
-                if constexpr (pass == 0) {
-                    hit = hit || (in && uv == v);
-                } else {
-                    const uint32_t one = 1u | (uv == v ? 0x100u : 0u) | (uv < v ? 0x10000u : 0u);
-                    acc += in ? (one | ((u & kF2) ? 0u : 0x1000000u)) : 0u;
-                }
-            }
-        }
-        if (!act) continue;
-        const uint32_t pos = w & 2047;
-        if constexpr (pass == 0) {
-            if (hit) s.sw[j] = w | kF2;
-        } else {
-            const uint2 c = closed_code(acc & 255, acc >> 24, (acc >> 8) & 255, (acc >> 16) & 255);
+    for (uint32_t W = 0; W < ks;) {
+        const uint32_t j = W + t;
+        const bool in = j < ks;
+        const uint32_t w = s.sw[in ? j : ks - 1];
+        const uint32_t a = (w >> 19) & 255, v = (w >> 11) & 255;
+        const uint32_t re = rend[a], rs = re - hist[a];
+        const bool act = in && re <= W + 64;
+        const uint64_t nt = __builtin_amdgcn_ballot_w64(in && !act);
+        const uint32_t nextW = nt ? __builtin_amdgcn_readlane(rs, static_cast<uint32_t>(__builtin_ctzll(nt))) : W + 64;
+        const uint64_t am = __builtin_amdgcn_ballot_w64(act);
+        uint32_t lt, less;
+        const KeyBits ka = key_bits(a), kv = key_bits(v);
+        const uint64_t ctx = act ? match_bits(a, ka, am, lt) : 0ull;
+        const uint64_t samem = match_bits(v, kv, ctx, less);
+        const bool f2 = act && (samem & below) != 0;
+        const uint64_t F2 = __builtin_amdgcn_ballot_w64(f2);
+        if (act) {
+            const uint32_t pos = w & 2047;
+            const uint2 c = closed_code(popc64(ctx & below), popc64(ctx & below & ~F2), popc64(samem & below), less);
             wrec[2 * pos] = make_uint2(c.x, c.y | v << 16);
-            if (w & kF2) {
+            if (f2) {
                 wrec[2 * pos + 1] = make_uint2(kNoCodeLo, kNoCodeTot);
                 atomicOr(&s.f2bits[pos >> 5], 1u << (pos & 31));
             }
         }
+        W = nextW;
     }
 }
 
@@ -1593,9 +1615,7 @@ DEV void wide_big_bucket(WScanLds& s, uint32_t bs, uint32_t k, uint2* wrec, W2Pr
     wave_sync();
     W2P(5)
     // short runs: the closed form, element-parallel; long runs: dense walks
-    wide_run_pass<0>(s, ks, hist, rst, wrec);
-    wave_sync();
-    wide_run_pass<1>(s, ks, hist, rst, wrec);
+    wide_short_runs(s, ks, hist, rst, wrec);
 #pragma unroll 1
     for (uint32_t r = 0; r < 4; ++r) {
         const uint32_t a = 4 * t + r;
@@ -1707,55 +1727,9 @@ void rc_enc2_wscan(rc_batch_dev b, E2Params e)
         const uint32_t x0 = s.x[q0];
         wave_sync();
         W2P(3)
-        // buckets of <= kE2Bucket elements, element-parallel over the list of
-        // their elements (in s.sw: element index | bucket start << 16),
-        // ordered by rank in the bucket, highest first: a lane's work is its
-        // rank, and a round costs its longest lane
-        uint32_t* rfill = reinterpret_cast<uint32_t*>(s.tab);        // [64] rank counts, then fill pointers
-        s.tab[t] = 0;
+        // buckets of <= kE2Bucket elements, whole buckets per round
+        wide_small_buckets(s, q0, total, wrec);
         wave_sync();
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-            const uint32_t kk = pick4(r, c4);
-            if (kk && kk <= kE2Bucket) {
-                atomicAdd(&rfill[0], 1u);                             // ranks 0 .. kk - 1: a range add
-                if (kk < 64) atomicSub(&rfill[kk], 1u);
-            }
-        }
-        wave_sync();
-        uint32_t ns;
-        {
-            const uint32_t cr = wave_incl_scan(s.tab[t]);             // elements of rank t
-            const uint32_t above = wave_incl_scan(__shfl(cr, static_cast<int>(63 - t), 64));   // ranks > 63 - t, incl.
-            ns = __builtin_amdgcn_readlane(above, 63);
-            // rank t starts after every element of a higher rank
-            const uint32_t start_t = __shfl(above - __shfl(cr, static_cast<int>(63 - t), 64), static_cast<int>(63 - t), 64);
-            wave_sync();
-            s.tab[t] = start_t;
-        }
-        wave_sync();
-#pragma unroll 1
-        for (uint32_t base = 0; base < total; base += 64) {
-            const uint32_t ei = base + t;
-            const uint32_t w = ei < total ? s.e[ei] : kPadWord;
-            bool sm = w != kPadWord;
-            uint32_t bs = 0;
-            if (sm) {
-                const uint32_t p = s.x[q0 + (w & 2047) - 1];
-                bs = s.start[p];
-                sm = s.cnt[p] - bs <= kE2Bucket;
-            }
-            if (sm) s.sw[atomicAdd(&rfill[ei - bs], 1u)] = ei | bs << 16;
-        }
-        wave_sync();
-        if (ns) {
-            wide_small_pass<0>(s, ns, wrec);
-            wave_sync();
-            wide_small_pass<1>(s, ns, wrec);
-            wave_sync();
-            wide_small_pass<2>(s, ns, wrec);
-            wave_sync();
-        }
         W2P(4)
         // big ones: the wavefront, one at a time
         uint32_t bigm = 0;
