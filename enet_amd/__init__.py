@@ -62,6 +62,37 @@ class RangeCoder:
         r = self.lib.enet_range_coder_compress(self.ctx, arr, len(spans), in_limit, C.addressof(out), out_limit)
         return int(r), out.raw[: r]
 
+    def compress_gather_batch(self, backing: bytes, lists: Sequence[Sequence[tuple]], out_caps: Sequence[int]):
+        """Batch of gather lists (``enet_rc_compress_gather_batch_host``):
+        packet i is the spans ``lists[i]`` = [(start, length)] into
+        ``backing``, consumed like ``compress_gather``.  Returns a list of
+        ``(return_value, bytes)``."""
+        import numpy as np
+        buf = C.create_string_buffer(bytes(backing) + b"\0" * 8)
+        base = C.addressof(buf)
+        nb = sum(len(l) for l in lists)
+        arr = (ENetBuffer * max(1, nb))()
+        first = np.zeros(len(lists) + 1, dtype=np.uint64)
+        k = 0
+        for i, spans in enumerate(lists):
+            first[i] = k
+            for s, l in spans:
+                arr[k].data = base + s
+                arr[k].dataLength = l
+                k += 1
+        first[len(lists)] = k
+        caps = np.asarray(out_caps, dtype=np.uint32)
+        offs = np.zeros(len(lists), dtype=np.uint64)
+        if len(lists) > 1:
+            offs[1:] = np.cumsum(caps[:-1], dtype=np.uint64)
+        out = np.zeros(int(caps.sum()) + 1, dtype=np.uint8)
+        olen = np.zeros(len(lists), dtype=np.uint32)
+        rc = self.lib.enet_rc_compress_gather_batch_host(self.ctx, arr, first.ctypes.data, len(lists), out.ctypes.data,
+                                                         offs.ctypes.data, caps.ctypes.data, olen.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"enet_rc_compress_gather_batch_host failed: HIP error {rc}")
+        return [(int(olen[i]), out[int(offs[i]): int(offs[i]) + int(olen[i])].tobytes()) for i in range(len(lists))]
+
     def compress(self, data: bytes, out_limit: Optional[int] = None, in_limit: Optional[int] = None):
         if out_limit is None:
             out_limit = 2 * len(data) + 64

@@ -52,6 +52,8 @@ def _load() -> C.CDLL:
         f = getattr(lib, name)
         f.restype = C.c_int
         f.argtypes = args
+    lib.enet_rc_compress_gather_batch_host.restype = C.c_int
+    lib.enet_rc_compress_gather_batch_host.argtypes = [vp, C.POINTER(ENetBuffer), vp, sz, vp, vp, vp, vp]
     lib.enet_rc_crc32_batch_device.restype = C.c_int
     lib.enet_rc_crc32_batch_device.argtypes = [vp, vp, vp, vp, sz, vp, vp]
     lib.enet_rc_crc32_batch_host.restype = C.c_int

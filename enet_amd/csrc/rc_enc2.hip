@@ -6,7 +6,7 @@
 // byte; this encoder derives it from the packet instead, and keeps only the
 // root context (order 0) and the range coder serial:
 //
-//   pass 1, rc_enc2_scan: one 256-thread workgroup per packet, in LDS.
+//   pass 1, rc_enc2_scan: one wavefront per packet, in LDS.
 //     Positions 1..N-1 are bucketed by their previous byte x[i-1].  Both
 //     sub-contexts of position i -- order 1 = (x[i-1]), order 2 =
 //     (x[i-2], x[i-1]) -- hold only positions of i's bucket, so thread b
@@ -34,8 +34,10 @@
 //
 // Fast path: 1 <= N <= 1919 (no model reset, compress.c:148-157) and no
 // bucket over 64 positions (every statistic <= 63, so no count reaches the
-// rescale threshold, compress.c:313).  Other packets are listed for the lane
-// kernels, which run after the two passes on that list only.
+// rescale threshold, compress.c:313).  Packets with a bigger bucket go to the
+// wide mode (rc_enc2_wscan / rc_enc2_wcode, below: explicit intervals, dense
+// walks with rescales); longer packets are listed for the lane kernels,
+// which run after the passes on that list only.
 //
 // Record of position i: two words (w0, w1)
 //   w0 bits 0-2 type, 3-8 tA, 9-14 dA, 16-27 ext

@@ -331,20 +331,48 @@ int enet_rc_decompress_batch_device_bounded(void *context, const uint8_t *in, co
 /* ---- host-side copies on several threads (the staging memcpy in and the
  * scatter of the packed results out are the largest host costs) */
 typedef struct {
-    int kind;                       /* 0: memcpy range, 1: scatter packets */
+    int kind;                       /* 0: memcpy range, 1: scatter packets, 2: flatten gather lists */
     uint8_t *dst;
     const uint8_t *src;
     size_t bytes;
     const uint64_t *out_off, *poff;
     const uint32_t *len;
     size_t lo, hi;
+    const ENetBuffer *gbuf;         /* kind 2: packet i = gbuf[gfirst[i] .. gfirst[i + 1]) */
+    const size_t *gfirst;
 } copy_job;
+
+/* packet i's gather list flattened the way compress.c:260-285 walks it: the
+ * first buffer as it is (empty: nothing), every later buffer at least its
+ * data[0] (an empty one still yields that byte, the phantom byte) */
+static size_t gather_len(const ENetBuffer *b, size_t k)
+{
+    if (k == 0) return 0;
+    size_t total = b[0].dataLength;
+    for (size_t j = 1; j < k; ++j) total += b[j].dataLength ? b[j].dataLength : 1;
+    return total;
+}
+
+static void gather_copy(uint8_t *dst, const ENetBuffer *b, size_t k)
+{
+    if (k == 0) return;
+    size_t pos = b[0].dataLength;
+    if (pos) memcpy(dst, b[0].data, pos);
+    for (size_t j = 1; j < k; ++j) {
+        const size_t l = b[j].dataLength;
+        if (l) { memcpy(dst + pos, b[j].data, l); pos += l; }
+        else dst[pos++] = *(const uint8_t *) b[j].data;
+    }
+}
 
 static void *copy_worker(void *p)
 {
     copy_job *j = (copy_job *) p;
     if (j->kind == 0) {
         memcpy(j->dst, j->src, j->bytes);
+    } else if (j->kind == 2) {
+        for (size_t i = j->lo; i < j->hi; ++i)
+            gather_copy(j->dst + j->poff[i], j->gbuf + j->gfirst[i], j->gfirst[i + 1] - j->gfirst[i]);
     } else {
         for (size_t i = j->lo; i < j->hi; ++i)
             if (j->len[i]) memcpy(j->dst + j->out_off[i], j->src + j->poff[i], j->len[i]);
@@ -455,6 +483,22 @@ static void par_scatter(uint8_t *out, const uint64_t *out_off, const uint8_t *pa
     par_run(jobs, k);
 }
 
+/* packets [lo, hi) of gather lists flattened into dst + poff[i] */
+static void par_gather(uint8_t *dst, const uint64_t *poff, const ENetBuffer *gbuf, const size_t *gfirst,
+                       size_t lo, size_t hi, uint64_t bytes)
+{
+    int k = bytes >= COPY_MIN_BYTES ? COPY_THREADS : 1;
+    copy_job jobs[COPY_THREADS];
+    const size_t n = hi - lo, per = (n + k - 1) / k;
+    for (int i = 0; i < k; ++i) {
+        jobs[i].kind = 2;
+        jobs[i].dst = dst; jobs[i].poff = poff; jobs[i].gbuf = gbuf; jobs[i].gfirst = gfirst;
+        jobs[i].lo = lo + ((size_t) i * per < n ? (size_t) i * per : n);
+        jobs[i].hi = lo + ((size_t) (i + 1) * per < n ? (size_t) (i + 1) * per : n);
+    }
+    par_run(jobs, k);
+}
+
 static int pack_reserve(rc_ctx *c, size_t bytes, size_t blocks)
 {
     if (bytes > c->d_pack_cap) {
@@ -509,7 +553,8 @@ static double now_ms(void)
 
 static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
                     const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
-                    const uint32_t *out_cap, uint32_t *out_len, int allow_pin)
+                    const uint32_t *out_cap, uint32_t *out_len, int allow_pin,
+                    const ENetBuffer *gbuf, const size_t *gfirst)
 {
     static int prof = -1;
     if (prof < 0) prof = getenv("ENET_RC_HOST_PROFILE") != NULL;
@@ -520,11 +565,13 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     /* the input as it goes to the device: packed back to back (a batch whose
      * packets sit in gapped slots -- the compressed side of a round trip --
      * moves only its bytes); a batch that already is back to back is one range */
-    uint64_t in_bytes = 0, out_bytes = 0, in_lo = in_off[0];
+    /* (gbuf: the input is packet i's gather list gbuf[gfirst[i] .. gfirst[i + 1]),
+     * flattened into the staging; in_len = the flattened lengths) */
+    uint64_t in_bytes = 0, out_bytes = 0, in_lo = gbuf ? 0 : in_off[0];
     uint32_t max_len = 0, max_cap = 0;
-    int packed_in = 1;
+    int packed_in = gbuf == NULL;
     for (size_t i = 0; i < n; ++i) {
-        if (in_off[i] != in_lo + in_bytes) packed_in = 0;
+        if (!gbuf && in_off[i] != in_lo + in_bytes) packed_in = 0;
         in_bytes += in_len[i];
         uint64_t f = out_off[i] + out_cap[i];
         if (f > out_bytes) out_bytes = f;
@@ -565,7 +612,8 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         const size_t lo = n * (size_t) g / (size_t) ig, hi = n * (size_t) (g + 1) / (size_t) ig;
         if (hi <= lo) continue;
         const uint64_t b0 = hio[lo], b1 = hio[hi - 1] + in_len[hi - 1];
-        if (packed_in) par_memcpy(h + a_in + b0, in + in_lo + b0, b1 - b0);
+        if (gbuf) par_gather(h + a_in, hio, gbuf, gfirst, lo, hi, b1 - b0);
+        else if (packed_in) par_memcpy(h + a_in + b0, in + in_lo + b0, b1 - b0);
         else par_scatter(h + a_in, hio, in, in_off, in_len, lo, hi, b1 - b0);
         if (b1 > b0) err = hipMemcpyAsync(d + a_in + b0, h + a_in + b0, b1 - b0, hipMemcpyHostToDevice, c->stream);
         if (err != hipSuccess) return (int) err;
@@ -674,14 +722,38 @@ int enet_rc_compress_batch_host(void *context, const uint8_t *in, const uint64_t
                                 const uint32_t *in_len, size_t n, uint8_t *out,
                                 const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return run_host((rc_ctx *) context, 0, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1);
+    return run_host((rc_ctx *) context, 0, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
 }
 
 int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
                                   const uint32_t *in_len, size_t n, uint8_t *out,
                                   const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1);
+    return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
+}
+
+/* compress.c:246-342 over a batch of gather lists: packet i is
+ * buffers[first[i] .. first[i + 1]), consumed as enet_range_coder_compress
+ * consumes its inBuffers (protocol.c:1688-1695 passes &buffers[1],
+ * bufferCount - 1); the lists are flattened straight into the pinned
+ * staging on the copy threads. */
+int enet_rc_compress_gather_batch_host(void *context, const ENetBuffer *buffers, const size_t *first, size_t n,
+                                       uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                                       uint32_t *out_len)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    if (!c || (n && (!buffers || !first))) return (int) hipErrorInvalidValue;
+    if (n == 0) return 0;
+    uint32_t *len = (uint32_t *) malloc(n * sizeof(uint32_t));
+    if (!len) return (int) hipErrorOutOfMemory;
+    for (size_t i = 0; i < n; ++i) {
+        const size_t l = first[i + 1] >= first[i] ? gather_len(buffers + first[i], first[i + 1] - first[i]) : 0;
+        if (l > 0xFFFFFFFFu) { free(len); return (int) hipErrorInvalidValue; }
+        len[i] = (uint32_t) l;
+    }
+    const int rc = run_host(c, 0, NULL, NULL, len, n, out, out_off, out_cap, out_len, 0, buffers, first);
+    free(len);
+    return rc;
 }
 
 /* --------------------------------------------------- datagram framing (§8f) */
@@ -914,29 +986,15 @@ size_t enet_range_coder_compress(void *context, const ENetBuffer *inBuffers, siz
 {
     rc_ctx *c = (rc_ctx *) context;
     if (c == NULL || inBufferCount <= 0 || inLimit <= 0) return 0;      /* compress.c:257-258 */
-    /* Flatten the gather list the way compress.c:275-284 walks it: the first
-     * buffer may be empty (skipped); every later buffer contributes at least
-     * one byte, its data[0], even when its length is 0. */
-    size_t total = inBuffers[0].dataLength;
-    for (size_t i = 1; i < inBufferCount; ++i)
-        total += inBuffers[i].dataLength ? inBuffers[i].dataLength : 1;
+    /* the gather list is flattened into the staging the way compress.c:275-284
+     * walks it (gather_len / gather_copy) */
+    const size_t total = gather_len(inBuffers, inBufferCount);
     if (total > 0xFFFFFFFFu || outLimit > 0xFFFFFFFFu) return 0;
-    uint8_t *flat = (uint8_t *) malloc(total ? total : 1);
-    if (!flat) return 0;
-    size_t pos = 0;
-    memcpy(flat, inBuffers[0].data, inBuffers[0].dataLength);
-    pos = inBuffers[0].dataLength;
-    for (size_t i = 1; i < inBufferCount; ++i) {
-        size_t l = inBuffers[i].dataLength;
-        if (l) { memcpy(flat + pos, inBuffers[i].data, l); pos += l; }
-        else flat[pos++] = *(const uint8_t *) inBuffers[i].data;
-    }
-    uint64_t ioff = 0, ooff = 0;
-    uint32_t ilen = (uint32_t) total, ocap = (uint32_t) outLimit, olen = 0;
-    int rc = 0;
-    if (total == 0) { free(flat); return 0; }   /* only empty buffers: compress.c flushes nothing */
-    rc = enet_rc_compress_batch_host(c, flat, &ioff, &ilen, 1, outData, &ooff, &ocap, &olen);
-    free(flat);
+    if (total == 0) return 0;   /* only an empty first buffer: compress.c flushes nothing */
+    const size_t first[2] = {0, inBufferCount};
+    uint64_t ooff = 0;
+    uint32_t ocap = (uint32_t) outLimit, olen = 0;
+    const int rc = enet_rc_compress_gather_batch_host(c, inBuffers, first, 1, outData, &ooff, &ocap, &olen);
     return rc == 0 ? (size_t) olen : 0;
 }
 
@@ -1006,7 +1064,7 @@ int rc_ctx_run_host(void *context, int decompress, const uint8_t *in, const uint
 {
     /* (no page-locking of the caller's memory: the devices' ranges share
      * boundary pages, and one range's unregister would unpin another's) */
-    return run_host((rc_ctx *) context, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 0);
+    return run_host((rc_ctx *) context, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 0, NULL, NULL);
 }
 
 /* The context's block-sum workspace of rc_pack.hip for n packets (device

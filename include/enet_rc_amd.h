@@ -123,6 +123,18 @@ int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64
                                   const uint32_t *in_len, size_t n, uint8_t *out,
                                   const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
 
+/* Compress a batch of gather lists (host pointers): packet i is the list
+ * buffers[first[i] .. first[i + 1]) (first has n + 1 entries), consumed
+ * exactly as enet_range_coder_compress consumes its inBuffers
+ * (compress.c:260-285: an empty first buffer contributes nothing, an empty
+ * later buffer its data[0]); protocol.c:1688-1695 hands the compressor
+ * &buffers[1], bufferCount - 1 per datagram.  A list of one empty buffer
+ * (or none) yields out_len 0.  Outputs as enet_rc_compress_batch_host.  The
+ * lists are flattened straight into the context's pinned staging. */
+int enet_rc_compress_gather_batch_host(void *context, const ENetBuffer *buffers, const size_t *first, size_t n,
+                                       uint8_t *out, const uint64_t *out_off, const uint32_t *out_cap,
+                                       uint32_t *out_len);
+
 /* ==================================================================== CRC-32
  * crc_out[i] = enet_crc32 (packet.c:143-163) of the single buffer
  * in[in_off[i] .. +in_len[i]): CRC-32/IEEE, returned in network byte order

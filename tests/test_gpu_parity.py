@@ -563,3 +563,49 @@ def test_encoder_chunks_vs_oracle(coder):
     torch.cuda.synchronize()
     assert torch.equal(dl, dlen)
     assert torch.equal(dout, din)
+
+
+def test_gather_batch_fixtures_and_oracle(coder):
+    """enet_rc_compress_gather_batch_host: the reference's gather fixtures in
+    one batch, then random gather lists (empty first buffers, empty later
+    buffers -- the phantom byte, compress.c:275-284 -- and single spans)
+    against the oracle's per-list compress."""
+    from oracle.pyoracle import Coder
+    cases = [c for c in golden_io.gather_cases() if c["in_limit"] > 0]
+    backing, lists, caps = b"", [], []
+    for c in cases:
+        base = len(backing)
+        backing += c["backing"]
+        lists.append([(base + s, l) for s, l in c["spans"]])
+        caps.append(c["out_limit"])
+    res = coder.compress_gather_batch(backing, lists, caps)
+    for c, r in zip(cases, res):
+        assert r[0] == c["ret"], c["spans"][:4]
+        if c["ret"]:
+            assert r[1] == c["expect"]
+    # random lists, enough bytes for the threaded flattening (> 16 MB)
+    from oracle.pyoracle import compress_batch as ocompress
+    rng = np.random.default_rng(17)
+    backing = rng.integers(0, 8, size=1 << 20, dtype=np.uint8).tobytes()
+    lists, flat = [], []
+    for i in range(24000):
+        spans = []
+        for j in range(int(rng.integers(1, 6))):
+            ln = 0 if rng.random() < 0.2 else int(rng.integers(1, 800))
+            spans.append((int(rng.integers(0, len(backing) - 1024)), ln))
+        lists.append(spans)
+        # compress.c:275-284: the first buffer as is, a later empty one its data[0]
+        f = backing[spans[0][0]: spans[0][0] + spans[0][1]]
+        for s0, l0 in spans[1:]:
+            f += backing[s0: s0 + l0] if l0 else backing[s0: s0 + 1]
+        flat.append(f)
+    keep = [i for i, f in enumerate(flat) if f]
+    d, o, l = synth.pack([flat[i] for i in keep])
+    ref, roff, cap, rlen = ocompress(d, o, l, "port")
+    caps = [2 * len(f) + 64 for f in flat]
+    res = coder.compress_gather_batch(backing, lists, caps)
+    assert sum(len(f) for f in flat) > (16 << 20)
+    for j, i in enumerate(keep):
+        assert res[i][0] == int(rlen[j])
+        assert res[i][1] == ref[int(roff[j]): int(roff[j]) + int(rlen[j])].tobytes()
+    assert all(res[i] == (0, b"") for i, f in enumerate(flat) if not f)
