@@ -1653,6 +1653,35 @@ DEV void wide_big_bucket(WScanLds& s, uint32_t bs, uint32_t k, uint2* wrec, W2Pr
     W2P(9)
 }
 
+// The wide scan's next packet, fetched while the current one is walked: its
+// length, alignment and 16-B chunks (list, order, lengths and offsets through
+// scalar loads; the loads are issued on every path, as in scan_prefetch).
+struct WPf {
+    uint32_t n, mis;
+    uint4 r0, r1;
+};
+
+DEV WPf wide_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t q, uint32_t nw)
+{
+    WPf f;
+    f.n = 0; f.mis = 0;
+    uintptr_t a0 = reinterpret_cast<uintptr_t>(b.in) & ~static_cast<uintptr_t>(15), a1 = a0;
+    if (q < nw) {
+        const uint32_t idx = const_load(e.wlist, q);
+        const uint32_t pkt = (e.order && !const_load(e.bins, RC_LEN_BINS)) ? const_load(e.order, idx) : idx;
+        f.n = const_load(b.in_len, pkt);
+        const uintptr_t src = reinterpret_cast<uintptr_t>(b.in + const_load(b.in_off, pkt));
+        const uintptr_t a16 = src & ~static_cast<uintptr_t>(15);
+        f.mis = static_cast<uint32_t>(src & 15);
+        const uint32_t last = (f.mis + f.n - 1) >> 4;
+        a0 = a16 + 16 * min(threadIdx.x, last);
+        a1 = a16 + 16 * min(threadIdx.x + kScanThreads, last);
+    }
+    f.r0 = gload16(a0);
+    f.r1 = gload16(a1);
+    return f;
+}
+
 extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_wscan(rc_batch_dev b, E2Params e)
 {
@@ -1661,21 +1690,15 @@ void rc_enc2_wscan(rc_batch_dev b, E2Params e)
     const uint32_t nw = min(*e.wcount, e.wcap);
     W2Prof wp;
     W2P_INIT
+    WPf pf = wide_prefetch(b, e, blockIdx.x, nw);
     for (uint32_t q = blockIdx.x; q < nw; q += gridDim.x) {
-        const uint32_t idx = e.wlist[q];
-        const uint32_t pkt = packet_of(e, idx);
-        const uint32_t n = b.in_len[pkt];             // (1 <= n <= slot_len: rc_enc2_scan)
+        const WPf cur = pf;
+        const uint32_t n = cur.n, mis = cur.mis;      // (1 <= n <= slot_len: rc_enc2_scan)
         uint2* wrec = reinterpret_cast<uint2*>(e.wide + static_cast<size_t>(q) * e.wslot_bytes);
-        const uintptr_t src = reinterpret_cast<uintptr_t>(b.in + b.in_off[pkt]);
-        const uintptr_t a16 = src & ~static_cast<uintptr_t>(15);
-        const uint32_t mis = static_cast<uint32_t>(src & 15);
-        const uint32_t last = (mis + n - 1) >> 4;
-        const uint4 r0 = gload16(a16 + 16 * min(t, last));
-        const uint4 r1 = gload16(a16 + 16 * min(t + kScanThreads, last));
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
         if (t < 16) *reinterpret_cast<uint4*>(&s.f2bits[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = r0;
-        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = r1;
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = cur.r0;
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = cur.r1;
         wave_sync();
         W2P(0)
         const uint32_t q0 = 16 + mis;
@@ -1728,6 +1751,7 @@ void rc_enc2_wscan(rc_batch_dev b, E2Params e)
         }
         const uint32_t x0 = s.x[q0];
         wave_sync();
+        pf = wide_prefetch(b, e, q + gridDim.x, nw);  // (the next packet, while this one is walked)
         W2P(3)
         // buckets of <= kE2Bucket elements, whole buckets per round
         wide_small_buckets(s, q0, total, wrec);

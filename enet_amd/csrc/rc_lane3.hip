@@ -161,9 +161,31 @@ DEV uint32_t slot_info(const Ctx<NV, O2>& c, const uint32_t* eq)
     return a | (b << 8);
 }
 
+// Dense blocks of big order-2 contexts (Ctx<6, false>) live in the arena
+// (dense 1) or, for the first one of a packet, in the lane's 288-B LDS block
+// ldsb (dense 2): game-state packets have exactly one such context, (0, 0),
+// visited by about half of their bytes, whose lookups, updates and rescales
+// then stay on chip.  (Two call sites, one per address space: a pointer
+// select would become flat memory operations.)
+template <uint32_t NV, bool O2>
+DEV void ctx_dense_find(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV, O2>& c, uint32_t v, Dense& z,
+                        uint32_t& u, uint32_t& n)
+{
+    if (!O2 && c.dense == 2) dense_find(ldsb, v, O2, z, u, n);
+    else dense_find(reg + c.ext, v, O2, z, u, n);
+}
+
+template <uint32_t NV, bool O2>
+DEV bool ctx_dense_search(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV, O2>& c, uint32_t code, Dense& z,
+                          uint32_t& v, uint32_t& u, uint32_t& n)
+{
+    if (!O2 && c.dense == 2) return dense_search(ldsb, code, O2, z, v, u, n);
+    return dense_search(reg + c.ext, code, O2, z, v, u, n);
+}
+
 // compress.c:159-199 lookup of v (minimum 0): slot, counts below v, count[v], o2 info
 template <uint32_t NV, bool O2>
-DEV Look<NV> ctx_find(const uint8_t* reg, const Ctx<NV, O2>& c, uint32_t v)
+DEV Look<NV> ctx_find(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV, O2>& c, uint32_t v)
 {
     Look<NV> h;
     h.k = 0; h.under = 0; h.cnt = 0;
@@ -182,7 +204,7 @@ DEV Look<NV> ctx_find(const uint8_t* reg, const Ctx<NV, O2>& c, uint32_t v)
     if (any_lane(c.dense != 0)) {
         if (c.dense != 0) {
             uint32_t u, n;
-            dense_find(reg + c.ext, v, O2, h.z, u, n);
+            ctx_dense_find(reg, ldsb, c, v, h.z, u, n);
             h.under = u; h.cnt = n; h.info = h.z.link;
         }
     }
@@ -194,7 +216,8 @@ DEV Look<NV> ctx_find(const uint8_t* reg, const Ctx<NV, O2>& c, uint32_t v)
 // (minimum 0): the dword whose running byte sum passes code, then halving
 // on byte sums inside it.  False = no such symbol (corrupt, compress.c:416).
 template <uint32_t NV, bool O2>
-DEV bool ctx_search(const uint8_t* reg, const Ctx<NV, O2>& c, uint32_t code, Look<NV>& h, uint32_t& v)
+DEV bool ctx_search(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV, O2>& c, uint32_t code, Look<NV>& h,
+                    uint32_t& v)
 {
     uint32_t acc = 0, base = 0, wc = 0, wv = 0xFFFFFFFFu, j = 0;
     bool hit = false;
@@ -222,7 +245,7 @@ DEV bool ctx_search(const uint8_t* reg, const Ctx<NV, O2>& c, uint32_t code, Loo
     if (any_lane(c.dense != 0)) {
         if (c.dense != 0) {
             uint32_t u, n, vv;
-            ok = dense_search(reg + c.ext, code, O2, h.z, vv, u, n);
+            ok = ctx_dense_search(reg, ldsb, c, code, h.z, vv, u, n);
             h.under = u; h.cnt = n; v = vv; h.info = h.z.link;
         }
     }
@@ -267,15 +290,11 @@ DEV void slot_set_info(Ctx<NV, O2>& c, const uint32_t* eq, uint32_t info, bool e
     }
 }
 
-// move an inline context to a fresh dense block; false = arena full
+// a dense block's contents from an inline context (C[16], counts, o2 info)
 template <uint32_t NV, bool O2>
-DEV bool densify(uint8_t* reg, Ctx<NV, O2>& c, uint32_t& bump, uint32_t end)
+DEV void dense_fill(uint8_t* blk, const Ctx<NV, O2>& c)
 {
     const uint32_t size = O2 ? kDenseO1 : kDenseO2;
-    const uint32_t at = (bump + 15) & ~15u;
-    if (at + size > end) return false;
-    bump = at + size;
-    uint8_t* blk = reg + at;
     uint4* p = reinterpret_cast<uint4*>(blk);
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
     for (uint32_t i = 2; i < size / 16; ++i) p[i] = z;
@@ -303,18 +322,38 @@ DEV bool densify(uint8_t* reg, Ctx<NV, O2>& c, uint32_t& bump, uint32_t end)
         blk[32 + vv] = static_cast<uint8_t>(cc);
         if (O2) reinterpret_cast<uint16_t*>(blk + 288)[vv] = static_cast<uint16_t>(ia | (ib << 8));
     }
+}
+
+// move an inline context to a fresh dense block -- the lane's LDS block for
+// the packet's first big order-2 context (ldsu: taken), else the arena;
+// false = arena full
+template <uint32_t NV, bool O2>
+DEV bool densify(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c, uint32_t& bump, uint32_t end)
+{
+    const bool lds = !O2 && ldsu == 0;
+    if (lds) {
+        dense_fill<NV, O2>(ldsb, c);
+        ldsu = 1;
+        c.ext = 0;
+    } else {
+        const uint32_t size = O2 ? kDenseO1 : kDenseO2;
+        const uint32_t at = (bump + 15) & ~15u;
+        if (at + size > end) return false;
+        bump = at + size;
+        dense_fill<NV, O2>(reg + at, c);
+        c.ext = at;
+    }
 #pragma unroll
     for (uint32_t d = 0; d < NV; ++d) { c.val[d] = 0xFFFFFFFFu; c.cnt[d] = 0u; }
 #pragma unroll
     for (uint32_t d = 0; d < (O2 ? NV : 1); ++d) { c.oa[d] = 0u; c.ob[d] = 0u; }
-    c.dense = 1;
-    c.ext = at;
+    c.dense = lds ? 2u : 1u;
     return true;
 }
 
 // compress.c:90-112 where `en`
 template <uint32_t NV, bool O2>
-DEV void ctx_rescale(uint8_t* reg, Ctx<NV, O2>& c, bool en)
+DEV void ctx_rescale(uint8_t* reg, uint8_t* ldsb, Ctx<NV, O2>& c, bool en)
 {
     if (!rare_lane(en)) return;
     uint32_t sum = 0;
@@ -325,7 +364,10 @@ DEV void ctx_rescale(uint8_t* reg, Ctx<NV, O2>& c, bool en)
         sum = sad(h, sum);
     }
     if (rare_lane(en && c.dense != 0)) {
-        if (en && c.dense != 0) sum = dense_rescale(reg + c.ext);
+        if (en && c.dense != 0) {
+            if (!O2 && c.dense == 2) sum = dense_rescale(ldsb);
+            else sum = dense_rescale(reg + c.ext);
+        }
     }
     c.esc -= en ? (c.esc >> 1) : 0u;
     c.tot = en ? ((c.esc + sum) & 0xFFFF) : c.tot;
@@ -335,8 +377,8 @@ DEV void ctx_rescale(uint8_t* reg, Ctx<NV, O2>& c, bool en)
 // the lookup h of v: bump v or insert it, then total and rescale.  h.k stays
 // the slot of v.
 template <uint32_t NV, bool O2>
-DEV void ctx_update(uint8_t* reg, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v, uint32_t& bump, uint32_t end,
-                    bool& ovf, bool en)
+DEV void ctx_update(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v,
+                    uint32_t& bump, uint32_t end, bool& ovf, bool en)
 {
     const bool ins = en && !h.found;
     const bool inl = c.dense == 0;
@@ -347,11 +389,14 @@ DEV void ctx_update(uint8_t* reg, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v, uint3
     const bool grow = ins && inl && c.len >= cap;
     if (rare_lane(grow || (en && !inl))) {
         if (grow) {
-            const bool ok = densify<NV, O2>(reg, c, bump, end);
+            const bool ok = densify<NV, O2>(reg, ldsb, ldsu, c, bump, end);
             ovf = ovf || !ok;
-            if (ok) { uint32_t u, n; dense_find(reg + c.ext, v, O2, h.z, u, n); }
+            if (ok) { uint32_t u, n; ctx_dense_find(reg, ldsb, c, v, h.z, u, n); }
         }
-        if (en && c.dense != 0 && !ovf) dense_add(reg + c.ext, v, kSubDelta, h.z);   // (new: o2 info is 0)
+        if (en && c.dense != 0 && !ovf) {                                   // (new: o2 info is 0)
+            if (!O2 && c.dense == 2) dense_add(ldsb, v, kSubDelta, h.z);
+            else dense_add(reg + c.ext, v, kSubDelta, h.z);
+        }
     }
     if (ins && c.dense == 0) {
 #pragma unroll
@@ -361,7 +406,7 @@ DEV void ctx_update(uint8_t* reg, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v, uint3
     c.esc += ins ? kSubEscDelta : 0u;
     const uint32_t tot = (c.tot + (ins ? kSubEscDelta : 0u) + kSubDelta) & 0xFFFF;
     c.tot = en ? tot : c.tot;
-    ctx_rescale<NV, O2>(reg, c, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
+    ctx_rescale<NV, O2>(reg, ldsb, c, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
 }
 
 // ------------------------------------------------------------ lane state
@@ -383,6 +428,7 @@ struct Lane {
     uint32_t same, fwd, prv_dirty, q_dirty, q_fwd, ovf;
     uint32_t nsame, fromprv;    // where the next step's R[v] comes from (lane_prefetch)
     uint32_t nodes;             // compress.c's nextSymbol: 1 (root) + the (context, value) pairs created
+    uint32_t ldsu;              // the lane's LDS dense block holds a big order-2 context
 };
 
 DEV void lane_init(Lane& L, uint8_t* reg)
@@ -394,6 +440,7 @@ DEV void lane_init(Lane& L, uint8_t* reg)
     L.same = false; L.fwd = true; L.prv_dirty = false; L.q_dirty = false; L.q_fwd = true; L.ovf = false;
     L.nsame = false; L.fromprv = false;
     L.nodes = 1;
+    L.ldsu = 0;
 }
 
 // compress.c:148-157: the model starts over (new epoch: every order-1 record
@@ -408,6 +455,7 @@ DEV void lane_reset(Lane& L, uint8_t* reg)
     L.same = false; L.fwd = true; L.prv_dirty = false; L.q_dirty = false; L.q_fwd = true;
     L.nsame = false; L.fromprv = false;
     L.nodes = 1;
+    L.ldsu = 0;
 }
 
 // top of a step: the records loaded by the previous step become registers
@@ -455,8 +503,8 @@ DEV void o2_stats(const Lane& L, uint32_t& esc, uint32_t& tot)
 //   2. update the o1 context b (at <= 1): bump or insert
 //   3. the o2 info of (b, v) and where it lives, the loads for step i+1
 template <bool HAVE_H1>
-DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, Look<3>& h1, Look<6>& h2,
-                      bool new0, bool track)
+DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32_t v, int at, Look<3>& h1,
+                      Look<6>& h2, bool new0, bool track)
 {
     // nodes compress.c creates this step: v in each visited context that lacks
     // it (the order-2 context is always visited, order 1 when order 2 did not
@@ -503,7 +551,7 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, L
         if (any_lane(big)) {
             if (big && !L.ovf) {
                 bool ovf = L.ovf != 0;
-                ctx_update<6, false>(reg, L.q, h2, v, L.bump, end, ovf, true);
+                ctx_update<6, false>(reg, ldsb, L.ldsu, L.q, h2, v, L.bump, end, ovf, true);
                 L.ovf = ovf;
                 L.q_dirty = true;
             }
@@ -520,11 +568,11 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, L
         }
     }
     // ---- 2. o1 context b, compress.c:286-316 (its lookup, when the decoder did not need it)
-    if (!HAVE_H1 && L.order >= 1 && at == 2) h1 = ctx_find<3, true>(reg, L.cur, v);
+    if (!HAVE_H1 && L.order >= 1 && at == 2) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
     if (L.order >= 1 && at <= 1) {
         if (track) created += h1.found ? 0u : 1u;
         bool ovf = L.ovf != 0;
-        ctx_update<3, true>(reg, L.cur, h1, v, L.bump, end, ovf, true);
+        ctx_update<3, true>(reg, ldsb, L.ldsu, L.cur, h1, v, L.bump, end, ovf, true);
         L.ovf = ovf;
     }
     if (track) L.nodes += created;
@@ -573,7 +621,7 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint32_t end, uint32_t v, int at, L
 // ------------------------------------------------------------ one packet
 
 DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg, uint8_t* root,
-                       const uint8_t* mtab)
+                       uint8_t* ldsb, const uint8_t* mtab)
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
@@ -617,7 +665,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         Look<6> h2;
         h2.found = (L.info & 0xFF) == v ? 1u : 0u; h2.under = 0; h2.cnt = L.info >> 8;
         if (any_lane(en2 && big)) {
-            if (en2 && big) h2 = ctx_find<6, false>(reg, L.q, v);
+            if (en2 && big) h2 = ctx_find<6, false>(reg, ldsb, L.q, v);
         }
         const bool done2 = en2 && h2.found;
         PROF(1)
@@ -626,7 +674,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         PROF(2)
         // order 1
         const bool en1 = !done2 && L.order >= 1;
-        Look<3> h1 = ctx_find<3, true>(reg, L.cur, v);
+        Look<3> h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
         PROF(3)
         const bool done1 = en1 && h1.found;
         const uint32_t esc1 = L.cur.esc, tot1 = L.cur.tot;
@@ -644,7 +692,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
         // no loop exit between the record load (lane_prefetch) and the record
         // store (lane_advance): an exit path there makes the compiler's vmcnt
         // bookkeeping wait for the store at the top of every step
-        lane_advance<true>(L, reg, end, v, done2 ? 2 : done1 ? 1 : 0, h1, h2, en0 && cnt0 == 0, track);
+        lane_advance<true>(L, reg, ldsb, end, v, done2 ? 2 : done1 ? 1 : 0, h1, h2, en0 && cnt0 == 0, track);
         PROF(6)
         if (rare_lane(!ok || L.ovf)) { if (!ok || L.ovf) break; }
         if (track) {                                                  // compress.c:332 -> :148-157
@@ -669,7 +717,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
 }
 
 DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg,
-                         uint8_t* root)
+                         uint8_t* root, uint8_t* ldsb)
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
@@ -722,7 +770,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
                 fu = esc2; fc = h2.cnt;
                 at = 2;
             } else {
-                if (!ctx_search<6, false>(reg, L.q, cd - esc2, h2, v)) { fail = true; break; }
+                if (!ctx_search<6, false>(reg, ldsb, L.q, cd - esc2, h2, v)) { fail = true; break; }
                 fu = esc2 + h2.under; fc = h2.cnt;
                 at = 2;
             }
@@ -734,7 +782,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (cd < L.cur.esc) {
                 dec_code(low, code, range, 0, L.cur.esc, in, true);
             } else {
-                if (!ctx_search<3, true>(reg, L.cur, cd - L.cur.esc, h1, v)) { fail = true; break; }
+                if (!ctx_search<3, true>(reg, ldsb, L.cur, cd - L.cur.esc, h1, v)) { fail = true; break; }
                 fu = L.cur.esc + h1.under; fc = h1.cnt;
                 at = 1;
             }
@@ -764,12 +812,12 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
         }
         // the patched o1 context needs v's lookup (compress.c:598-615)
-        if (at == 0 && L.order >= 1) h1 = ctx_find<3, true>(reg, L.cur, v);
-        if (at == 2 && L.order >= 1) h1 = ctx_find<3, true>(reg, L.cur, v);
-        if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, L.q, v);
+        if (at == 0 && L.order >= 1) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
+        if (at == 2 && L.order >= 1) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
+        if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, ldsb, L.q, v);
         fail = o.n >= o.cap;                                         // compress.c:617
         PROF(4)
-        lane_advance<true>(L, reg, end, v, at, h1, h2, new0, true); // (see compress_one3)
+        lane_advance<true>(L, reg, ldsb, end, v, at, h1, h2, new0, true); // (see compress_one3)
         PROF(5)
         if (fail || L.ovf) break;
         if (rare_lane(L.nodes >= kNodeLimit)) {                      // compress.c:617-621 -> :148-157
@@ -819,6 +867,7 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     if (l >= act) return;
     const uint32_t local = wave * act + l;
     uint8_t* root = smem + local * (DECOMP ? kRootStrideDec : kRootStride3);
+    uint8_t* ldsb = smem + (DECOMP ? 4 * act * kRootStrideDec : 4 * act * kRootStride3 + 256) + local * kDenseO2;
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
@@ -826,8 +875,8 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t count = ws.sub_count ? *ws.sub_count : b.n;   // a sub-list: the two-pass encoder's leftovers
     for (uint32_t i = slot; i < count; i += gridDim.x * per_block) {
         const uint32_t pkt = ws.sub_list ? ws.sub_list[i] : (order ? order[i] : i);
-        if (DECOMP) decompress_one3(b, ws, pkt, reg, root);
-        else compress_one3(b, ws, pkt, reg, root, mtab);
+        if (DECOMP) decompress_one3(b, ws, pkt, reg, root, ldsb);
+        else compress_one3(b, ws, pkt, reg, root, ldsb, mtab);
     }
 }
 
@@ -843,10 +892,11 @@ extern "C" int rc_hip_lane3_launch(int decompress, const rc_batch_dev* b, const 
                                    uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // the encoder: roots with their D copy + the mask table; the decoder: roots only (LDS
-    // left for a co-resident encoder block, rc_enc2_code)
-    const size_t lds = decompress ? static_cast<size_t>(4 * ws->lane_active) * kRootStrideDec
-                                  : static_cast<size_t>(4 * ws->lane_active) * kRootStride3 + 256;
+    // the encoder: roots with their D copy + the mask table; the decoder: roots;
+    // then a dense order-2 block per lane
+    const size_t lds = (decompress ? static_cast<size_t>(4 * ws->lane_active) * kRootStrideDec
+                                   : static_cast<size_t>(4 * ws->lane_active) * kRootStride3 + 256) +
+                       static_cast<size_t>(4 * ws->lane_active) * kDenseO2;
     if (decompress)
         hipLaunchKernelGGL(rc_decompress_lane3, dim3(blocks), dim3(256), lds, st, *b, *ws);
     else

@@ -14,8 +14,9 @@
 
 static uint8_t g_root[304] __attribute__((aligned(16)));
 static uint8_t g_mtab[256] __attribute__((aligned(16)));
+static uint8_t g_ldsb[kDenseO2] __attribute__((aligned(16)));   // the lane's LDS dense block
 static bool g_mtab_init = [] { for (uint32_t j = 0; j < 16; ++j) root3_mask_init(g_mtab, j); return true; }();
-#define COMPRESS_ARGS , g_mtab
+#define COMPRESS_ARGS , g_ldsb, g_mtab
 
 extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t cap,
                              uint32_t max_len, uint32_t* out_len)
@@ -42,7 +43,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     }
 #endif
 
-    if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root);
+    if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root, g_ldsb);
     else COMPRESS_ONE(b, ws, 0, region, g_root COMPRESS_ARGS);
     return counters[0] ? 1 : (counters[3] ? 2 : 0);   // 1 = routed to the exact path, 2 = left by dec4
 }

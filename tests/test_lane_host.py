@@ -105,3 +105,29 @@ def test_lane_logic_region_overflow_routes_exact(lane):
     data = np.random.default_rng(3).integers(0, 256, 1200, dtype=np.uint8)
     data &= 15
     assert lane(0, data.tobytes(), 4096, max_len=16)[0] == "exact"
+
+
+def test_lane_logic_dense_order2_contexts(lane):
+    """Packets whose order-2 contexts go dense (more than 24 symbols): game
+    state ((0, 0) in every packet -- the lane's LDS dense block), several dense
+    order-2 contexts per packet (the first in the LDS block, the others in the
+    arena), long packets across the model reset.  Both directions, against
+    the oracle."""
+    from enet_amd import synth
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(23)
+    d, o, l = synth.gamestate_batch(6, 1200)
+    pk = [d[int(o[i]): int(o[i]) + 1200].tobytes() for i in range(6)]
+    for n in (1500, 3000, 4096):
+        # three heavy contexts: bytes after (0, 0), (1, 1) and (2, 2) drawn from 40 values
+        x = np.zeros(n, np.uint8)
+        for j in range(2, n):
+            x[j] = rng.integers(0, 40) if x[j - 1] == x[j - 2] and rng.random() < 0.5 else x[j - 1]
+        pk.append(x.tobytes())
+        pk.append(np.where(rng.random(n) < 0.7, 0, rng.integers(0, 256, n)).astype(np.uint8).tobytes())
+    for p in pk:
+        cap = 2 * len(p) + 64
+        ref = port.compress(p, out_limit=cap)
+        assert lane(0, p, cap, max_len=len(p)) == ref
+        assert lane(1, ref[1], len(p), max_len=len(p)) == (len(p), p)
