@@ -281,15 +281,14 @@ def _walk(vals, found):
     return _dense_walk(vals, found)
 
 
-def scan_wide(p: bytes):
-    """Wide-mode pass 1: one (A, B, root) record per position, or None for a
-    packet the wide scan does not take (empty, or long enough for a model
-    reset)."""
+def _scan_wide_segment(p: bytes):
+    """Records of a model segment (the packet, or the bytes after a model
+    reset): (A, B, root) per position, and per position whether order 2 /
+    order 1 found its byte."""
     n = len(p)
-    if n == 0 or n > MAX_LEN:
-        return None
     recs = [None] * n
     recs[0] = (None, None, True)
+    f2all, f1all = [False] * n, [False] * n
     buckets = defaultdict(list)
     for i in range(1, n):
         buckets[p[i - 1]].append(i)
@@ -324,12 +323,53 @@ def scan_wide(p: bytes):
         codes = _walk([p[i] for i in vis1], found) if len(lst) > MAX_BUCKET else _closed_form([p[i] for i in vis1], found)
         B = {i: (cd, fd) for i, cd, fd in zip(vis1, codes, found)}
         for i in lst:
+            f2all[i] = f2[i]
             if f2[i]:
                 recs[i] = (A.get(i), None, False)
             else:
                 cd, fd = B[i]
+                f1all[i] = fd
                 recs[i] = (A.get(i), cd, not fd)
-    return recs
+    return recs, f2all, f1all
+
+
+NODE_LIMIT = 4096 - 2          # compress.c:148-157
+
+
+def _reset_point(p: bytes, f2, f1):
+    """compress.c:148-157: the first position after which the segment holds
+    NODE_LIMIT symbols (1 for the root, one per symbol created: in the
+    order-2 context when it lacks the byte, in the order-1 context when it is
+    visited and lacks it, at the root when it is visited for the first time
+    with that byte), or None."""
+    nodes, seen = 1, set()
+    for i, v in enumerate(p):
+        nodes += (i >= 2 and not f2[i]) + (i >= 1 and not f2[i] and not f1[i])
+        if i == 0 or (not f2[i] and not f1[i]):
+            nodes += v not in seen
+            seen.add(v)
+        if nodes >= NODE_LIMIT:
+            return i
+    return None
+
+
+def scan_wide(p: bytes, max_len: int = MAX_LEN):
+    """Wide-mode pass 1: one (A, B, root, reset) record per position (reset:
+    the model starts over after the position), or None for a packet the wide
+    scan does not take (empty, or longer than max_len)."""
+    n = len(p)
+    if n == 0 or n > max_len:
+        return None
+    out, s = [], 0
+    while s < n:
+        recs, f2, f1 = _scan_wide_segment(p[s:])
+        r = _reset_point(p[s:], f2, f1)
+        if r is None or s + r + 1 >= n:
+            out += [rc + (False,) for rc in recs]
+            break
+        out += [rc + (False,) for rc in recs[: r]] + [recs[r] + (True,)]
+        s += r + 1
+    return out
 
 
 def code_wide(p: bytes, recs, out_limit: int):
@@ -338,7 +378,7 @@ def code_wide(p: bytes, recs, out_limit: int):
     cnt = [0] * 256
     rtot = 257
     for i, v in enumerate(p):
-        a, b, root = recs[i]
+        a, b, root, reset = recs[i]
         for op in (a, b):
             if op is not None:
                 enc.code(*op)
@@ -352,6 +392,9 @@ def code_wide(p: bytes, recs, out_limit: int):
                 for u in range(256):
                     cnt[u] -= cnt[u] >> 1
                 rtot = sum(cnt) + 1 + 256
+        if reset:                                           # compress.c:148-157
+            cnt = [0] * 256
+            rtot = 257
         if not enc.ok:
             return 0, b""
     enc.flush()
@@ -360,8 +403,8 @@ def code_wide(p: bytes, recs, out_limit: int):
     return len(enc.out), bytes(enc.out)
 
 
-def compress_wide(p: bytes, out_limit: int):
-    r = scan_wide(p)
+def compress_wide(p: bytes, out_limit: int, max_len: int = MAX_LEN):
+    r = scan_wide(p, max_len)
     if r is None:
         return None
     return code_wide(p, r, out_limit)

@@ -125,3 +125,18 @@ def test_wide_model_golden_fixtures():
             assert r[1] == c["expect"]
         n += 1
     assert n > 100
+
+
+def test_wide_model_long_packets_with_resets(port):
+    """Packets of 1920-4096 B: model resets (compress.c:148-157) where the
+    segment's node count reaches 4094; each segment is modelled afresh."""
+    rng = np.random.default_rng(9)
+    resets = 0
+    for n in (1920, 2600, 4096):
+        for p in (rng.integers(0, 256, n, dtype=np.uint8).tobytes(),
+                  np.where(rng.random(n) < 0.6, 0, rng.integers(0, 256, n)).astype(np.uint8).tobytes(),
+                  rng.integers(0, 40, n, dtype=np.uint8).tobytes(), bytes(n)):
+            resets += sum(r[3] for r in twopass.scan_wide(p, 4096))
+            for lim in (2 * n + 64, n):
+                assert twopass.compress_wide(p, lim, 4096) == port.compress(p, out_limit=lim)
+    assert resets >= 3
