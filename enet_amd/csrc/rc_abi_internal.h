@@ -58,9 +58,15 @@ typedef struct {
     void     *enc2_wide;
     uint64_t  enc2_wide_cap;  /* bytes */
     uint32_t *enc2_wlist;     /* [n_cap] */
-    /* bucket-history decoder (rc_dec4.hip) in front of the v3 lane decoder; the packets it
-       leaves go to enc2_list / counters[3] (ENET_RC_DEC4=0: off) */
+    /* the fast decoder in front of the v3 lane decoder: 6 = record-light (rc_dec6.hip, default),
+       4 = bucket-history (rc_dec4.hip; ENET_RC_DEC=4), 0 = none (ENET_RC_DEC4=0 or ENET_RC_DEC=0);
+       the packets it leaves go to enc2_list / counters[3] */
     uint32_t  dec4;
+    /* rc_dec6.hip: per packet, the positions the decoder took to start a new bigram (its
+       check, rc_dec6_verify), 0xFFFFFFFF for a packet left to the lane kernels */
+    uint32_t *claims;       /* [n_cap] */
+    uint32_t  dec6_debug;   /* diagnostic (ENET_RC_DEC6_DEBUG): 1 = the check lists every packet */
+    void     *dec6_pool;    /* lane_slots * RC_DEC6_TAB_BYTES: rc_dec6.hip's bucket records */
     /* test switch (ENET_RC_ENC2_SLOW=1): the scan takes its slow paths (every position
        exceptional, every bucket sorted and re-walked) */
     uint32_t  enc2_slow;
@@ -70,6 +76,7 @@ typedef struct {
 } rc_workspace_dev;
 
 #define RC_SMALL_AUTO 0xFFFFFFFFu
+#define RC_DEC6_TAB_BYTES 12288u  /* per lane: 256 buckets x (a 16-B and a 32-B record) */
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */
 #define RC_KERNEL_WAVE 1u   /* one packet per wavefront */
@@ -93,6 +100,11 @@ int rc_hip_enc2_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *
  * regions; packets off its fast path are listed in ws->enc2_list, count in
  * ws->counters[3]. */
 int rc_hip_dec4_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
+
+/* Record-light decoder (rc_dec6.hip) and its check: one packet per lane, model in LDS;
+ * packets off its fast path or failing the check are listed in ws->enc2_list, count in
+ * ws->counters[3]. */
+int rc_hip_dec6_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
 uint32_t rc_hip_lane3_region_bytes(uint32_t max_len);

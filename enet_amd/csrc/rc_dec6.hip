@@ -1,0 +1,490 @@
+// rc_dec6.hip -- record-light range decoder (compress.c:498-627), bit-exact.
+//
+// One packet per lane, like the bucket-history decoder (rc_dec4.hip), whose
+// algebra it shares: position j's order-1 context is x[j-1], its order-2
+// context (x[j-2], x[j-1]); both hold only the positions of bucket x[j-1], and
+// every sub-context statistic is a function of those elements (a = x[j-2],
+// v = x[j], decoded at order 2 or not).  What differs is where the model
+// lives.  dec4 reads and writes a 64-B bucket record in HBM for every byte --
+// one random read-modify-write per byte over a 1-GB table, which is the
+// decoder's bound.  Here the common step touches no model in
+// memory at all:
+//
+//   * per bucket, one LDS byte: t1 (positions that visited order 1) and
+//     r1 = t1 - d1 (those that found their symbol there): the order-1
+//     context's escapes 5 d1 and total 5 d1 + 2 t1 (compress.c:536-568);
+//   * a symbol decoded at the root after escaping order 1 is new to the
+//     order-1 context -- compress.c escapes only past symbols a context
+//     lacks -- so (x[j-1], x[j]) is a new bigram, and position j+1's order-2
+//     context (x[j-1], x[j]) has never been visited: its escapes are 0 and
+//     compress.c skips it (:536-538).  The step after a root-decoded byte
+//     therefore needs nothing but the LDS byte, the root and the coder.
+//
+// Every element also goes, with a blind 2-B store (no read), into the lane's
+// bucket records: a 16-B record per bucket for its first 8 order-1 elements
+// (4 KB per lane, 268 MB for 65536 lanes), a 32-B one for the next 16, touched
+// only by buckets that grow that big.  A random partial write costs about
+// what its footprint costs in the 256-MB Infinity Cache
+// (tools/mb/membench6.hip: 0.77 us per step over 268 MB, 2.2 us over 1 GB).  A step that
+// needs a context's symbols -- order 1 holds the coded symbol (a hit), or the
+// order-2 context exists (the step after a hit) -- stalls its lane.  Every
+// kBlock6 steps the wavefront runs the rare phase for its stalled lanes
+// together: each loads its bucket's records and decodes its step exactly, with
+// dec4's algebra over the unsorted elements (order-2 hits, which leave order
+// 1 alone, are kept in registers).  An earlier version rebuilt the bucket by
+// scanning the packet's decoded output instead: ~40 dependent 16-B loads per
+// rare phase, 7.3 ms for C2 against 1.06 ms for the common steps alone.
+
+// The common step's one assumption -- a root-decoded byte is new to its
+// order-1 context -- holds for every stream compress.c produces, but a
+// corrupt stream can escape past a symbol the context holds.  Each lane
+// therefore counts the positions it took to start a new bigram (the common
+// step's assumptions, and the rare phase's exact findings); the bigrams that
+// really are new are at most as many, with equality iff every assumption
+// held, i.e. iff the decode followed compress.c's model exactly (every
+// context's statistics are functions of which elements it holds).
+// rc_dec6_verify counts the distinct bigrams of every decoded packet and
+// lists those that differ for the lane kernels, which decode them again.
+//
+// Off the fast path (listed for the lane kernels from the start): a bucket
+// with more than 24 order-1 visits or more than 7 order-1 hits (no rescale is
+// possible below that, compress.c:313), more than 4 order-2 hits, the model
+// reset (4094 nodes, compress.c:148-157), root codes past symbol 255 (the
+// exact path), an output that does not fit, or -- once a quarter of the
+// wavefront has left -- the rest of the wavefront (low-entropy batches).
+// tests/proto/lane_host.cpp compiles the per-lane code for the host
+// (tests/test_lane_host.py, variant v6).
+
+#ifndef RC_LANE_HOST_TEST
+#include <hip/hip_runtime.h>
+#else
+#include "lane_host_shim.h"   // tests/proto: host build of the per-lane logic (test only)
+#endif
+#include <stdint.h>
+
+#include "rc_abi_internal.h"
+#include "rc_udiv.h"
+#include "rc_lane_common.h"
+#include "rc_root3.h"
+#include "rc_bucket4.h"
+
+namespace {
+
+#ifndef DEC6_BLOCK
+#define DEC6_BLOCK 16
+#endif
+#ifndef DEC6_RARE_ITERS
+#define DEC6_RARE_ITERS 2
+#endif
+constexpr uint32_t kBlock6 = DEC6_BLOCK;        // common steps between rare phases
+constexpr uint32_t kRareIters6 = DEC6_RARE_ITERS;   // rare steps per phase and lane
+constexpr uint32_t kWaveBail6 = 16;
+constexpr uint32_t kStats6 = kRootStrideDec;     // the LDS bucket bytes follow the root
+constexpr uint32_t kLds6 = kRootStrideDec + 256; // 528 B per lane (33 x 16 B: b128 conflict-free)
+constexpr uint32_t kTab2 = 4096;                 // the second table: 32-B records (elements 8..23)
+constexpr uint32_t kTabCap = 24;                 // order-1 elements a bucket's records hold
+
+// a bucket rebuilt from the history: elements in position order
+struct Hist6 { uint32_t A[8], V[8]; uint32_t p1, hit, k; };
+
+// A 16-B record, read past the vector L1 (agent-scope loads: sc1): the lane
+// appends to its records with stores, and a copy of the line an earlier load
+// left in the L1 would be stale.
+DEV uint4 hload16(uintptr_t a)
+{
+#ifndef RC_LANE_HOST_TEST
+    const uint64_t lo = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a) + 1, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4(static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32), static_cast<uint32_t>(hi),
+                      static_cast<uint32_t>(hi >> 32));
+#else
+    return gload16(a);
+#endif
+}
+
+// byte j of a 32-byte array (a masked OR: see rc_bucket4.h byte_at)
+DEV uint32_t byte_at6(const uint32_t* x, uint32_t j)
+{
+    const uint32_t d = j >> 2;
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 8; ++e) w |= x[e] & (0u - static_cast<uint32_t>(d == e));
+    return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
+// elements whose byte in X equals u (nd wave-uniform live dwords)
+DEV uint32_t eqmask6(const uint32_t* X, uint32_t u, uint32_t nd)
+{
+    const uint32_t ur = u * 0x01010101u;
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 8; ++d)
+        if (d < nd) m |= gather4(eq01(X[d], ur)) << (4 * d);
+    return m;
+}
+
+// elements whose byte in X is below u (u <= 256)
+DEV uint32_t ltmask6(const uint32_t* X, uint32_t u, uint32_t nd)
+{
+    const uint32_t ny = ny_of(u);
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 8; ++d)
+        if (d < nd) m |= (gather4(swar_ge(X[d], ny)) ^ 0xFu) << (4 * d);
+    return m;
+}
+
+// The elements of bucket p from the lane's two tables of 16-B records (the
+// bucket's first 8 and next 8 order-1 elements, appended blind, a | v << 8)
+// and its order-2 hits from the hit list hl[nh] (p | a << 8 | v << 16).
+// Record bytes past t1 are stale (earlier packets): only t1 are taken.
+// Position 1 (no order-2 context) is element 0 of bucket x0.
+DEV void rec_build(const uint8_t* tab, uint32_t p, uint32_t t1, const uint32_t* hl, uint32_t nh, uint32_t x0,
+                   uint32_t n, Hist6& H)
+{
+    const uint4 r1 = hload16(reinterpret_cast<uintptr_t>(tab) + 16 * p);
+    const uint4 r2 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p);
+    const uint4 r3 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p + 16);
+    H.A[0] = bperm(r1.y, r1.x, 0x06040200u); H.V[0] = bperm(r1.y, r1.x, 0x07050301u);
+    H.A[1] = bperm(r1.w, r1.z, 0x06040200u); H.V[1] = bperm(r1.w, r1.z, 0x07050301u);
+    H.A[2] = bperm(r2.y, r2.x, 0x06040200u); H.V[2] = bperm(r2.y, r2.x, 0x07050301u);
+    H.A[3] = bperm(r2.w, r2.z, 0x06040200u); H.V[3] = bperm(r2.w, r2.z, 0x07050301u);
+    H.A[4] = bperm(r3.y, r3.x, 0x06040200u); H.V[4] = bperm(r3.y, r3.x, 0x07050301u);
+    H.A[5] = bperm(r3.w, r3.z, 0x06040200u); H.V[5] = bperm(r3.w, r3.z, 0x07050301u);
+    H.A[6] = 0u; H.V[6] = 0u; H.A[7] = 0u; H.V[7] = 0u;
+    H.p1 = (p == x0 && t1 > 0 && n >= 2) ? 1u : 0u;
+    H.hit = 0u;
+    uint32_t k = t1;
+#pragma unroll
+    for (uint32_t h = 0; h < 4; ++h) {
+        const bool mine = h < nh && (hl[h] & 0xFFu) == p;
+        const uint32_t ks = 8 * (k & 3);
+#pragma unroll
+        for (uint32_t d = 0; d < 8; ++d) {
+            const bool here = mine && (k >> 2) == d;
+            H.A[d] = here ? ((H.A[d] & ~(0xFFu << ks)) | (((hl[h] >> 8) & 0xFFu) << ks)) : H.A[d];
+            H.V[d] = here ? ((H.V[d] & ~(0xFFu << ks)) | (((hl[h] >> 16) & 0xFFu) << ks)) : H.V[d];
+        }
+        H.hit |= mine ? (1u << k) : 0u;
+        k += mine ? 1u : 0u;
+    }
+    H.k = k;
+}
+
+// compress.c:536-568 in a sub-context holding the elements g of H with d
+// distinct values: READ, then an escape (false) or the symbol the code selects
+// (true: v, its interval under/count -- coded by the caller).  fail: the
+// code is past the context's symbols (compress.c:416).
+DEV bool sub_decode6(const Hist6& H, uint32_t nd, uint32_t g, uint32_t t, uint32_t d, bool en, uint32_t& low,
+                     uint32_t& code, uint32_t& range, ByteSrc& in, uint32_t& v, uint32_t& under, uint32_t& count,
+                     bool& fail)
+{
+    const uint32_t esc = kSubEscDelta * d, tot = en ? esc + kSubDelta * t : 1u;
+    const uint32_t r1 = udiv16d(range, tot, rcp64(tot));
+    const uint32_t cd = udiv_lo16(code - low, r1);
+    range = en ? r1 : range;
+    const bool e = en && cd < esc;
+    dec_code(low, code, range, 0u, esc, in, e);
+    const bool hit = en && !e;
+    fail = fail || (hit && cd - esc >= kSubDelta * t);
+    const bool sel = hit && cd - esc < kSubDelta * t;
+    // the element of rank q in value order: the largest u with fewer than q + 1 values below it
+    const uint32_t q = sel ? (cd - esc) >> 1 : 0u;
+    uint32_t u = 0;
+    if (any_lane(sel)) {
+#pragma unroll
+        for (uint32_t s = 128; s >= 1; s >>= 1) {
+            const uint32_t c = popc(g & ltmask6(H.V, u + s, nd));
+            u = c <= q ? u + s : u;
+        }
+        const uint32_t lt = popc(g & ltmask6(H.V, u, nd)), eq = popc(g & eqmask6(H.V, u, nd));
+        under = sel ? esc + kSubDelta * lt : under;
+        count = sel ? kSubDelta * eq : count;
+    }
+    v = sel ? u : v;
+    return sel;
+}
+
+DEV void bail6(const rc_workspace_dev& ws, uint32_t pkt) { bail(ws, pkt); }
+
+DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* root,
+                         uint8_t* stats, uint8_t* tab)
+{
+    const uint32_t len = bt.in_len[pkt];
+    const uint32_t cap = bt.out_cap[pkt];
+    if (len == 0) { bt.out_len[pkt] = 0; ws.claims[pkt] = 0; return; }     // compress.c:513
+    ByteSink o;
+    sink_init(o, bt.out + bt.out_off[pkt], cap);
+    ByteSrc in;
+    src_init(in, bt.in + bt.in_off[pkt], len);
+    Root R;
+    root3_clear<false>(root, R);
+    {
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) reinterpret_cast<uint4*>(stats)[i] = z;
+    }
+    uint32_t rtot = 1 + 256;
+    double rrt = rcp64(rtot);
+    uint32_t low = 0, range = ~0u;
+    uint32_t code = static_cast<uint32_t>(in.la >> 32);            // compress.c:344-350 (0 past the end)
+    in.la <<= 32;
+    in.na -= 4;
+    src_refill(in, true);
+
+    uint32_t order = 0, a = 0, p = 0, nodes = 1, claims = 0, x0 = 0;
+    uint32_t hl[4] = {0u, 0u, 0u, 0u}, nh = 0;   // elements decoded at order 2: p | a << 8 | v << 16
+    bool repeat = false;                      // this step's order-2 context has been visited
+    bool stall = false, done = false, off = false, fail = false;
+
+    for (;;) {
+        // ---------------------------------------------------------- common steps
+        for (uint32_t s = 0; s < kBlock6; ++s) {
+            src_fill(in, true);
+            sink_flush(o);
+            const bool go = !done && !stall;
+            const uint32_t st = (go && order >= 1) ? stats[p] : 0u;
+            const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
+            bool need = go && order >= 2 && repeat;
+            // order 1 (compress.c:536-568): READ; an escape is coded here, a hit stalls the lane
+            const bool o1 = go && !need && order >= 1 && t1 > 0;
+            const uint32_t esc1 = kSubEscDelta * d1, tot1 = o1 ? esc1 + kSubDelta * t1 : 1u;
+            const uint32_t r1 = udiv16d(range, tot1, rcp64(tot1));
+            const uint32_t cd1 = udiv_lo16(code - low, r1);
+            need = need || (o1 && cd1 >= esc1);
+            need = need && !(ws.dec6_debug & 2);      // (timing experiment: no rare steps, output lost)
+            const bool e1 = o1 && cd1 < esc1;
+            range = e1 ? r1 : range;
+            dec_code(low, code, range, 0u, esc1, in, e1);
+            // the root (compress.c:570-596)
+            const bool rg = go && !need;
+            const uint32_t r0 = udiv16d(range, rtot, rrt);
+            const uint32_t cd0 = udiv_lo16(code - low, r0);
+            const bool eos = rg && cd0 < 1;                                // end of stream
+            const bool past = rg && !eos && cd0 - 1 >= rtot - 1;           // past symbol 255: exact path
+            const bool sym = rg && !eos && !past;
+            range = sym ? r0 : range;
+            uint32_t under0 = 0, cnt0 = 0;
+            const uint32_t v = root3_search(root, R, sym ? cd0 - 1 : 0u, under0, cnt0);
+            dec_code_late(low, code, range, 1 + under0, 1 + cnt0, in, sym);
+            if (sym) {
+                root3_add<false>(root, R, v, cnt0);
+                rtot = (rtot + kRootDelta) & 0xFFFF;
+            }
+            if (rare_lane(sym && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit))) {
+                if (sym && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit))
+                    rtot = root3_rescale<false>(root, R);
+            }
+            rrt = sym ? rcp64(rtot) : rrt;
+            // the element joins bucket p: new to its order-2 context (never visited) and,
+            // by the assumption above, to order 1; nodes as compress.c creates them
+            nodes += sym ? (cnt0 == 0 ? 1u : 0u) + (order >= 1 ? 1u : 0u) + (order >= 2 ? 1u : 0u) : 0u;
+            const bool o1v = sym && order >= 1;
+            if (o1v) stats[p] = static_cast<uint8_t>(st + 1);
+            const bool full = o1v && t1 >= kTabCap;
+            // the element into the bucket's records (a blind 2-B store; no read)
+            if (o1v && !full)
+                *GPTR(uint16_t, reinterpret_cast<uintptr_t>(tab) + (t1 < 8 ? 16 * p + 2 * t1 : kTab2 + 32 * p + 2 * (t1 - 8))) =
+                    static_cast<uint16_t>(a | (v << 8));
+            x0 = (sym && order == 0) ? v : x0;
+            const bool fl = sym && o.n >= o.cap;                           // compress.c:617
+            claims += (o1v && !fl) ? 1u : 0u;
+            const bool lv = past || full || (sym && nodes >= kMaxNodes);
+            off = off || lv;
+            fail = fail || fl;
+            done = done || eos || lv || fl;
+            sink_put(o, v, 1, sym && !lv && !fl);
+            a = sym ? p : a;
+            p = sym ? v : p;
+            order += (sym && order < 2) ? 1u : 0u;
+            repeat = sym ? false : repeat;
+            stall = stall || need;
+            src_adv(in);
+        }
+        // ------------------------------------------------------------ rare phase
+        for (uint32_t it = 0; it < kRareIters6 && any_lane(stall && !done); ++it) {
+            const bool rs = stall && !done;
+            src_fill(in, true);
+            sink_flush(o);
+            __builtin_amdgcn_s_waitcnt(0);            // (the blind stores of this lane's records)
+            const uint32_t st = rs && order >= 1 ? stats[p] : 0u;
+            const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
+            Hist6 H;
+            rec_build(tab, p, rs ? t1 : 0u, hl, nh, x0, o.n, H);
+            const bool over = false;
+            uint32_t kmax = H.k;
+#ifndef RC_LANE_HOST_TEST
+            for (int sft = 32; sft >= 1; sft >>= 1) kmax = max(kmax, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmax), sft)));
+#endif
+            const uint32_t nd = min((kmax + 3) >> 2, 8u);
+            const uint32_t km = low_bits(H.k);
+            const uint32_t g2 = (rs && order >= 2) ? (eqmask6(H.A, a, nd) & km & ~H.p1) : 0u;
+            const uint32_t g1 = km & ~H.hit;
+            const uint32_t t2 = popc(g2);
+            // distinct values of the order-2 context (members first of their value)
+            uint32_t d2 = 0;
+            {
+                uint32_t rem = g2;
+                while (any_lane(rem != 0)) {
+                    const uint32_t j = rem ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
+                    const uint32_t same = eqmask6(H.V, byte_at6(H.V, j), nd) & g2 & low_bits(j);
+                    d2 += (rem != 0 && same == 0) ? 1u : 0u;
+                    rem &= rem ? rem - 1u : 0u;
+                }
+            }
+            int at = -1;
+            uint32_t v = 0, hu = 0, hc = 0;
+            bool sf = false;
+            const bool c2 = rs && !over && order >= 2 && t2 > 0;
+            if (any_lane(c2)) {
+                if (sub_decode6(H, nd, g2, t2, d2, c2, low, code, range, in, v, hu, hc, sf)) at = 2;
+            }
+            const bool c1 = rs && !over && !sf && at < 0 && order >= 1 && t1 > 0;
+            if (any_lane(c1)) {
+                if (sub_decode6(H, nd, g1, t1, d1, c1, low, code, range, in, v, hu, hc, sf)) at = 1;
+            }
+            // the root, or the hit's interval
+            const bool rg = rs && !over && !sf && at < 0;
+            const uint32_t r0 = udiv16d(range, rtot, rrt);
+            const uint32_t cd0 = udiv_lo16(code - low, r0);
+            const bool eos = rg && cd0 < 1;
+            const bool past = rg && !eos && cd0 - 1 >= rtot - 1;
+            const bool sym0 = rg && !eos && !past;
+            range = sym0 ? r0 : range;
+            uint32_t under0 = 0, cnt0 = 0;
+            const uint32_t v0 = root3_search(root, R, sym0 ? cd0 - 1 : 0u, under0, cnt0);
+            const bool sym = sym0 || at > 0;
+            v = sym0 ? v0 : v;
+            dec_code(low, code, range, sym0 ? 1 + under0 : hu, sym0 ? 1 + cnt0 : hc, in, sym);
+            if (sym0) {
+                root3_add<false>(root, R, v, cnt0);
+                rtot = (rtot + kRootDelta) & 0xFFFF;
+            }
+            if (rare_lane(sym0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit))) {
+                if (sym0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit))
+                    rtot = root3_rescale<false>(root, R);
+            }
+            rrt = sym0 ? rcp64(rtot) : rrt;
+            // the element joins its contexts (compress.c:598-615)
+            const uint32_t eqv = eqmask6(H.V, v, nd) & km;
+            const bool n2 = order >= 2 && (eqv & g2) == 0;
+            const bool n1 = order >= 1 && at != 2 && (eqv & g1) == 0;
+            const bool nb = eqv == 0;                                       // a new bigram (p, v)
+            nodes += sym ? (sym0 && cnt0 == 0 ? 1u : 0u) + (n2 ? 1u : 0u) + (n1 ? 1u : 0u) : 0u;
+            const bool o1v = sym && order >= 1 && at != 2;
+            const uint32_t nst = st + 1 + (n1 ? 0u : 32u);
+            if (o1v) stats[p] = static_cast<uint8_t>(nst);
+            const bool tfull = o1v && t1 >= kTabCap;
+            if (o1v && !tfull)
+                *GPTR(uint16_t, reinterpret_cast<uintptr_t>(tab) + (t1 < 8 ? 16 * p + 2 * t1 : kTab2 + 32 * p + 2 * (t1 - 8))) =
+                    static_cast<uint16_t>(a | (v << 8));
+            claims += (sym && order >= 1 && nb && o.n < o.cap) ? 1u : 0u;
+            const bool h2 = sym && at == 2;
+            const uint32_t he = p | (a << 8) | (v << 16);
+#pragma unroll
+            for (uint32_t h = 0; h < 4; ++h) hl[h] = (h2 && nh == h) ? he : hl[h];
+            const bool hfull = h2 && nh >= 4;
+            nh += h2 ? 1u : 0u;
+            const bool fl = sym && o.n >= o.cap;
+            const bool lv = over || sf || past || hfull || tfull || (o1v && !n1 && (st >> 5) >= 7) ||
+                            (sym && nodes >= kMaxNodes);
+            off = off || (rs && lv);
+            fail = fail || (rs && fl);
+            done = done || (rs && (eos || lv || fl));
+            sink_put(o, v, 1, sym && !lv && !fl);
+            a = sym ? p : a;
+            p = sym ? v : p;
+            order += (sym && order < 2) ? 1u : 0u;
+            repeat = sym ? !nb : repeat;
+            // the step after a hit has a visited order-2 context: another rare step
+            stall = rs ? (sym && !lv && !fl && order >= 2 && repeat) : stall;
+            src_adv(in);
+        }
+        // once a quarter of the wavefront has left, the rest follow
+        const uint32_t left = static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(off)));
+        if (left >= kWaveBail6) { off = off || !done; done = true; }
+        if (!any_lane(!done)) break;
+    }
+    if (off) { bail6(ws, pkt); ws.claims[pkt] = 0xFFFFFFFFu; return; }
+    // an output that does not fit returns 0 (compress.c:617) once the check has
+    // passed: until then out_len holds the bytes decoded (bit 31 of the claims)
+    sink_finish(o, true);
+    bt.out_len[pkt] = o.n;
+    ws.claims[pkt] = claims | (fail ? 0x80000000u : 0u);
+}
+
+}  // namespace
+
+#ifndef RC_LANE_HOST_TEST
+// one wave per SIMD by design (a packet per lane, 65536 lanes fill the chip)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void rc_decompress_dec6(rc_batch_dev b, rc_workspace_dev ws)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t act = ws.lane_active;
+    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l >= act) return;
+    const uint32_t local = wave * act + l;
+    uint8_t* root = smem + local * kLds6;
+    uint8_t* stats = root + kStats6;
+    const uint32_t per_block = 4 * act;
+    const uint32_t slot = blockIdx.x * per_block + local;
+    uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * RC_DEC6_TAB_BYTES;
+    const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
+    for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
+        const uint32_t pkt = order ? order[i] : i;
+        decompress_one6(b, ws, pkt, root, stats, tab);
+    }
+}
+
+// Counts the distinct bigrams of each packet rc_decompress_dec6 decoded and
+// lists the packets whose count differs from the decoder's (see the header).
+// A wavefront per packet: a 65536-bit set in LDS.
+constexpr uint32_t kVerifyWaves = 4;
+extern "C" __global__ __launch_bounds__(256) void rc_dec6_verify(rc_batch_dev b, rc_workspace_dev ws)
+{
+    __shared__ uint32_t bits[kVerifyWaves][2048];
+    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+    uint32_t* set = bits[wave];
+    for (uint32_t pkt = blockIdx.x * kVerifyWaves + wave; pkt < b.n; pkt += gridDim.x * kVerifyWaves) {
+        const uint32_t cl = ws.claims[pkt];
+        if (cl == 0xFFFFFFFFu) continue;                          // left to the lanes already
+        const uint32_t want = cl & 0x7FFFFFFFu;
+        const uint32_t n = b.out_len[pkt];
+        const uint8_t* x = b.out + b.out_off[pkt];
+#pragma unroll
+        for (uint32_t i = 0; i < 2048 / 64; ++i) set[i * 64 + l] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t j = 1 + l; j < n; j += 64) {
+            const uint32_t bg = (static_cast<uint32_t>(x[j - 1]) << 8) | x[j];
+            atomicOr(&set[bg >> 5], 1u << (bg & 31));
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 2048 / 64; ++i) c += static_cast<uint32_t>(__builtin_popcount(set[i * 64 + l]));
+        for (int s = 32; s >= 1; s >>= 1) c += static_cast<uint32_t>(__shfl_xor(static_cast<int>(c), s));
+        if (l == 0 && (c != want || (ws.dec6_debug & 1))) {
+            const uint32_t k = atomicAdd(&ws.counters[3], 1u);
+            ws.enc2_list[k] = pkt;
+        }
+        if (l == 0 && c == want && !(ws.dec6_debug & 1) && (cl >> 31)) b.out_len[pkt] = 0;     // compress.c:617
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// The decoder over the batch, then the check; packets off its fast path or
+// failing the check are listed in ws->enc2_list, count in ws->counters[3],
+// for the lane kernels.
+extern "C" int rc_hip_dec6_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t blocks, void* stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kLds6;
+    hipLaunchKernelGGL(rc_decompress_dec6, dim3(blocks), dim3(256), lds, st, *b, *ws);
+    const uint32_t vb = (b->n + kVerifyWaves - 1) / kVerifyWaves;
+    hipLaunchKernelGGL(rc_dec6_verify, dim3(vb < 4096 ? vb : 4096), dim3(256), 0, st, *b, *ws);
+    return static_cast<int>(hipGetLastError());
+}
+#endif  // RC_LANE_HOST_TEST

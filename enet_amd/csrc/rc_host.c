@@ -70,12 +70,15 @@ static int ws_reserve(rc_ctx *c, size_t n)
     if (n <= c->ws.n_cap) return 0;
     size_t cap = c->ws.n_cap ? c->ws.n_cap : 1024;
     while (cap < n) cap *= 2;
-    uint32_t *fl = NULL, *ord = NULL, *el = NULL, *wl = NULL;
-    if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) return -1;
-    if (hipMalloc((void **) &ord, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(fl); return -1; }
-    if (hipMalloc((void **) &el, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(fl); hipFree(ord); return -1; }
+    uint32_t *fl = NULL, *ord = NULL, *el = NULL, *wl = NULL, *cl = NULL;
+    if (hipMalloc((void **) &cl, cap * sizeof(uint32_t)) != hipSuccess) return -1;
+    if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(cl); return -1; }
+    if (hipMalloc((void **) &ord, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(cl); hipFree(fl); return -1; }
+    if (hipMalloc((void **) &el, cap * sizeof(uint32_t)) != hipSuccess) {
+        hipFree(cl); hipFree(fl); hipFree(ord); return -1;
+    }
     if (hipMalloc((void **) &wl, cap * sizeof(uint32_t)) != hipSuccess) {
-        hipFree(fl); hipFree(ord); hipFree(el); return -1;
+        hipFree(cl); hipFree(fl); hipFree(ord); hipFree(el); return -1;
     }
     if (c->ws.flag_list) {
         hipDeviceSynchronize();
@@ -83,7 +86,9 @@ static int ws_reserve(rc_ctx *c, size_t n)
         hipFree(c->ws.order);
         hipFree(c->ws.enc2_list);
         hipFree(c->ws.enc2_wlist);
+        hipFree(c->ws.claims);
     }
+    c->ws.claims = cl;
     c->ws.flag_list = fl;
     c->ws.order = ord;
     c->ws.enc2_list = el;
@@ -108,8 +113,12 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     if (region < c->ws.lane_region) region = c->ws.lane_region;
     hipDeviceSynchronize();
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
-    c->ws.lane_pool = NULL; c->ws.lane_slots = 0; c->ws.lane_region = 0;
+    if (c->ws.dec6_pool) hipFree(c->ws.dec6_pool);
+    c->ws.lane_pool = NULL; c->ws.dec6_pool = NULL; c->ws.lane_slots = 0; c->ws.lane_region = 0;
     if (hipMalloc(&c->ws.lane_pool, slots * (size_t) region) != hipSuccess) return -1;
+    /* rc_dec6.hip's bucket records: never cleared (a record's stale bytes past
+       the bucket's element count are never read) */
+    if (hipMalloc(&c->ws.dec6_pool, slots * (size_t) RC_DEC6_TAB_BYTES) != hipSuccess) return -1;
     /* lane regions start at epoch 0: no order-1 record is live (rc_lane3.hip) */
     if (hipMemset(c->ws.lane_pool, 0, slots * (size_t) region) != hipSuccess) return -1;
     /* hipMemset runs on the null stream, which the context's non-blocking
@@ -232,8 +241,15 @@ void *enet_range_coder_create(void)
         c->enc2_wide_on = !(ew && strcmp(ew, "0") == 0);
         c->enc2_stream_max = env_mb_cap("ENET_RC_ENC2_STREAM_MB", ENC2_STREAM_MAX);
         c->enc2_wide_max = env_mb_cap("ENET_RC_ENC2_WIDE_MB", ENC2_WIDE_MAX);
+        /* the fast decoder: rc_dec6.hip unless ENET_RC_DEC=4 (rc_dec4.hip); none with
+           ENET_RC_DEC=0 or ENET_RC_DEC4=0 */
         const char *d4 = getenv("ENET_RC_DEC4");
-        c->ws.dec4 = !(d4 && strcmp(d4, "0") == 0);
+        const char *dk = getenv("ENET_RC_DEC");
+        c->ws.dec4 = 6;
+        if (dk && strcmp(dk, "4") == 0) c->ws.dec4 = 4;
+        if ((dk && strcmp(dk, "0") == 0) || (d4 && strcmp(d4, "0") == 0)) c->ws.dec4 = 0;
+        const char *dd = getenv("ENET_RC_DEC6_DEBUG");
+        c->ws.dec6_debug = dd ? (uint32_t) atoi(dd) : 0u;
         const char *es = getenv("ENET_RC_ENC2_SLOW");
         c->ws.enc2_slow = (es && strcmp(es, "1") == 0) ? 1u : 0u;
         const char *sl = getenv("ENET_RC_SLOTS");
@@ -256,6 +272,8 @@ void enet_range_coder_destroy(void *context)
     if (c->ws.counters) hipFree(c->ws.counters);
     if (c->ws.order) hipFree(c->ws.order);
     if (c->ws.enc2_list) hipFree(c->ws.enc2_list);
+    if (c->ws.claims) hipFree(c->ws.claims);
+    if (c->ws.dec6_pool) hipFree(c->ws.dec6_pool);
     if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
     if (c->ws.enc2_wlist) hipFree(c->ws.enc2_wlist);
     if (c->ws.enc2_wide) hipFree(c->ws.enc2_wide);

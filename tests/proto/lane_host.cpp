@@ -7,6 +7,25 @@
 #ifdef DEC4
 #include "../../enet_amd/csrc/rc_dec4.hip"
 #endif
+#ifdef DEC6
+#include "../../enet_amd/csrc/rc_dec6.hip"
+static uint8_t g_lds6[528] __attribute__((aligned(16)));   // root + bucket bytes
+static uint8_t g_tab6[RC_DEC6_TAB_BYTES] __attribute__((aligned(16)));   // bucket records (never cleared)
+
+// rc_dec6_verify on the host: distinct bigrams of the output
+static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n)
+{
+    static uint8_t seen[65536];
+    memset(seen, 0, sizeof seen);
+    uint32_t c = 0;
+    for (uint32_t j = 1; j < n; ++j) {
+        const uint32_t b = (x[j - 1] << 8) | x[j];
+        c += seen[b] ? 0u : 1u;
+        seen[b] = 1;
+    }
+    return c;
+}
+#endif
 
 #define REGION_BYTES rc_hip_lane3_region_bytes
 #define COMPRESS_ONE compress_one3
@@ -17,6 +36,9 @@ static uint8_t g_mtab[256] __attribute__((aligned(16)));
 static uint8_t g_ldsb[kDenseO2] __attribute__((aligned(16)));   // the lane's LDS dense block
 static bool g_mtab_init = [] { for (uint32_t j = 0; j < 16; ++j) root3_mask_init(g_mtab, j); return true; }();
 #define COMPRESS_ARGS , g_ldsb, g_mtab
+
+static uint32_t g_dec6_unverified = 0;
+extern "C" uint32_t lane_host_dec6_unverified(void) { return g_dec6_unverified; }
 
 extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t cap,
                              uint32_t max_len, uint32_t* out_len)
@@ -29,16 +51,28 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
         memset(region, 0, need);                                   // like the device pool (epoch 0 = unused)
     }
     uint64_t ioff = 0, ooff = 0;
-    uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0}, bails[2] = {0, 0};
+    uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0}, bails[2] = {0, 0}, claims[1] = {0};
     rc_batch_dev b = { in, &ioff, &len, out, &ooff, &cap, out_len, 1, max_len };
     rc_workspace_dev ws = {};
     ws.flag_list = flags; ws.counters = counters; ws.enc2_list = bails; ws.lane_region = need; ws.lane_pool = region; ws.lane_active = 64;
+    ws.claims = claims;
     *out_len = 0xFFFFFFFFu;
 #ifdef DEC4
     // the bucket-history decoder first; a packet it leaves goes to the lanes (as on the GPU)
     if (decompress) {
         uint32_t wbail = 0;
         decompress_one4(b, ws, 0, region, g_root, &wbail);
+        if (!counters[3]) return 0;
+    }
+#endif
+#ifdef DEC6
+    // the record-light decoder and its check; a packet it leaves or that fails the check goes to the lanes
+    if (decompress) {
+        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6);
+        if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
+            counters[3] = 1; g_dec6_unverified++;
+        }
+        if (!counters[3] && (claims[0] >> 31)) *out_len = 0;
         if (!counters[3]) return 0;
     }
 #endif

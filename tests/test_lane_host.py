@@ -17,17 +17,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "tests", "proto", "liblanehost.so")
 
 
-# v3: the lane kernels alone; v4: the bucket-history decoder (rc_dec4.hip) in front of them, as on the GPU
-@pytest.fixture(scope="module", params=["v3", "v4"])
+# v3: the lane kernels alone; v4: the bucket-history decoder (rc_dec4.hip) in front of them;
+# v6: the record-light decoder (rc_dec6.hip) and its check in front of them, as on the GPU
+@pytest.fixture(scope="module", params=["v3", "v4", "v6"])
 def lane(request):
     so = SO.replace("liblanehost", "liblanehost" + request.param[1])
     csrc = os.path.join(ROOT, "enet_amd", "csrc")
     src = [os.path.join(ROOT, "tests", "proto", "lane_host.cpp")] + \
-        [os.path.join(csrc, f) for f in ("rc_lane3.hip", "rc_dec4.hip", "rc_bucket4.h", "rc_lane_common.h",
-                                         "rc_root3.h")]
+        [os.path.join(csrc, f) for f in ("rc_lane3.hip", "rc_dec4.hip", "rc_dec6.hip", "rc_bucket4.h",
+                                         "rc_lane_common.h", "rc_root3.h")]
     if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in src):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared"] +
-                              {"v3": [], "v4": ["-DDEC4"]}[request.param] +
+                              {"v3": [], "v4": ["-DDEC4"], "v6": ["-DDEC6"]}[request.param] +
                               ["-I", csrc, "-I", os.path.join(ROOT, "tests", "proto"), "-o", so, src[0]])
     lib = C.CDLL(so)
     lib.lane_host_run.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
@@ -75,16 +76,16 @@ def test_lane_logic_decompress_fixtures(lane):
         if c["ret"]:
             assert r[1] == c["expect"]
     assert 0 < exact < 2000
-    if lane.version == "v4":     # most fixtures are garbage or low-entropy: those are left to the lanes
+    if lane.version in ("v4", "v6"):     # most fixtures are garbage or low-entropy: those are left to the lanes
         assert 0 < lane.left < len(cases) - 1000, (lane.left, len(cases))
 
 
 def test_dec4_takes_random_packets(lane):
-    """The bucket-history decoder decodes random packets up to MTU size itself
-    (no bucket reaches its 20 elements) and matches the oracle at every
-    output limit edge."""
-    if lane.version != "v4":
-        pytest.skip("dec4 only")
+    """The bucket-history decoder (and the record-light one) decodes random
+    packets up to MTU size itself (no bucket reaches its limits) and matches
+    the oracle at every output limit edge."""
+    if lane.version == "v3":
+        pytest.skip("dec4 / dec6 only")
     from oracle.pyoracle import Coder
     port = Coder("port")
     rng = np.random.default_rng(11)
