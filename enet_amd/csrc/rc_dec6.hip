@@ -83,6 +83,7 @@ constexpr uint32_t kStats6 = kRootStrideDec;     // the LDS bucket bytes follow 
 constexpr uint32_t kLds6 = kRootStrideDec + 256; // 528 B per lane (33 x 16 B: b128 conflict-free)
 constexpr uint32_t kTab2 = 4096;                 // the second table: 32-B records (elements 8..23)
 constexpr uint32_t kTabCap = 24;                 // order-1 elements a bucket's records hold
+constexpr uint32_t kDummy6 = 12288;              // the slot of the stores that record nothing
 
 // a bucket rebuilt from the history: elements in position order
 struct Hist6 { uint32_t A[8], V[8]; uint32_t p1, hit, k; };
@@ -93,10 +94,8 @@ struct Hist6 { uint32_t A[8], V[8]; uint32_t p1, hit, k; };
 DEV uint4 hload16(uintptr_t a)
 {
 #ifndef RC_LANE_HOST_TEST
-    const uint64_t lo = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t hi = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a) + 1, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t lo = __hip_atomic_load(GPTRC(uint64_t, a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(GPTRC(uint64_t, a + 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return make_uint4(static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32), static_cast<uint32_t>(hi),
                       static_cast<uint32_t>(hi >> 32));
 #else
@@ -142,11 +141,21 @@ DEV uint32_t ltmask6(const uint32_t* X, uint32_t u, uint32_t nd)
 // Record bytes past t1 are stale (earlier packets): only t1 are taken.
 // Position 1 (no order-2 context) is element 0 of bucket x0.
 DEV void rec_build(const uint8_t* tab, uint32_t p, uint32_t t1, const uint32_t* hl, uint32_t nh, uint32_t x0,
-                   uint32_t n, Hist6& H)
+                   uint32_t n, bool en, Hist6& H)
 {
-    const uint4 r1 = hload16(reinterpret_cast<uintptr_t>(tab) + 16 * p);
-    const uint4 r2 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p);
-    const uint4 r3 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p + 16);
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    uint4 r1 = z, r2 = z, r3 = z;
+#ifndef DEC6_UNCOND_LOADS
+    if (en) r1 = hload16(reinterpret_cast<uintptr_t>(tab) + 16 * p);
+    if (en && t1 > 8) {
+        r2 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p);
+        r3 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p + 16);
+    }
+#else
+    r1 = hload16(reinterpret_cast<uintptr_t>(tab) + 16 * p);
+    r2 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p);
+    r3 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p + 16);
+#endif
     H.A[0] = bperm(r1.y, r1.x, 0x06040200u); H.V[0] = bperm(r1.y, r1.x, 0x07050301u);
     H.A[1] = bperm(r1.w, r1.z, 0x06040200u); H.V[1] = bperm(r1.w, r1.z, 0x07050301u);
     H.A[2] = bperm(r2.y, r2.x, 0x06040200u); H.V[2] = bperm(r2.y, r2.x, 0x07050301u);
@@ -239,9 +248,16 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     bool repeat = false;                      // this step's order-2 context has been visited
     bool stall = false, done = false, off = false, fail = false;
 
+    PROF_DECL
+    // One loop of common steps; every kBlock6 steps (or once no lane can take
+    // one) the rare phase.  The step's memory operations are unconditional --
+    // a lane that stores no element stores to its dummy slot -- so that the
+    // compiler can wait for an input chunk with vmcnt(n) rather than behind
+    // every store in flight (see rc_lane3.hip lane_prefetch).
+    uint32_t s = 0;
     for (;;) {
-        // ---------------------------------------------------------- common steps
-        for (uint32_t s = 0; s < kBlock6; ++s) {
+        {
+            // ------------------------------------------------------ a common step
             src_fill(in, true);
             sink_flush(o);
             const bool go = !done && !stall;
@@ -285,9 +301,9 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (o1v) stats[p] = static_cast<uint8_t>(st + 1);
             const bool full = o1v && t1 >= kTabCap;
             // the element into the bucket's records (a blind 2-B store; no read)
-            if (o1v && !full)
-                *GPTR(uint16_t, reinterpret_cast<uintptr_t>(tab) + (t1 < 8 ? 16 * p + 2 * t1 : kTab2 + 32 * p + 2 * (t1 - 8))) =
-                    static_cast<uint16_t>(a | (v << 8));
+            *GPTR(uint16_t, reinterpret_cast<uintptr_t>(tab) +
+                            (!(o1v && !full) ? kDummy6 : (t1 < 8 ? 16 * p + 2 * t1 : kTab2 + 32 * p + 2 * (t1 - 8)))) =
+                static_cast<uint16_t>(a | (v << 8));
             x0 = (sym && order == 0) ? v : x0;
             const bool fl = sym && o.n >= o.cap;                           // compress.c:617
             claims += (o1v && !fl) ? 1u : 0u;
@@ -302,21 +318,32 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             repeat = sym ? false : repeat;
             stall = stall || need;
             src_adv(in);
+            PROF(0)
         }
+        ++s;
+        if (s < kBlock6 && any_lane(!done && !stall)) continue;
+        s = 0;
         // ------------------------------------------------------------ rare phase
         for (uint32_t it = 0; it < kRareIters6 && any_lane(stall && !done); ++it) {
             const bool rs = stall && !done;
             src_fill(in, true);
             sink_flush(o);
+#ifndef DEC6_NO_DRAIN
             __builtin_amdgcn_s_waitcnt(0);            // (the blind stores of this lane's records)
+#endif
             const uint32_t st = rs && order >= 1 ? stats[p] : 0u;
             const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
             Hist6 H;
-            rec_build(tab, p, rs ? t1 : 0u, hl, nh, x0, o.n, H);
+            rec_build(tab, p, rs ? t1 : 0u, hl, nh, x0, o.n, rs, H);
             const bool over = false;
             uint32_t kmax = H.k;
 #ifndef RC_LANE_HOST_TEST
             for (int sft = 32; sft >= 1; sft >>= 1) kmax = max(kmax, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmax), sft)));
+#endif
+            PROF(1)
+#ifdef RC_PROFILE
+            prof_acc[8] += 1;
+            prof_acc[9] += static_cast<unsigned long long>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(rs)));
 #endif
             const uint32_t nd = min((kmax + 3) >> 2, 8u);
             const uint32_t km = low_bits(H.k);
@@ -367,6 +394,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
                     rtot = root3_rescale<false>(root, R);
             }
             rrt = sym0 ? rcp64(rtot) : rrt;
+            PROF(2)
             // the element joins its contexts (compress.c:598-615)
             const uint32_t eqv = eqmask6(H.V, v, nd) & km;
             const bool n2 = order >= 2 && (eqv & g2) == 0;
@@ -401,12 +429,18 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             // the step after a hit has a visited order-2 context: another rare step
             stall = rs ? (sym && !lv && !fl && order >= 2 && repeat) : stall;
             src_adv(in);
+            PROF(3)
         }
+        // (nothing of the rare phase left in flight: a record load pending on some
+        // path would make the common step wait for vmcnt(0) before reusing its registers)
+        __builtin_amdgcn_s_waitcnt(0);
         // once a quarter of the wavefront has left, the rest follow
         const uint32_t left = static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(off)));
         if (left >= kWaveBail6) { off = off || !done; done = true; }
+        PROF(4)
         if (!any_lane(!done)) break;
     }
+    PROF_FLUSH(16)
     if (off) { bail6(ws, pkt); ws.claims[pkt] = 0xFFFFFFFFu; return; }
     // an output that does not fit returns 0 (compress.c:617) once the check has
     // passed: until then out_len holds the bytes decoded (bit 31 of the claims)
