@@ -568,8 +568,10 @@ def dominant_kernel(decompress, handed_off=0, n=1):
     if os.environ.get("ENET_RC_KERNEL", "lane3") == "wave":
         return "rc_decompress_wave" if decompress else "rc_compress_wave"
     if decompress:
-        fast = os.environ.get("ENET_RC_DEC4", "1") != "0"
-        return "rc_decompress_dec4" if fast and 2 * handed_off < n else "rc_decompress_lane3"
+        dk = os.environ.get("ENET_RC_DEC", "6")
+        fast = os.environ.get("ENET_RC_DEC4", "1") != "0" and dk != "0"
+        name = "rc_decompress_dec4" if dk == "4" else "rc_decompress_dec6"
+        return name if fast and 2 * handed_off < n else "rc_decompress_lane3"
     if os.environ.get("ENET_RC_ENC2", "1") == "0" or 2 * handed_off >= n:
         return "rc_compress_lane3"
     one = os.environ.get("ENET_RC_ENC2_CODE1") == "1" or os.environ.get("ENET_RC_ENC2_LANES") == "32"

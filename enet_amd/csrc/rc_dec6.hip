@@ -103,16 +103,6 @@ DEV uint4 hload16(uintptr_t a)
 #endif
 }
 
-// byte j of a 32-byte array (a masked OR: see rc_bucket4.h byte_at)
-DEV uint32_t byte_at6(const uint32_t* x, uint32_t j)
-{
-    const uint32_t d = j >> 2;
-    uint32_t w = 0;
-#pragma unroll
-    for (uint32_t e = 0; e < 8; ++e) w |= x[e] & (0u - static_cast<uint32_t>(d == e));
-    return (w >> (8 * (j & 3))) & 0xFFu;
-}
-
 // elements whose byte in X equals u (nd wave-uniform live dwords)
 DEV uint32_t eqmask6(const uint32_t* X, uint32_t u, uint32_t nd)
 {
@@ -121,17 +111,6 @@ DEV uint32_t eqmask6(const uint32_t* X, uint32_t u, uint32_t nd)
 #pragma unroll
     for (uint32_t d = 0; d < 8; ++d)
         if (d < nd) m |= gather4(eq01(X[d], ur)) << (4 * d);
-    return m;
-}
-
-// elements whose byte in X is below u (u <= 256)
-DEV uint32_t ltmask6(const uint32_t* X, uint32_t u, uint32_t nd)
-{
-    const uint32_t ny = ny_of(u);
-    uint32_t m = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 8; ++d)
-        if (d < nd) m |= (gather4(swar_ge(X[d], ny)) ^ 0xFu) << (4 * d);
     return m;
 }
 
@@ -166,6 +145,7 @@ DEV void rec_build(const uint8_t* tab, uint32_t p, uint32_t t1, const uint32_t* 
     H.p1 = (p == x0 && t1 > 0 && n >= 2) ? 1u : 0u;
     H.hit = 0u;
     uint32_t k = t1;
+    if (any_lane(nh > 0))
 #pragma unroll
     for (uint32_t h = 0; h < 4; ++h) {
         const bool mine = h < nh && (hl[h] & 0xFFu) == p;
@@ -182,11 +162,63 @@ DEV void rec_build(const uint8_t* tab, uint32_t p, uint32_t t1, const uint32_t* 
     H.k = k;
 }
 
+// The values of a bucket's elements as bit planes: bit j of pl[b] is bit b of
+// element j's value (nd live dwords).  A select, an equality mask or a count
+// below a value is then 8 steps on 32-bit masks.
+DEV void planes6(const uint32_t* V, uint32_t nd, uint32_t* pl)
+{
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+        uint32_t m = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < 8; ++d)
+            if (d < nd) m |= dot4((V[d] >> b) & 0x01010101u, 0x08040201u, 0u) << (4 * d);
+        pl[b] = m;
+    }
+}
+
+// elements of the 32 whose value is u
+DEV uint32_t peq6(const uint32_t* pl, uint32_t u)
+{
+    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) m &= ((u >> b) & 1u) ? pl[b] : ~pl[b];
+    return m;
+}
+
+// the value of rank q (0-based, by value) among the elements g, bit by bit
+// from the top; lt / eq: the members below it / equal to it
+DEV uint32_t pselect6(const uint32_t* pl, uint32_t g, uint32_t q, uint32_t& lt, uint32_t& eq)
+{
+    uint32_t cand = g, below = 0, u = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const uint32_t zeros = cand & ~pl[b];
+        const uint32_t nz = popc(zeros);
+        const bool one = q >= below + nz;
+        below += one ? nz : 0u;
+        cand = one ? (cand & pl[b]) : zeros;
+        u |= one ? (1u << b) : 0u;
+    }
+    lt = below;
+    eq = popc(cand);
+    return u;
+}
+
+// the value of element j
+DEV uint32_t pval6(const uint32_t* pl, uint32_t j)
+{
+    uint32_t u = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) u |= ((pl[b] >> j) & 1u) << b;
+    return u;
+}
+
 // compress.c:536-568 in a sub-context holding the elements g of H with d
 // distinct values: READ, then an escape (false) or the symbol the code selects
 // (true: v, its interval under/count -- coded by the caller).  fail: the
 // code is past the context's symbols (compress.c:416).
-DEV bool sub_decode6(const Hist6& H, uint32_t nd, uint32_t g, uint32_t t, uint32_t d, bool en, uint32_t& low,
+DEV bool sub_decode6(const uint32_t* pl, uint32_t g, uint32_t t, uint32_t d, bool en, uint32_t& low,
                      uint32_t& code, uint32_t& range, ByteSrc& in, uint32_t& v, uint32_t& under, uint32_t& count,
                      bool& fail)
 {
@@ -199,20 +231,14 @@ DEV bool sub_decode6(const Hist6& H, uint32_t nd, uint32_t g, uint32_t t, uint32
     const bool hit = en && !e;
     fail = fail || (hit && cd - esc >= kSubDelta * t);
     const bool sel = hit && cd - esc < kSubDelta * t;
-    // the element of rank q in value order: the largest u with fewer than q + 1 values below it
-    const uint32_t q = sel ? (cd - esc) >> 1 : 0u;
-    uint32_t u = 0;
+    // the member of rank q in value order: its value, and the members below it / equal to it
     if (any_lane(sel)) {
-#pragma unroll
-        for (uint32_t s = 128; s >= 1; s >>= 1) {
-            const uint32_t c = popc(g & ltmask6(H.V, u + s, nd));
-            u = c <= q ? u + s : u;
-        }
-        const uint32_t lt = popc(g & ltmask6(H.V, u, nd)), eq = popc(g & eqmask6(H.V, u, nd));
+        uint32_t lt, eq;
+        const uint32_t u = pselect6(pl, g, sel ? (cd - esc) >> 1 : 0u, lt, eq);
         under = sel ? esc + kSubDelta * lt : under;
         count = sel ? kSubDelta * eq : count;
+        v = sel ? u : v;
     }
-    v = sel ? u : v;
     return sel;
 }
 
@@ -255,13 +281,20 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     // compiler can wait for an input chunk with vmcnt(n) rather than behind
     // every store in flight (see rc_lane3.hip lane_prefetch).
     uint32_t s = 0;
+#ifdef DEC6_STATS_PREFETCH
+    uint32_t stn = 0;
+#endif
     for (;;) {
         {
             // ------------------------------------------------------ a common step
             src_fill(in, true);
             sink_flush(o);
             const bool go = !done && !stall;
+#ifdef DEC6_STATS_PREFETCH
+            const uint32_t st = (go && order >= 1) ? stn : 0u;
+#else
             const uint32_t st = (go && order >= 1) ? stats[p] : 0u;
+#endif
             const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
             bool need = go && order >= 2 && repeat;
             // order 1 (compress.c:536-568): READ; an escape is coded here, a hit stalls the lane
@@ -317,8 +350,12 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             order += (sym && order < 2) ? 1u : 0u;
             repeat = sym ? false : repeat;
             stall = stall || need;
-            src_adv(in);
+#ifdef DEC6_STATS_PREFETCH
+            stn = stats[p];                           // (the next step's bucket byte, read ahead)
+#endif
             PROF(0)
+            src_adv(in);
+            PROF(5)
         }
         ++s;
         if (s < kBlock6 && any_lane(!done && !stall)) continue;
@@ -336,16 +373,16 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             Hist6 H;
             rec_build(tab, p, rs ? t1 : 0u, hl, nh, x0, o.n, rs, H);
             const bool over = false;
-            uint32_t kmax = H.k;
-#ifndef RC_LANE_HOST_TEST
-            for (int sft = 32; sft >= 1; sft >>= 1) kmax = max(kmax, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmax), sft)));
-#endif
             PROF(1)
 #ifdef RC_PROFILE
             prof_acc[8] += 1;
             prof_acc[9] += static_cast<unsigned long long>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(rs)));
 #endif
-            const uint32_t nd = min((kmax + 3) >> 2, 8u);
+            uint32_t nd = 1;                          // live dwords of the element arrays, wave-wide
+#pragma unroll
+            for (uint32_t j = 1; j < 8; ++j) nd += any_lane(H.k > 4 * j) ? 1u : 0u;
+            uint32_t pl[8];
+            planes6(H.V, nd, pl);
             const uint32_t km = low_bits(H.k);
             const uint32_t g2 = (rs && order >= 2) ? (eqmask6(H.A, a, nd) & km & ~H.p1) : 0u;
             const uint32_t g1 = km & ~H.hit;
@@ -356,7 +393,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
                 uint32_t rem = g2;
                 while (any_lane(rem != 0)) {
                     const uint32_t j = rem ? static_cast<uint32_t>(__builtin_ctz(rem)) : 0u;
-                    const uint32_t same = eqmask6(H.V, byte_at6(H.V, j), nd) & g2 & low_bits(j);
+                    const uint32_t same = peq6(pl, pval6(pl, j)) & g2 & low_bits(j);
                     d2 += (rem != 0 && same == 0) ? 1u : 0u;
                     rem &= rem ? rem - 1u : 0u;
                 }
@@ -366,11 +403,11 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             bool sf = false;
             const bool c2 = rs && !over && order >= 2 && t2 > 0;
             if (any_lane(c2)) {
-                if (sub_decode6(H, nd, g2, t2, d2, c2, low, code, range, in, v, hu, hc, sf)) at = 2;
+                if (sub_decode6(pl, g2, t2, d2, c2, low, code, range, in, v, hu, hc, sf)) at = 2;
             }
             const bool c1 = rs && !over && !sf && at < 0 && order >= 1 && t1 > 0;
             if (any_lane(c1)) {
-                if (sub_decode6(H, nd, g1, t1, d1, c1, low, code, range, in, v, hu, hc, sf)) at = 1;
+                if (sub_decode6(pl, g1, t1, d1, c1, low, code, range, in, v, hu, hc, sf)) at = 1;
             }
             // the root, or the hit's interval
             const bool rg = rs && !over && !sf && at < 0;
@@ -396,7 +433,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             rrt = sym0 ? rcp64(rtot) : rrt;
             PROF(2)
             // the element joins its contexts (compress.c:598-615)
-            const uint32_t eqv = eqmask6(H.V, v, nd) & km;
+            const uint32_t eqv = peq6(pl, v) & km;
             const bool n2 = order >= 2 && (eqv & g2) == 0;
             const bool n1 = order >= 1 && at != 2 && (eqv & g1) == 0;
             const bool nb = eqv == 0;                                       // a new bigram (p, v)
@@ -434,6 +471,9 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // (nothing of the rare phase left in flight: a record load pending on some
         // path would make the common step wait for vmcnt(0) before reusing its registers)
         __builtin_amdgcn_s_waitcnt(0);
+#ifdef DEC6_STATS_PREFETCH
+        stn = stats[p];
+#endif
         // once a quarter of the wavefront has left, the rest follow
         const uint32_t left = static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(off)));
         if (left >= kWaveBail6) { off = off || !done; done = true; }

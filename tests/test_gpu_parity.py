@@ -18,9 +18,11 @@ torch = pytest.importorskip("torch")
 
 
 VARIANTS = {
-    # default: two-pass encoder (rc_enc2.hip) and bucket-history decoder
-    # (rc_dec4.hip) in front of the v3 lane kernels (rc_lane3.hip)
+    # default: two-pass encoder (rc_enc2.hip) and record-light decoder with its
+    # check (rc_dec6.hip) in front of the v3 lane kernels (rc_lane3.hip)
     "lane3": {"ENET_RC_KERNEL": "lane3"},
+    # the bucket-history decoder (rc_dec4.hip) in front of the lane kernels instead
+    "dec4": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "4"},
     # the two-pass encoder's slow paths forced (every position exceptional,
     # every bucket sorted and re-walked: what a device without lane-ordered
     # LDS atomics would take)
@@ -300,6 +302,32 @@ def test_random_fuzz_vs_oracle(coder):
     for g, r in zip(garbage, res):
         e = port.decompress(g, 2048)
         assert r[0] == e[0] and (e[0] == 0 or r[1] == e[1])
+
+
+def test_corrupted_streams_vs_oracle(coder):
+    """Valid streams of random packets with a few bytes flipped: the decode
+    stays on the record-light decoder's common steps for a while, then
+    escapes past symbols its contexts hold (compress.c:606-610), which only
+    its bigram-count check (rc_dec6_verify) can tell.  Every result, the
+    packets the check sent to the lane kernels included, matches the oracle."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(29)
+    streams = []
+    for _ in range(3000):
+        n = int(rng.integers(200, 1300))
+        p = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        r, c = port.compress(p, 2 * n + 64)
+        b = bytearray(c)
+        for _ in range(int(rng.integers(1, 4))):
+            j = int(rng.integers(len(b) // 4, len(b)))
+            b[j] ^= 1 << int(rng.integers(0, 8))
+        streams.append(bytes(b))
+    caps = [int(rng.choice([1400, 4096])) for _ in streams]
+    res = _run(coder, True, streams, caps)
+    bad = [i for i, (g, c, r) in enumerate(zip(streams, caps, res))
+           if (lambda e: r[0] != e[0] or (e[0] and r[1] != e[1]))(port.decompress(g, c))]
+    assert not bad, bad[:10]
 
 
 @pytest.fixture(scope="module")

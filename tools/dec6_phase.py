@@ -22,8 +22,8 @@ import torch  # noqa: E402
 
 from enet_amd import RangeCoder, compress_batch, decompress_batch, get_lib, synth  # noqa: E402
 
-NAMES = {0: "common steps", 1: "rare: drain + record loads", 2: "rare: decode", 3: "rare: update, output",
-         4: "wave bail check"}
+NAMES = {0: "common steps", 5: "common: input advance (src_adv)", 1: "rare: drain + record loads",
+         2: "rare: decode", 3: "rare: update, output", 4: "wave bail check"}
 
 
 def main():
