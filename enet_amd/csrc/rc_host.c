@@ -543,13 +543,25 @@ static int pack_reserve(rc_ctx *c, size_t bytes, size_t blocks)
 /* Page-locks [p, p + bytes) for direct DMA (hipHostRegister: ~0.35 ms for
  * 80 MB the first time, microseconds after), so that a host batch skips the
  * copy through pinned staging.  1: registered here (host_unpin after the
- * transfers), 0: not usable (already registered by someone else, or the call
- * failed) -- the staging path then. */
+ * transfers), 2: the caller's memory is page-locked already (its own
+ * hipHostMalloc / hipHostRegister, e.g. a long-lived receive buffer): DMA'd
+ * directly, left registered; 0: not usable (the call failed) -- the staging
+ * path then. */
 static int host_pin(const void *p, size_t bytes)
 {
     static int off = -1;
     if (off < 0) off = getenv("ENET_RC_NO_HOST_PIN") != NULL;
     if (off || bytes < (1u << 20)) return 0;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost) {
+        /* page-locked by the caller: usable if the whole range is */
+        hipPointerAttribute_t ae;
+        if (hipPointerGetAttributes(&ae, (const uint8_t *) p + bytes - 1) == hipSuccess &&
+            ae.type == hipMemoryTypeHost)
+            return 2;
+        return 0;
+    }
+    (void) hipGetLastError();
     const uintptr_t a = (uintptr_t) p & ~(uintptr_t) 4095, e = ((uintptr_t) p + bytes + 4095) & ~(uintptr_t) 4095;
     if (hipHostRegister((void *) a, e - a, hipHostRegisterDefault) == hipSuccess) return 1;
     (void) hipGetLastError();
