@@ -515,36 +515,57 @@ void rc_decompress_dec6(rc_batch_dev b, rc_workspace_dev ws)
 
 // Counts the distinct bigrams of each packet rc_decompress_dec6 decoded and
 // lists the packets whose count differs from the decoder's (see the header).
-// A wavefront per packet: a 65536-bit set in LDS.
+// A wavefront per packet: a 65536-bit set in LDS; each lane takes an aligned
+// 16-B chunk of the output per round (and the byte before it), sets the bits
+// of its positions' bigrams, and the set's population is the count.
 constexpr uint32_t kVerifyWaves = 4;
 extern "C" __global__ __launch_bounds__(256) void rc_dec6_verify(rc_batch_dev b, rc_workspace_dev ws)
 {
-    __shared__ uint32_t bits[kVerifyWaves][2048];
+    __shared__ uint4 bits[kVerifyWaves][512];
     const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-    uint32_t* set = bits[wave];
+    uint4* set4 = bits[wave];
+    uint32_t* set = reinterpret_cast<uint32_t*>(set4);
     for (uint32_t pkt = blockIdx.x * kVerifyWaves + wave; pkt < b.n; pkt += gridDim.x * kVerifyWaves) {
         const uint32_t cl = ws.claims[pkt];
         if (cl == 0xFFFFFFFFu) continue;                          // left to the lanes already
         const uint32_t want = cl & 0x7FFFFFFFu;
         const uint32_t n = b.out_len[pkt];
-        const uint8_t* x = b.out + b.out_off[pkt];
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(b.out + b.out_off[pkt]);
+        const uintptr_t base = lo & ~static_cast<uintptr_t>(15);
 #pragma unroll
-        for (uint32_t i = 0; i < 2048 / 64; ++i) set[i * 64 + l] = 0u;
+        for (uint32_t i = 0; i < 512 / 64; ++i) set4[i * 64 + l] = make_uint4(0u, 0u, 0u, 0u);
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t j = 1 + l; j < n; j += 64) {
-            const uint32_t bg = (static_cast<uint32_t>(x[j - 1]) << 8) | x[j];
-            atomicOr(&set[bg >> 5], 1u << (bg & 31));
+        const uint32_t chunks = n > 1 ? static_cast<uint32_t>((lo + n - base + 15) >> 4) : 0u;
+        for (uint32_t c = l; c < chunks; c += 64) {
+            const uintptr_t a = base + 16 * c;
+            const uint4 w = *reinterpret_cast<const uint4*>(a);
+            uint32_t prev = a > lo ? *reinterpret_cast<const uint8_t*>(a - 1) : 0u;
+            const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (uint32_t t = 0; t < 16; ++t) {
+                const uint32_t x = (d[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                const uintptr_t at = a + t;                   // position at - lo
+                if (at > lo && at < lo + n) {
+                    const uint32_t bg = (prev << 8) | x;
+                    atomicOr(&set[bg >> 5], 1u << (bg & 31));
+                }
+                prev = x;
+            }
         }
         __builtin_amdgcn_wave_barrier();
-        uint32_t c = 0;
+        uint32_t cnt = 0;
 #pragma unroll
-        for (uint32_t i = 0; i < 2048 / 64; ++i) c += static_cast<uint32_t>(__builtin_popcount(set[i * 64 + l]));
-        for (int s = 32; s >= 1; s >>= 1) c += static_cast<uint32_t>(__shfl_xor(static_cast<int>(c), s));
-        if (l == 0 && (c != want || (ws.dec6_debug & 1))) {
+        for (uint32_t i = 0; i < 512 / 64; ++i) {
+            const uint4 q = set4[i * 64 + l];
+            cnt += static_cast<uint32_t>(__builtin_popcount(q.x) + __builtin_popcount(q.y) +
+                                         __builtin_popcount(q.z) + __builtin_popcount(q.w));
+        }
+        for (int sft = 32; sft >= 1; sft >>= 1) cnt += static_cast<uint32_t>(__shfl_xor(static_cast<int>(cnt), sft));
+        if (l == 0 && (cnt != want || (ws.dec6_debug & 1))) {
             const uint32_t k = atomicAdd(&ws.counters[3], 1u);
             ws.enc2_list[k] = pkt;
         }
-        if (l == 0 && c == want && !(ws.dec6_debug & 1) && (cl >> 31)) b.out_len[pkt] = 0;     // compress.c:617
+        if (l == 0 && cnt == want && !(ws.dec6_debug & 1) && (cl >> 31)) b.out_len[pkt] = 0;     // compress.c:617
         __builtin_amdgcn_wave_barrier();
     }
 }
