@@ -7,9 +7,9 @@
  * below have exactly the reference signatures and return conventions, so
  * host.c / protocol.c call them unchanged.  The batch entry points are new:
  * they are how the GPU is meant to be used: large batches run one packet
- * per lane (the two-pass encoder and the bucket-history decoder, then the
- * lane kernels for what they leave), batches that fit on the chip at one
- * wavefront per packet run on the wavefront-per-packet kernels.
+ * per lane (the two-pass encoder and the record-light decoder with its
+ * check, then the lane kernels for what they leave), batches that fit on the
+ * chip at one wavefront per packet run on the wavefront-per-packet kernels.
  *
  * Plain C, plain pointers and sizes; no HIP or torch types appear here
  * (streams are passed as void*).
@@ -251,7 +251,7 @@ int enet_rc_pack_batch_device(void *context, const uint8_t *out, const uint64_t 
 /* Number of packets of the last batch that took the exact (binary-tree) path. */
 uint32_t enet_rc_last_exact_count(void *context);
 /* Number of packets of the last batch that the first pass (the two-pass
- * encoder, or the bucket-history decoder) left to the lane kernels. */
+ * encoder, or the record-light decoder and its check) left to the lane kernels. */
 uint32_t enet_rc_last_lane_count(void *context);
 /* Library version string. */
 const char *enet_rc_version(void);
