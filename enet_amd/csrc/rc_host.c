@@ -398,8 +398,21 @@ static void *copy_worker(void *p)
     return NULL;
 }
 
-#define COPY_THREADS 8
+#define COPY_THREADS_MAX 16
 #define COPY_MIN_BYTES (4u << 20)
+
+/* Threads of the host copies (ENET_RC_COPY_THREADS, 1..16; default 8) */
+static int copy_threads(void)
+{
+    static int k = 0;
+    if (k == 0) {
+        const char *e = getenv("ENET_RC_COPY_THREADS");
+        int v = e ? atoi(e) : 8;
+        k = v < 1 ? 1 : (v > COPY_THREADS_MAX ? COPY_THREADS_MAX : v);
+    }
+    return k;
+}
+#define COPY_THREADS (copy_threads())
 
 /* A persistent pool of COPY_THREADS - 1 workers (created on first use):
  * creating threads per copy group cost ~1-3 ms per host batch.  One caller
@@ -475,7 +488,7 @@ static void par_run(copy_job *jobs, int k)
 static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
 {
     int k = bytes >= COPY_MIN_BYTES ? COPY_THREADS : 1;
-    copy_job jobs[COPY_THREADS];
+    copy_job jobs[COPY_THREADS_MAX];
     size_t per = (bytes + k - 1) / k;
     for (int i = 0; i < k; ++i) {
         size_t lo = (size_t) i * per, hi = lo + per < bytes ? lo + per : bytes;
@@ -490,7 +503,7 @@ static void par_scatter(uint8_t *out, const uint64_t *out_off, const uint8_t *pa
                         const uint32_t *len, size_t lo, size_t hi, uint64_t bytes)
 {
     int k = bytes >= COPY_MIN_BYTES ? COPY_THREADS : 1;
-    copy_job jobs[COPY_THREADS];
+    copy_job jobs[COPY_THREADS_MAX];
     const size_t n = hi - lo, per = (n + k - 1) / k;
     for (int i = 0; i < k; ++i) {
         jobs[i].kind = 1;
@@ -506,7 +519,7 @@ static void par_gather(uint8_t *dst, const uint64_t *poff, const ENetBuffer *gbu
                        size_t lo, size_t hi, uint64_t bytes)
 {
     int k = bytes >= COPY_MIN_BYTES ? COPY_THREADS : 1;
-    copy_job jobs[COPY_THREADS];
+    copy_job jobs[COPY_THREADS_MAX];
     const size_t n = hi - lo, per = (n + k - 1) / k;
     for (int i = 0; i < k; ++i) {
         jobs[i].kind = 2;
