@@ -301,10 +301,20 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const bool o1 = go && !need && order >= 1 && t1 > 0;
             const uint32_t esc1 = kSubEscDelta * d1, tot1 = o1 ? esc1 + kSubDelta * t1 : 1u;
             const uint32_t r1 = udiv16d(range, tot1, rcp64(tot1));
+#ifndef DEC6_READ1
+            // READ < escapes without the READ's division: (code - low) / r1 < esc1
+            // iff code - low < esc1 r1 (the quotient is then below 2^16: no
+            // truncation, compress.c:352); otherwise a hit -- or, on a corrupt
+            // stream, a quotient truncated to 16 bits -- both for the rare step,
+            // which READs in full
+            const bool e1 = o1 && code - low < esc1 * r1;
+            need = need || (o1 && !e1);
+#else
             const uint32_t cd1 = udiv_lo16(code - low, r1);
             need = need || (o1 && cd1 >= esc1);
-            need = need && !(ws.dec6_debug & 2);      // (timing experiment: no rare steps, output lost)
             const bool e1 = o1 && cd1 < esc1;
+#endif
+            need = need && !(ws.dec6_debug & 2);      // (timing experiment: no rare steps, output lost)
             range = e1 ? r1 : range;
             dec_code(low, code, range, 0u, esc1, in, e1);
             // the root (compress.c:570-596)
