@@ -283,6 +283,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     uint32_t s = 0;
 #ifdef DEC6_STATS_PREFETCH
     uint32_t stn = 0;
+    double rtn = 1.0;                         // 1 / the order-1 total of the next step's bucket
 #endif
     for (;;) {
         {
@@ -300,7 +301,11 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             // order 1 (compress.c:536-568): READ; an escape is coded here, a hit stalls the lane
             const bool o1 = go && !need && order >= 1 && t1 > 0;
             const uint32_t esc1 = kSubEscDelta * d1, tot1 = o1 ? esc1 + kSubDelta * t1 : 1u;
+#ifdef DEC6_STATS_PREFETCH
+            const uint32_t r1 = udiv16d(range, tot1, o1 ? rtn : 1.0);
+#else
             const uint32_t r1 = udiv16d(range, tot1, rcp64(tot1));
+#endif
 #ifndef DEC6_READ1
             // READ < escapes without the READ's division: (code - low) / r1 < esc1
             // iff code - low < esc1 r1 (the quotient is then below 2^16: no
@@ -362,6 +367,10 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             stall = stall || need;
 #ifdef DEC6_STATS_PREFETCH
             stn = stats[p];                           // (the next step's bucket byte, read ahead)
+            {
+                const uint32_t nt = stn & 31u, nd1 = nt - (stn >> 5);
+                rtn = rcp64(max(kSubEscDelta * nd1 + kSubDelta * nt, 1u));
+            }
 #endif
             PROF(0)
             src_adv(in);
@@ -483,6 +492,10 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         __builtin_amdgcn_s_waitcnt(0);
 #ifdef DEC6_STATS_PREFETCH
         stn = stats[p];
+        {
+            const uint32_t nt = stn & 31u, nd1 = nt - (stn >> 5);
+            rtn = rcp64(max(kSubEscDelta * nd1 + kSubDelta * nt, 1u));
+        }
 #endif
         // once a quarter of the wavefront has left, the rest follow
         const uint32_t left = static_cast<uint32_t>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(off)));
