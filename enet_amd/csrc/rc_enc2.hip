@@ -1260,17 +1260,22 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
 
 constexpr uint32_t kWideDense = 32;             // runs longer than this take a dense walk
 
-struct WScanLds {
+// L: the longest packet of the launch (its positions); two sizes are built,
+// 2048 and 1216 -- the smaller one leaves room for 9 wavefronts per CU
+// instead of 6 (the scan is latency-bound: LDS and ballots)
+template <uint32_t L>
+struct WScanLdsT {
     uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i]; then a big bucket's run sizes / starts
     uint32_t cnt[256];                // bucket sizes, then fill pointers
     uint32_t start[256];              // bucket starts (4-aligned)
-    uint32_t e[2048 + 768];           // elements in bucket order (element word as in pass 1)
-    uint32_t sw[2048];                // a big bucket's element words by a, then its order-1 visits
+    uint32_t e[L + 768];              // elements in bucket order (element word as in pass 1)
+    uint32_t sw[L];                   // a big bucket's element words by a, then its order-1 visits
     uint32_t f2bits[64];              // positions found at order 2 (big buckets)
     uint32_t tab[64];                 // dense walk: a round's updated counts (256 bytes); rank counts
     uint32_t runs[64];                // a big bucket's long runs (a keys)
     uint32_t nruns;
 };
+constexpr uint32_t kWideSmallL = 1216;
 
 DEV uint32_t lane_id() { return threadIdx.x & 63; }
 DEV uint64_t below_mask() { return (1ull << lane_id()) - 1ull; }
@@ -1367,7 +1372,8 @@ DEV uint32_t akey_of(uint32_t w) { return (w & (256u << 19)) ? (w >> 19) & 511 :
 //   order 1 (not found2): the bucket's lanes not found2, likewise.
 // found2 of every lane is known at once (an earlier lane with the same a and
 // v), so nothing runs lane after lane.
-DEV void wide_small_buckets(WScanLds& s, uint32_t q0, uint32_t total, uint2* wrec)
+template <class S>
+DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
 {
     const uint32_t t = lane_id();
     const uint64_t below = below_mask();
@@ -1436,7 +1442,8 @@ DEV void wide_small_buckets(WScanLds& s, uint32_t q0, uint32_t total, uint2* wre
 // windows of whole runs over their sorted words sw[0, ks) (short runs first),
 // counted over lanes as in wide_small_buckets: record half A, and the
 // position's order-2 hit bit.
-DEV void wide_short_runs(WScanLds& s, uint32_t ks, const uint32_t* hist, const uint32_t* rend, uint2* wrec)
+template <class S>
+DEV void wide_short_runs(S& s, uint32_t ks, const uint32_t* hist, const uint32_t* rend, uint2* wrec)
 {
     const uint32_t t = lane_id();
     const uint64_t below = below_mask();
@@ -1485,7 +1492,8 @@ DEV uint32_t nonzero_bytes(uint32_t x)
 // owning lane (ds_bpermute).  order2: record half A, a hit sets the
 // position's order-2 hit bit and closes half B; else half B with the root
 // flag.
-DEV void wide_dense_walk(WScanLds& s, const uint32_t* list, uint32_t m, bool order2, uint2* wrec)
+template <class S>
+DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, uint2* wrec)
 {
     const uint32_t t = lane_id();
     uint8_t* sc = reinterpret_cast<uint8_t*>(s.tab);   // a round's final counts of its symbols (0: untouched)
@@ -1569,7 +1577,8 @@ DEV void wide_dense_walk(WScanLds& s, const uint32_t* list, uint32_t m, bool ord
 
 // a big bucket of a wide packet (> kE2Bucket elements, [bs, bs + k) in
 // position order), the whole wavefront
-DEV void wide_big_bucket(WScanLds& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp)
+template <class S>
+DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp)
 {
     const uint32_t t = lane_id();
     uint32_t* hist = reinterpret_cast<uint32_t*>(s.x);          // [256] run sizes by a
@@ -1682,10 +1691,9 @@ DEV WPf wide_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t q, uint
     return f;
 }
 
-extern "C" __global__ __launch_bounds__(kScanThreads)
-void rc_enc2_wscan(rc_batch_dev b, E2Params e)
+template <uint32_t L>
+DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
 {
-    __shared__ __attribute__((aligned(16))) WScanLds s;
     const uint32_t t = threadIdx.x;
     const uint32_t nw = min(*e.wcount, e.wcap);
     W2Prof wp;
@@ -1781,6 +1789,21 @@ void rc_enc2_wscan(rc_batch_dev b, E2Params e)
         W2P(10)
     }
     W2P_FLUSH
+}
+
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_wscan(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) WScanLdsT<2048> s;
+    wscan_main<2048>(b, e, s);
+}
+
+// the same for launches whose packets are at most kWideSmallL bytes
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_wscan_s(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) WScanLdsT<kWideSmallL> s;
+    wscan_main<kWideSmallL>(b, e, s);
 }
 
 // ---- wide code pass: rc_enc2_code over explicit records
@@ -1974,8 +1997,12 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         else
             hipLaunchKernelGGL(rc_enc2_code2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
         if (e.wide) {
-            hipLaunchKernelGGL(rc_enc2_wscan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
-                               0, st, *b, e);
+            if (e.slot_len <= kWideSmallL)
+                hipLaunchKernelGGL(rc_enc2_wscan_s, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max),
+                                   dim3(kScanThreads), 0, st, *b, e);
+            else
+                hipLaunchKernelGGL(rc_enc2_wscan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max),
+                                   dim3(kScanThreads), 0, st, *b, e);
             hipLaunchKernelGGL(rc_enc2_wcode, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
         }
     }
