@@ -123,7 +123,6 @@ struct E2Params {
 
 // the last element slot: buckets of 1918 positions, each padded to 4, end
 // below it (1918 + 3 * 255 < 2815); lanes past a packet's end write there
-constexpr uint32_t kScanDummyE = 2048 + 768 - 1;
 
 DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 {
@@ -132,13 +131,19 @@ DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 
 // ------------------------------------------------------------------ pass 1
 
-struct ScanLds {
+// L: the longest packet of the launch (as WScanLdsT below): with 1216 the
+// element array fits the bigram set's space (14 KB instead of 17 KB per
+// wavefront)
+constexpr uint32_t kWideSmallL = 1216;     // the smaller LDS layouts: packets up to this many bytes
+template <uint32_t L>
+struct ScanLdsT {
+    static constexpr uint32_t kDummyE = L + 768 - 1;   // element slot of lanes past the packet
     uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i] (128 chunks of 16 B)
     uint32_t cnt[256];                // bucket sizes, then fill pointers
     uint32_t start[256];              // bucket starts (4-aligned)
     union {
         uint32_t seen[2048];          // bigrams (x[i-1], x[i]) seen, 64 Ki bits
-        uint32_t e[2048 + 768];       // elements in bucket order (below), buckets 4-aligned
+        uint32_t e[L + 768];          // elements in bucket order (below), buckets 4-aligned
     };
     uint32_t excm[64];                // exceptional positions: i or i - 1 repeats an earlier bigram (2048 bits)
     uint32_t probe[16];               // lane-order probe (rc_enc2_scan)
@@ -206,7 +211,8 @@ DEV void wave_sync()
 // global atomic per 32 packets instead of one per packet (a batch of low-
 // entropy packets sends every packet there, and atomics on one address
 // serialise).
-DEV void fb_flush(ScanLds& s, const E2Params& e, uint32_t t)
+template <class S>
+DEV void fb_flush(S& s, const E2Params& e, uint32_t t)
 {
     wave_sync();
     const uint32_t k = s.nfb;
@@ -220,7 +226,8 @@ DEV void fb_flush(ScanLds& s, const E2Params& e, uint32_t t)
     wave_sync();
 }
 
-DEV void fb_add(ScanLds& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uint32_t t)
+template <class S>
+DEV void fb_add(S& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uint32_t t)
 {
     if (t == 0) {
         slot[0] = kSkipFallback;
@@ -233,7 +240,8 @@ DEV void fb_add(ScanLds& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uin
 
 // The wavefront's packets for the wide kernels, 32 per global atomic as
 // above; a packet past the wide stream's capacity goes to the lane kernels.
-DEV void wb_flush(ScanLds& s, const E2Params& e, uint32_t t)
+template <class S>
+DEV void wb_flush(S& s, const E2Params& e, uint32_t t)
 {
     wave_sync();
     const uint32_t k = s.nwb;
@@ -259,7 +267,8 @@ DEV void wb_flush(ScanLds& s, const E2Params& e, uint32_t t)
 
 // a packet with a bucket over kE2Bucket positions: the wide kernels, or the
 // lane kernels when wide mode is off
-DEV void big_add(ScanLds& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uint32_t idx, uint32_t t)
+template <class S>
+DEV void big_add(S& s, const E2Params& e, uint32_t* slot, uint32_t pkt, uint32_t idx, uint32_t t)
 {
     if (!e.wide) {
         fb_add(s, e, slot, pkt, t);
@@ -309,7 +318,8 @@ DEV uint2 make_record(uint32_t acc2, uint32_t acc1, bool f2, bool f1, uint32_t v
 
 // exceptional position j of bucket [bs, ...): statistics over all its
 // predecessors [bs, j) (their flags are final), its flags, its record
-DEV uint32_t scan_exceptional(ScanLds& s, uint32_t bs, uint32_t j, uint32_t w,
+template <class S>
+DEV uint32_t scan_exceptional(S& s, uint32_t bs, uint32_t j, uint32_t w,
                                                                uint2* rec)
 {
     const uint32_t pos = w & 2047, v = (w >> 11) & 255;
@@ -333,7 +343,8 @@ DEV uint32_t scan_exceptional(ScanLds& s, uint32_t bs, uint32_t j, uint32_t w,
 
 // insertion sort of a bucket by position (diagnostic safety net: the scatter
 // keeps position order when LDS atomics apply in lane order, as on gfx950)
-DEV void sort_bucket(ScanLds& s, uint32_t bs, uint32_t be)
+template <class S>
+DEV void sort_bucket(S& s, uint32_t bs, uint32_t be)
 {
     for (uint32_t j = bs + 1; j < be; ++j) {
         const uint32_t w = s.e[j];
@@ -357,7 +368,8 @@ DEV void sort_bucket(ScanLds& s, uint32_t bs, uint32_t be)
 // (the plain positions between keep the scatter's records), after it every
 // position (their t1, dist1 change).  xm = ~0: every position, every record
 // rewritten (after a sort).
-DEV void walk_from(ScanLds& s, uint32_t bs, uint32_t k, uint32_t xm, uint2* rec)
+template <class S>
+DEV void walk_from(S& s, uint32_t bs, uint32_t k, uint32_t xm, uint2* rec)
 {
     const bool all = xm == ~0u;
     uint32_t nf2 = 0, nh1 = 0;
@@ -449,10 +461,9 @@ DEV bool lane_order_probe(uint32_t* pr, uint32_t t)
     return !any_lane(!ok);
 }
 
-extern "C" __global__ __launch_bounds__(kScanThreads)
-void rc_enc2_scan(rc_batch_dev b, E2Params e)
+template <class S>
+DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
 {
-    __shared__ __attribute__((aligned(16))) ScanLds s;
     const uint32_t t = threadIdx.x;
     E2P_DECL
     // The repeat bits and bucket ranks below rely on same-address LDS atomics
@@ -595,7 +606,7 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
-                s.e[ok[m] ? k[m] : kScanDummyE] = w[m];
+                s.e[ok[m] ? k[m] : S::kDummyE] = w[m];
                 const uint32_t j = k[m] - st[m];
                 if (ok[m]) {
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
@@ -651,6 +662,21 @@ void rc_enc2_scan(rc_batch_dev b, E2Params e)
     fb_flush(s, e, t);
     wb_flush(s, e, t);
     E2P_FLUSH
+}
+
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_scan(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) ScanLdsT<2048> s;
+    scan_main(b, e, s);
+}
+
+// the same for launches whose packets are at most kWideSmallL bytes
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_scan_s(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) ScanLdsT<kWideSmallL> s;
+    scan_main(b, e, s);
 }
 
 // ------------------------------------------------------------------ pass 2
@@ -1275,7 +1301,7 @@ struct WScanLdsT {
     uint32_t runs[64];                // a big bucket's long runs (a keys)
     uint32_t nruns;
 };
-constexpr uint32_t kWideSmallL = 1216;
+
 
 DEV uint32_t lane_id() { return threadIdx.x & 63; }
 DEV uint64_t below_mask() { return (1ull << lane_id()) - 1ull; }
@@ -1988,8 +2014,12 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
             const hipError_t err = hipMemsetAsync(e.wcount, 0, sizeof(uint32_t), st);
             if (err != hipSuccess) return static_cast<int>(err);
         }
-        hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
-                           0, st, *b, e);
+        if (e.slot_len <= kWideSmallL)
+            hipLaunchKernelGGL(rc_enc2_scan_s, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
+                               0, st, *b, e);
+        else
+            hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
+                               0, st, *b, e);
         static const char* one = getenv("ENET_RC_ENC2_CODE1");        // the one-wavefront code pass (A/B)
         if ((one && atoi(one) == 1) || e.act != 64)
             hipLaunchKernelGGL(rc_enc2_code, dim3((cnt + 4 * e.act - 1) / (4 * e.act)), dim3(256), kCodeItab + 512, st,
