@@ -51,12 +51,11 @@ constexpr uint32_t kWavesPerGroup = 16;             // 1024-thread workgroups: t
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, uint32_t k) { return (w >> (8 * k)) & 0xFFu; }
 
 // 0xFF in every byte whose index (0..3 within dword d of a 16-B chunk) is >= k
+// (branch-free: this runs on every round that holds some packet's start)
 __device__ __forceinline__ uint32_t bytes_from(int k, int d)
 {
-    const int kd = k - 4 * d;
-    if (kd <= 0) return 0xFFFFFFFFu;
-    if (kd >= 4) return 0u;
-    return 0xFFFFFFFFu << (8 * kd);
+    const int kd = min(max(k - 4 * d, 0), 4);
+    return static_cast<uint32_t>(0xFFFFFFFFull << (8 * kd));
 }
 
 __device__ __forceinline__ uint32_t shift_by(const uint32_t* s, uint32_t v)
@@ -83,7 +82,7 @@ __device__ __forceinline__ uint32_t row_next(uint32_t x)
 __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh)
 {
     // bytes sh.. of the 8-byte little-endian pair (lo, hi), sh in 0..3
-    return sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
 }  // namespace
@@ -143,23 +142,31 @@ void rc_crc32_batch(const uint8_t* __restrict__ in, const uint64_t* __restrict__
             x.x = row_next(w[0]); x.y = row_next(w[1]); x.z = row_next(w[2]); x.w = row_next(w[3]);
             if (on && s == kLanesPer - 1 && mis) x = gload16(a + kLaneBytes);
             w[4 * kGran] = x.x; w[4 * kGran + 1] = x.y; w[4 * kGran + 2] = x.z; w[4 * kGran + 3] = x.w;
-            // funnel-shift the 80 bytes right by mis -> 64 bytes d[0..15]
+            // funnel-shift the 80 bytes right by mis -> 64 bytes d[0..15]: a
+            // two-stage dword shifter (two-way selects; a four-way select on
+            // dq became a branch per dword), then the byte shift
+            // (as bit selects: the compiler turns two-way selects over the
+            // array into a scratch-memory indexed copy)
+            const uint32_t m2 = 0u - ((dq >> 1) & 1u), m1 = 0u - (dq & 1u);
 #pragma unroll
-            for (uint32_t k = 0; k < 4 * kGran; ++k) {
-                const uint32_t lo = dq == 0 ? w[k] : dq == 1 ? w[k + 1] : dq == 2 ? w[k + 2] : w[k + 3];
-                const uint32_t hi = dq == 0 ? w[k + 1] : dq == 1 ? w[k + 2] : dq == 2 ? w[k + 3] : w[k + 4];
-                d[k] = funnel(lo, hi, bs);
-            }
+            for (uint32_t k = 0; k < 4 * kGran + 2; ++k) w[k] = (w[k + 2] & m2) | (w[k] & ~m2);
+#pragma unroll
+            for (uint32_t k = 0; k < 4 * kGran + 1; ++k) w[k] = (w[k + 1] & m1) | (w[k] & ~m1);
+#pragma unroll
+            for (uint32_t k = 0; k < 4 * kGran; ++k) d[k] = funnel(w[k], w[k + 1], bs);
         }
         // zero the bytes before the packet; complement its first four
         // (register preset): only the chunks at a packet's start
         const int lead = static_cast<int>(static_cast<int64_t>(start - c));   // packet byte 0 in chunk
         if (__builtin_amdgcn_ballot_w64(on && lead > -4) != 0) {
+            // (bytes_from(lead + 4, k) == bytes_from(lead, k - 1))
+            const uint32_t cm = len >= 4 ? ~0u : 0u;
+            uint32_t prev = bytes_from(lead, -1);
 #pragma unroll
             for (int k = 0; k < static_cast<int>(4 * kGran); ++k) {
                 const uint32_t keep = bytes_from(lead, k);
-                d[k] &= keep;
-                if (len >= 4) d[k] ^= keep & ~bytes_from(lead + 4, k);
+                d[k] = (d[k] & keep) ^ (keep & ~prev & cm);
+                prev = keep;
             }
         }
         // raw CRC of the 64 bytes (slice-by-16 per granule, the register
