@@ -515,11 +515,11 @@ def pcie_inclusive(coder, d, o, l, args):
     bc, bd, ok = measure(lambda k: np.zeros(k, np.uint8))
     res = {"value": round(nb / (bc + bd) / GIB, 4), "unit": "GiB/s",
            "compress_GiBps": round(nb / bc / GIB, 4), "decompress_GiBps": round(nb / bd / GIB, 4),
-           "bit_exact": ok, "note": "enet_rc_*_batch_host from pageable caller buffers: a back-to-back input DMA'd "
-                   "from the caller buffer page-locked for the call (else gathered into pinned staging on a thread "
-                   "pool, overlapped with chunked H2D), kernels, outputs that fill their slots DMA'd into place "
-                   "(else packed on the device, chunked D2H of the produced bytes overlapped with the pooled "
-                   "scatter); best of 3"}
+           "bit_exact": ok, "note": "enet_rc_*_batch_host from pageable caller buffers, page-locked for the call: "
+                   "a back-to-back input DMA'd directly, slots at a uniform pitch one strided DMA, other gapped "
+                   "inputs gathered by a GPU kernel over PCIe; kernels; outputs that fill their slots DMA'd into "
+                   "place, others packed on the device and scattered into the caller's slots by a GPU kernel "
+                   "over PCIe; best of 3"}
     pc, pd, pok = measure(lambda k: torch.zeros(k, dtype=torch.uint8).pin_memory().numpy())
     res["pinned_caller"] = {"value": round(nb / (pc + pd) / GIB, 4), "compress_GiBps": round(nb / pc / GIB, 4),
                             "decompress_GiBps": round(nb / pd / GIB, 4), "bit_exact": pok,

@@ -155,6 +155,12 @@ int rc_hip_dgram_launch(int stage, const rc_dgram_dev *g, void *stream);
 int rc_hip_pack(const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len, uint32_t n,
                 uint64_t *bsum, uint8_t *packed, void *stream);
 /* The reverse: packed (back to back) -> out[out_off[i] .. +out_len[i]). */
+/* packets [src + soff[i], +len[i]) -> dst + doff[i] in whole 16-B granules
+ * (doff[i] has the source address's alignment mod 16, its granules belong
+ * to packet i alone); src may
+ * be mapped host memory (rc_pack.hip) */
+int rc_hip_gather16(const uint8_t *src, const uint64_t *soff, uint8_t *dst, const uint64_t *doff,
+                    const uint32_t *len, uint32_t n, void *stream);
 int rc_hip_unpack(const uint8_t *packed, uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                   uint32_t n, uint64_t *bsum, void *stream);
 

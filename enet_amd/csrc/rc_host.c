@@ -586,6 +586,19 @@ static void host_unpin(const void *p, int pinned)
     if (pinned == 1) hipHostUnregister((void *) ((uintptr_t) p & ~(uintptr_t) 4095));
 }
 
+/* ENET_RC_GPU_COPY=0: host batches move gapped inputs and outputs through
+ * pinned staging on the host instead of the GPU's gather / scatter kernels
+ * over mapped caller memory */
+static int gpu_copy(void)
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("ENET_RC_GPU_COPY");
+        on = e ? atoi(e) != 0 : 1;
+    }
+    return on;
+}
+
 /* ENET_RC_HOST_PROFILE=1: phase times of run_host on stderr (diagnostic) */
 static double now_ms(void)
 {
@@ -621,21 +634,88 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         if (in_len[i] > max_len) max_len = in_len[i];
         if (out_cap[i] > max_cap) max_cap = out_cap[i];
     }
+    /* An input in gapped slots (the compressed side of a round trip) is
+     * gathered by the GPU: the caller's buffer is page-locked for the call and
+     * mapped, and rc_gather16 (rc_pack.hip) reads the packets over PCIe in whole
+     * 16-B granules into the device input (each packet in granules of its own,
+     * at its source alignment) -- no staging copy on the host, and the
+     * gaps between slots never cross PCIe.  ENET_RC_GPU_COPY=0: the staging
+     * path. */
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    int zc_pin = 0;
+    const uint8_t *zc_dev = NULL;
+    uint64_t zc_lo = 0;
+    /* Slots at a uniform pitch (a caller's array of fixed-size buffers) are
+     * one strided DMA instead (hipMemcpy2DAsync: max_len bytes of each slot,
+     * rows round_up(max_len, 16) apart on the device) */
+    uint64_t pitch = 0, row = 0;
+    if (!packed_in && !gbuf && allow_pin && gpu_copy() && in_bytes >= (16u << 20) && n >= 2 &&
+        in_off[1] > in_off[0] && in_off[1] - in_off[0] >= max_len) {
+        pitch = in_off[1] - in_off[0];
+        for (size_t i = 2; i < n && pitch; ++i)
+            if (in_off[i] != in_off[0] + i * pitch) pitch = 0;
+        if (pitch) {
+            zc_lo = in_off[0];
+            zc_pin = host_pin(in + zc_lo, in_off[n - 1] + in_len[n - 1] - zc_lo);
+            if (zc_pin) row = (max_len + 15) & ~(uint64_t) 15;
+            else pitch = 0;
+        }
+    }
+    if (!pitch && !packed_in && !gbuf && allow_pin && gpu_copy() && in_bytes >= (16u << 20)) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (size_t i = 0; i < n; ++i)
+            if (in_len[i]) {
+                if (in_off[i] < lo) lo = in_off[i];
+                if (in_off[i] + in_len[i] > hi) hi = in_off[i] + in_len[i];
+            }
+        if (hi > lo) zc_pin = host_pin(in + lo, hi - lo);
+        if (zc_pin) {
+            void *dp = NULL;
+            /* (the mapping keeps the page offset: granule phases match) */
+            if (hipHostGetDevicePointer(&dp, (void *) (in + lo), 0) == hipSuccess && dp &&
+                (((uintptr_t) dp ^ (uintptr_t) (in + lo)) & 4095) == 0) {
+                zc_dev = (const uint8_t *) dp;
+                zc_lo = lo;
+            } else {
+                (void) hipGetLastError();
+                host_unpin(in + lo, zc_pin);
+                zc_pin = 0;
+            }
+        }
+    }
+    /* device input bytes: back to back, or (GPU gather) granule-padded */
+    uint64_t dev_in = pitch ? n * row : in_bytes;
+    if (zc_dev) {
+        dev_in = 0;
+        for (size_t i = 0; i < n; ++i)
+            if (in_len[i]) dev_in += (((uintptr_t) (in + in_off[i]) & 15) + in_len[i] + 15) & ~(uint64_t) 15;
+    }
     size_t a_in = 0;
-    size_t a_ioff = (a_in + in_bytes + 15) & ~(size_t) 15;
+    size_t a_ioff = (a_in + dev_in + 15) & ~(size_t) 15;
     size_t a_ilen = a_ioff + n * 8;
     size_t a_ooff = (a_ilen + n * 4 + 15) & ~(size_t) 15;
     size_t a_ocap = a_ooff + n * 8;
     size_t a_olen = (a_ocap + n * 4 + 15) & ~(size_t) 15;
     size_t a_out = (a_olen + n * 4 + 15) & ~(size_t) 15;
     size_t total = a_out + out_bytes + 16;
-    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
-    if (stage_reserve(c, total) != 0) return (int) hipErrorOutOfMemory;
+    size_t a_soff = (total + 15) & ~(size_t) 15;        /* source offsets of a device-side gather */
     const size_t blocks = (n + 1023) / 1024;
-    if (pack_reserve(c, out_bytes + 16, blocks) != 0) return (int) hipErrorOutOfMemory;
+    if (stage_reserve(c, a_soff + n * 8) != 0 || pack_reserve(c, out_bytes + 16, blocks) != 0) {
+        host_unpin(in + zc_lo, zc_pin);
+        return (int) hipErrorOutOfMemory;
+    }
     uint8_t *h = c->h_stage, *d = c->d_stage;
     uint64_t *hio = (uint64_t *) (h + a_ioff);
-    {
+    if (pitch) {
+        for (size_t i = 0; i < n; ++i) hio[i] = i * row;
+    } else if (zc_dev) {
+        uint64_t acc = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const uint64_t ph = (uintptr_t) (in + in_off[i]) & 15;
+            hio[i] = in_len[i] ? acc + ph : acc;
+            if (in_len[i]) acc += (ph + in_len[i] + 15) & ~(uint64_t) 15;
+        }
+    } else {
         uint64_t acc = 0;
         for (size_t i = 0; i < n; ++i) { hio[i] = acc; acc += in_len[i]; }
     }
@@ -643,14 +723,34 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     memcpy(h + a_ooff, out_off, n * 8);
     memcpy(h + a_ocap, out_cap, n * 4);
     hipError_t err = hipMemcpyAsync(d + a_ioff, h + a_ioff, a_olen - a_ioff, hipMemcpyHostToDevice, c->stream);
-    if (err != hipSuccess) return (int) err;
+    if (err != hipSuccess) { host_unpin(in + zc_lo, zc_pin); return (int) err; }
     /* the payload: straight from the caller's memory when it is one range and
      * can be page-locked; else in four packet groups through pinned staging,
      * the staging copy of group k+1 overlapping the DMA of group k */
     const int pin_in = packed_in && allow_pin ? host_pin(in + in_lo, in_bytes) : 0;
     if (pin_in) err = hipMemcpyAsync(d + a_in, in + in_lo, in_bytes, hipMemcpyHostToDevice, c->stream);
-    if (err != hipSuccess) { host_unpin(in + in_lo, pin_in); return (int) err; }
-    const int ig = pin_in ? 0 : in_bytes >= (16u << 20) ? 4 : 1;
+    if (pitch) {
+        err = hipMemcpy2DAsync(d + a_in, row, in + zc_lo, pitch, max_len, n - 1, hipMemcpyHostToDevice, c->stream);
+        if (err == hipSuccess && in_len[n - 1])
+            err = hipMemcpyAsync(d + a_in + (n - 1) * row, in + in_off[n - 1], in_len[n - 1], hipMemcpyHostToDevice,
+                                 c->stream);
+    }
+    if (zc_dev) {
+        uint64_t *hso = (uint64_t *) (h + a_soff);
+        for (size_t i = 0; i < n; ++i) hso[i] = in_len[i] ? in_off[i] - zc_lo : 0;
+        err = hipMemcpyAsync(d + a_soff, h + a_soff, n * 8, hipMemcpyHostToDevice, c->stream);
+        if (err == hipSuccess)
+            err = (hipError_t) rc_hip_gather16(zc_dev, (const uint64_t *) (d + a_soff), d + a_in,
+                                               (const uint64_t *) (d + a_ioff), (const uint32_t *) (d + a_ilen),
+                                               (uint32_t) n, (void *) c->stream);
+    }
+    if (err != hipSuccess) {
+        if (pin_in || zc_pin) hipStreamSynchronize(c->stream);
+        host_unpin(in + in_lo, pin_in);
+        host_unpin(in + zc_lo, zc_pin);
+        return (int) err;
+    }
+    const int ig = pin_in || zc_pin ? 0 : in_bytes >= (16u << 20) ? 4 : 1;
     for (int g = 0; g < ig; ++g) {
         const size_t lo = n * (size_t) g / (size_t) ig, hi = n * (size_t) (g + 1) / (size_t) ig;
         if (hi <= lo) continue;
@@ -666,9 +766,10 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
                         (const uint32_t *) (d + a_ilen), n, max_len, max_cap, d + a_out,
                         (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_ocap),
                         (uint32_t *) (d + a_olen), (void *) c->stream);
-    if (pin_in) {               /* the input DMA is behind the kernels on the stream */
+    if (pin_in || zc_pin) {     /* the input DMA / gather is behind the kernels on the stream */
         hipStreamSynchronize(c->stream);
         host_unpin(in + in_lo, pin_in);
+        host_unpin(in + zc_lo, zc_pin);
     }
     if (rc != 0) return rc;
     if (prof) { hipStreamSynchronize(c->stream); tp[3] = now_ms(); }
@@ -726,6 +827,36 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     if (prof) tp[4] = now_ms();
     if (packed > out_bytes) return (int) hipErrorUnknown;
     memcpy(out_len, h + a_olen, n * 4);
+    /* the packed results into the caller's slots by the GPU (rc_pack.hip's
+     * copy kernel writing the mapped, page-locked caller buffer over PCIe):
+     * no host scatter.  ENET_RC_GPU_COPY=0: D2H + scatter on the host. */
+    if (allow_pin && gpu_copy() && packed >= (16u << 20)) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (out_off[i] < lo) lo = out_off[i];
+            if (out_off[i] + out_cap[i] > hi) hi = out_off[i] + out_cap[i];
+        }
+        const int op = hi > lo ? host_pin(out + lo, hi - lo) : 0;
+        void *dp = NULL;
+        if (op && hipHostGetDevicePointer(&dp, (void *) (out + lo), 0) == hipSuccess && dp) {
+            err = (hipError_t) rc_hip_unpack(c->d_pack, (uint8_t *) dp - lo, (const uint64_t *) (d + a_ooff),
+                                             (const uint32_t *) (d + a_olen), (uint32_t) n, c->d_bsum,
+                                             (void *) c->stream);
+            const hipError_t e2 = hipStreamSynchronize(c->stream);
+            host_unpin(out + lo, op);
+            if (err == hipSuccess) err = e2;
+            if (prof) {
+                tp[5] = now_ms();
+                fprintf(stderr, "enet_rc host %s n=%zu in=%.1f MB out=%.1f MB (GPU copies): stage+H2D enqueue %.3f, "
+                        "H2D drain %.3f, kernels %.3f, pack+lens %.3f, scatter %.3f, total %.3f ms\n",
+                        decompress ? "dec" : "enc", n, in_bytes / 1e6, packed / 1e6, tp[1] - tp[0], tp[2] - tp[1],
+                        tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[5] - tp[0]);
+            }
+            return err == hipSuccess ? 0 : (int) err;
+        }
+        (void) hipGetLastError();
+        host_unpin(out + lo, op);
+    }
     uint64_t *poff = (uint64_t *) malloc((n + 1) * sizeof(uint64_t));
     if (!poff) return (int) hipErrorOutOfMemory;
     uint64_t acc = 0;
@@ -907,8 +1038,9 @@ static int run_dgram_host(rc_ctx *c, int decode, const uint8_t *in, const uint64
     size_t a_olen = (a_ooff + n * 8 + 15) & ~(size_t) 15;
     size_t a_out = (a_olen + n * 4 + 15) & ~(size_t) 15;
     size_t total = a_out + out_bytes + 16;
+    size_t a_soff = (total + 15) & ~(size_t) 15;        /* source offsets of a device-side gather */
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
-    if (stage_reserve(c, total) != 0) return (int) hipErrorOutOfMemory;
+    if (stage_reserve(c, a_soff + n * 8) != 0) return (int) hipErrorOutOfMemory;
     uint8_t *h = c->h_stage, *d = c->d_stage;
     memcpy(h, in, in_bytes);
     memcpy(h + a_ioff, in_off, n * 8);

@@ -177,3 +177,43 @@ extern "C" int rc_hip_pack(const uint8_t* out, const uint64_t* out_off, const ui
                        bsum, packed);
     return static_cast<int>(hipGetLastError());
 }
+
+// Gather of a host batch's packets by the GPU over PCIe (rc_host.c: an input
+// in gapped slots of a mapped, page-locked caller buffer): packet i's bytes
+// [src + soff[i], +len[i]) -> dst + doff[i], where doff[i] has the source's
+// alignment mod 16 and the 16-B granules around [doff[i], +len[i]) belong to
+// packet i alone, so whole aligned 16-B chunks are copied (the bytes around
+// the packet in its first and last granule come along; they are never read).
+// Sixteen lanes per packet, four packets per wavefront.
+extern "C" __global__ __launch_bounds__(kThreads)
+void rc_gather16(const uint8_t* src, const uint64_t* soff, uint8_t* dst, const uint64_t* doff, const uint32_t* len,
+                 uint32_t n)
+{
+    const uint32_t lane = threadIdx.x & 15;
+    const uint32_t groups = gridDim.x * (kThreads / 16);
+    for (uint32_t i = (blockIdx.x * kThreads + threadIdx.x) >> 4; i < n; i += groups) {
+        const uint32_t m = len[i];
+        if (m == 0) continue;
+        const uintptr_t s0 = reinterpret_cast<uintptr_t>(src) + soff[i];
+        const uintptr_t sa = s0 & ~static_cast<uintptr_t>(15), se = (s0 + m + 15) & ~static_cast<uintptr_t>(15);
+        const uintptr_t da = (reinterpret_cast<uintptr_t>(dst) + doff[i]) & ~static_cast<uintptr_t>(15);
+        const uint32_t nch = static_cast<uint32_t>((se - sa) >> 4);
+        for (uint32_t c = lane; c < nch; c += 16)
+            reinterpret_cast<uint4*>(da)[c] = reinterpret_cast<const uint4*>(sa)[c];
+    }
+}
+
+extern "C" int rc_hip_gather16(const uint8_t* src, const uint64_t* soff, uint8_t* dst, const uint64_t* doff,
+                               const uint32_t* len, uint32_t n, void* stream)
+{
+    if (n == 0) return 0;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    uint32_t blocks = (n + kThreads / 16 - 1) / (kThreads / 16);
+    const uint32_t cap = static_cast<uint32_t>(cus) * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(rc_gather16, dim3(blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream), src, soff, dst,
+                       doff, len, n);
+    return static_cast<int>(hipGetLastError());
+}

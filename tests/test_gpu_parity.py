@@ -401,6 +401,37 @@ def test_host_pointer_batches_large(coder):
     assert np.array_equal(dout[: d.size], d)
 
 
+def test_host_pointer_batches_uniform_slots(coder):
+    """Host batches whose compressed packets sit in slots at a uniform, odd
+    pitch from an odd base (rc_host.c run_host: the strided H2D of max_len
+    bytes per slot for the decompress input; the GPU scatter of the packed
+    results into the caller's slots for the compress output): bit-exact
+    against the oracle, the last slot's bytes beyond its packet untouched."""
+    import ctypes as C
+    from oracle.pyoracle import compress_batch as ocompress, fnv_digest
+    d, o, l = synth.mixed_batch(26000, seed=91)          # > 16 MB each way
+    lib = coder.lib
+    n = len(l)
+    ln = l.astype(np.uint32)
+    pitch = 2 * 1392 + 64 + 1
+    cap = np.full(n, pitch - 1, np.uint32)
+    coff = (5 + np.arange(n, dtype=np.uint64) * np.uint64(pitch)).astype(np.uint64)
+    cout = np.full(int(coff[-1]) + pitch + 64, 0xA5, np.uint8)
+    clen = np.zeros(n, np.uint32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    assert lib.enet_rc_compress_batch_host(coder.ctx, p(d), p(o), p(ln), n, p(cout), p(coff), p(cap), p(clen)) == 0
+    want, wo, wcap, wl = ocompress(d, o, l, "port")
+    assert np.array_equal(clen, wl)
+    assert fnv_digest(cout, coff, clen) == fnv_digest(want, wo, wl)
+    assert np.all(cout[int(coff[-1]) + int(clen[-1]):] == 0xA5)
+    dout = np.zeros(int(o[-1]) + int(l[-1]) + 16, np.uint8)
+    dlen = np.zeros(n, np.uint32)
+    assert lib.enet_rc_decompress_batch_host(coder.ctx, p(cout), p(coff), p(clen), n, p(dout), p(o), p(ln),
+                                             p(dlen)) == 0
+    assert np.array_equal(dlen, ln)
+    assert np.array_equal(dout[: d.size], d)
+
+
 def test_device_decoder_bounded_vs_oracle(coder):
     """enet_rc_decompress_batch_device_bounded: the caller's output bound sizes
     the wave decoder's model, so 513-1024-packet batches decode one wavefront
