@@ -1431,8 +1431,11 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
             const uint32_t v = (w >> 11) & 255, a = (w >> 19) & 255;
             const bool has = (w & (256u << 19)) != 0;
             uint32_t lt;
-            const KeyBits kp = key_bits(p), ka = key_bits(a), kv = key_bits(v);
-            const uint64_t mine = act ? match_bits(p, kp, am, lt) : 0ull;          // my bucket
+            const KeyBits ka = key_bits(a), kv = key_bits(v);
+            // my bucket: its elements are lanes [bs - W, be - W) of the window
+            // (buckets are contiguous in e[], and an active one lies inside it)
+            const uint32_t blo = bs - W, bhi = be - W;
+            const uint64_t mine = act ? ((bhi >= 64 ? ~0ull : (1ull << bhi) - 1ull) & ~((1ull << blo) - 1ull)) : 0ull;
             const uint64_t hm = __builtin_amdgcn_ballot_w64(has);
             const uint64_t ctx2 = has ? match_bits(a, ka, mine & hm, lt) : 0ull;   // my order-2 context
             uint32_t less2;
