@@ -1621,7 +1621,7 @@ DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp)
         const bool ok0 = q + t < k;
         const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
         const bool has = (w & (256u << 19)) != 0;
-        group_add<false>(hist, (w >> 19) & 255, ok0 && has);
+        if (ok0 && has) atomicAdd(&hist[(w >> 19) & 255], 1u);
         if (ok0 && !has) wrec[2 * (w & 2047)] = make_uint2(kNoCodeLo, kNoCodeTot | ((w >> 11) & 255) << 16);
     }
     wave_sync();
@@ -1744,7 +1744,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         for (uint32_t i = 1 + t; i < n + t; i += kScanThreads) {
             const bool ok = i < n;
             const uint32_t p = s.x[q0 + (ok ? i : 1) - 1];
-            group_add<false>(s.cnt, p, ok);
+            if (ok) atomicAdd(&s.cnt[p], 1u);          // (a count: the order of same-address adds does not matter)
         }
         wave_sync();
         W2P(1)
