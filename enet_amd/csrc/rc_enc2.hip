@@ -1486,10 +1486,11 @@ DEV void wide_short_runs(S& s, uint32_t ks, const uint32_t* hist, const uint32_t
         const bool act = in && re <= W + 64;
         const uint64_t nt = __builtin_amdgcn_ballot_w64(in && !act);
         const uint32_t nextW = nt ? __builtin_amdgcn_readlane(rs, static_cast<uint32_t>(__builtin_ctzll(nt))) : W + 64;
-        const uint64_t am = __builtin_amdgcn_ballot_w64(act);
-        uint32_t lt, less;
-        const KeyBits ka = key_bits(a), kv = key_bits(v);
-        const uint64_t ctx = act ? match_bits(a, ka, am, lt) : 0ull;
+        uint32_t less;
+        const KeyBits kv = key_bits(v);
+        // my run (order-2 context): lanes [rs - W, re - W) of the window
+        const uint32_t rlo = rs - W, rhi = re - W;
+        const uint64_t ctx = act ? ((rhi >= 64 ? ~0ull : (1ull << rhi) - 1ull) & ~((1ull << rlo) - 1ull)) : 0ull;
         const uint64_t samem = match_bits(v, kv, ctx, less);
         const bool f2 = act && (samem & below) != 0;
         const uint64_t F2 = __builtin_amdgcn_ballot_w64(f2);
