@@ -1403,6 +1403,13 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
 {
     const uint32_t t = lane_id();
     const uint64_t below = below_mask();
+    // lanes by order-2 key a: a 256-entry table of lane masks (in sw, free
+    // until the big buckets), or-ed into and read back per window, then
+    // cleared by the lanes that set it
+    uint64_t* amask = reinterpret_cast<uint64_t*>(s.sw);
+    *reinterpret_cast<uint4*>(&amask[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(&amask[4 * t + 2]) = make_uint4(0u, 0u, 0u, 0u);
+    wave_sync();
 #pragma unroll 1
     for (uint32_t W = 0; W < total;) {
         const uint32_t ei = W + t;
@@ -1430,14 +1437,19 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
         if (am) {
             const uint32_t v = (w >> 11) & 255, a = (w >> 19) & 255;
             const bool has = (w & (256u << 19)) != 0;
-            uint32_t lt;
-            const KeyBits ka = key_bits(a), kv = key_bits(v);
+            const KeyBits kv = key_bits(v);
             // my bucket: its elements are lanes [bs - W, be - W) of the window
             // (buckets are contiguous in e[], and an active one lies inside it)
             const uint32_t blo = bs - W, bhi = be - W;
             const uint64_t mine = act ? ((bhi >= 64 ? ~0ull : (1ull << bhi) - 1ull) & ~((1ull << blo) - 1ull)) : 0ull;
-            const uint64_t hm = __builtin_amdgcn_ballot_w64(has);
-            const uint64_t ctx2 = has ? match_bits(a, ka, mine & hm, lt) : 0ull;   // my order-2 context
+            // my order-2 context: the lanes of my bucket with my a
+            const bool ah = act && has;
+            if (ah) atomicOr(reinterpret_cast<unsigned long long*>(&amask[a]), 1ull << t);
+            wave_sync();
+            const uint64_t am2 = ah ? amask[a] : 0ull;
+            wave_sync();
+            if (ah) amask[a] = 0ull;
+            const uint64_t ctx2 = am2 & mine;
             uint32_t less2;
             const uint64_t same2m = match_bits(v, kv, ctx2, less2);
             const bool f2 = act && (same2m & below) != 0;
