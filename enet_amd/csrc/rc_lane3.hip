@@ -52,6 +52,14 @@
 namespace {
 
 constexpr uint32_t kRec = 64;                       // order-1 record, big order-2 record
+// decoder: links (o2 info) of symbols 0..kLinkCache-1 of the packet's first
+// dense order-1 context, cached in LDS (64 B per lane).  A step decoded at
+// order 2 needs only the link of (b, v) from its order-1 context b, and on
+// game state b is mostly 0, whose dense block is in HBM: the cache takes that
+// dependent load off the step for small v.  A link of a symbol b lacks is 0
+// (blocks start zeroed, links are written only for present symbols), so the
+// link alone gives the next step's order-2 info.
+constexpr uint32_t kLinkCache = 32;
 constexpr uint32_t kArena3 = kO1Base + 256 * kRec;  // arena start (after header and order-1 table)
 constexpr uint32_t kMaxLen3 = 1919;                 // <= 2*1919 + 256 nodes < 4094: no reset (compress.c:150)
 constexpr uint32_t kNodeLimit = 4096 - 2;           // compress.c:148-157: sizeof symbols / sizeof ENetSymbol - order
@@ -429,6 +437,7 @@ struct Lane {
     uint32_t nsame, fromprv;    // where the next step's R[v] comes from (lane_prefetch)
     uint32_t nodes;             // compress.c's nextSymbol: 1 (root) + the (context, value) pairs created
     uint32_t ldsu;              // the lane's LDS dense block holds a big order-2 context
+    uint32_t cext;              // decoder: the dense order-1 block whose first links are in the LDS cache (0: none)
 };
 
 DEV void lane_init(Lane& L, uint8_t* reg)
@@ -441,6 +450,7 @@ DEV void lane_init(Lane& L, uint8_t* reg)
     L.nsame = false; L.fromprv = false;
     L.nodes = 1;
     L.ldsu = 0;
+    L.cext = 0;
 }
 
 // compress.c:148-157: the model starts over (new epoch: every order-1 record
@@ -456,6 +466,7 @@ DEV void lane_reset(Lane& L, uint8_t* reg)
     L.nsame = false; L.fromprv = false;
     L.nodes = 1;
     L.ldsu = 0;
+    L.cext = 0;
 }
 
 // top of a step: the records loaded by the previous step become registers
@@ -504,7 +515,7 @@ DEV void o2_stats(const Lane& L, uint32_t& esc, uint32_t& tot)
 //   3. the o2 info of (b, v) and where it lives, the loads for step i+1
 template <bool HAVE_H1>
 DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32_t v, int at, Look<3>& h1,
-                      Look<6>& h2, bool new0, bool track)
+                      Look<6>& h2, bool new0, bool track, uint16_t* lc = nullptr)
 {
     // nodes compress.c creates this step: v in each visited context that lacks
     // it (the order-2 context is always visited, order 1 when order 2 did not
@@ -565,6 +576,9 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32
             L.prv_dirty = L.prv_dirty || (!L.same && ni != L.info);
         } else if (ni != L.info) {
             *reinterpret_cast<uint16_t*>(reg + L.ipos) = static_cast<uint16_t>(ni);
+            // (the link cache: a copy of the cached block's first links)
+            const uint32_t li = (L.ipos - L.cext - 288) >> 1;
+            if (lc && L.cext != 0 && L.ipos >= L.cext + 288 && li < kLinkCache) lc[li] = static_cast<uint16_t>(ni);
         }
     }
     // ---- 2. o1 context b, compress.c:286-316 (its lookup, when the decoder did not need it)
@@ -572,8 +586,20 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32
     if (L.order >= 1 && at <= 1) {
         if (track) created += h1.found ? 0u : 1u;
         bool ovf = L.ovf != 0;
+        const bool was = L.cur.dense != 0;
         ctx_update<3, true>(reg, ldsb, L.ldsu, L.cur, h1, v, L.bump, end, ovf, true);
         L.ovf = ovf;
+        // the decoder's first dense order-1 block: its links for symbols below
+        // kLinkCache copied to the lane's LDS cache (once per packet)
+        if (lc && any_lane(!was && L.cur.dense != 0 && L.cext == 0 && !L.ovf)) {
+            if (!was && L.cur.dense != 0 && L.cext == 0 && !L.ovf) {
+                L.cext = L.cur.ext;
+                const uint4* src = reinterpret_cast<const uint4*>(reg + L.cext + 288);
+                uint4* dst = reinterpret_cast<uint4*>(lc);
+#pragma unroll
+                for (uint32_t k = 0; k < 2 * kLinkCache / 16; ++k) dst[k] = src[k];
+            }
+        }
     }
     if (track) L.nodes += created;
     // ---- 3. next step: contexts (b, v)
@@ -717,7 +743,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
 }
 
 DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg,
-                         uint8_t* root, uint8_t* ldsb)
+                         uint8_t* root, uint8_t* ldsb, uint16_t* lc)
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
@@ -813,11 +839,18 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         }
         // the patched o1 context needs v's lookup (compress.c:598-615)
         if (at == 0 && L.order >= 1) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
-        if (at == 2 && L.order >= 1) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
+        if (at == 2 && L.order >= 1) {
+            // (the next step's order-2 info: the link cache where it holds v)
+            const bool lcv = L.cur.dense != 0 && L.cext != 0 && L.cur.ext == L.cext && v < kLinkCache;
+            if (any_lane(!lcv)) {
+                if (!lcv) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
+            }
+            if (lcv) { h1.info = lc[v]; h1.found = 1u; }
+        }
         if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, ldsb, L.q, v);
         fail = o.n >= o.cap;                                         // compress.c:617
         PROF(4)
-        lane_advance<true>(L, reg, ldsb, end, v, at, h1, h2, new0, true); // (see compress_one3)
+        lane_advance<true>(L, reg, ldsb, end, v, at, h1, h2, new0, true, lc); // (see compress_one3)
         PROF(5)
         if (fail || L.ovf) break;
         if (rare_lane(L.nodes >= kNodeLimit)) {                      // compress.c:617-621 -> :148-157
@@ -868,6 +901,7 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t local = wave * act + l;
     uint8_t* root = smem + local * (DECOMP ? kRootStrideDec : kRootStride3);
     uint8_t* ldsb = smem + (DECOMP ? 4 * act * kRootStrideDec : 4 * act * kRootStride3 + 256) + local * kDenseO2;
+    uint16_t* lc = reinterpret_cast<uint16_t*>(smem + 4 * act * (kRootStrideDec + kDenseO2) + local * 2 * kLinkCache);
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
@@ -875,7 +909,7 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t count = ws.sub_count ? *ws.sub_count : b.n;   // a sub-list: the two-pass encoder's leftovers
     for (uint32_t i = slot; i < count; i += gridDim.x * per_block) {
         const uint32_t pkt = ws.sub_list ? ws.sub_list[i] : (order ? order[i] : i);
-        if (DECOMP) decompress_one3(b, ws, pkt, reg, root, ldsb);
+        if (DECOMP) decompress_one3(b, ws, pkt, reg, root, ldsb, lc);
         else compress_one3(b, ws, pkt, reg, root, ldsb, mtab);
     }
 }
@@ -894,7 +928,8 @@ extern "C" int rc_hip_lane3_launch(int decompress, const rc_batch_dev* b, const 
     hipStream_t st = static_cast<hipStream_t>(stream);
     // the encoder: roots with their D copy + the mask table; the decoder: roots;
     // then a dense order-2 block per lane
-    const size_t lds = (decompress ? static_cast<size_t>(4 * ws->lane_active) * kRootStrideDec
+    // (+ the decoder's link cache)
+    const size_t lds = (decompress ? static_cast<size_t>(4 * ws->lane_active) * (kRootStrideDec + 2 * kLinkCache)
                                    : static_cast<size_t>(4 * ws->lane_active) * kRootStride3 + 256) +
                        static_cast<size_t>(4 * ws->lane_active) * kDenseO2;
     if (decompress)

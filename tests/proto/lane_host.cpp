@@ -34,6 +34,7 @@ static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n)
 static uint8_t g_root[304] __attribute__((aligned(16)));
 static uint8_t g_mtab[256] __attribute__((aligned(16)));
 static uint8_t g_ldsb[kDenseO2] __attribute__((aligned(16)));   // the lane's LDS dense block
+static uint16_t g_lc[kLinkCache] __attribute__((aligned(16)));   // the decoder's link cache
 static bool g_mtab_init = [] { for (uint32_t j = 0; j < 16; ++j) root3_mask_init(g_mtab, j); return true; }();
 #define COMPRESS_ARGS , g_ldsb, g_mtab
 
@@ -77,7 +78,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     }
 #endif
 
-    if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root, g_ldsb);
+    if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root, g_ldsb, g_lc);
     else COMPRESS_ONE(b, ws, 0, region, g_root COMPRESS_ARGS);
     return counters[0] ? 1 : (counters[3] ? 2 : 0);   // 1 = routed to the exact path, 2 = left by dec4
 }
