@@ -634,20 +634,20 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         if (in_len[i] > max_len) max_len = in_len[i];
         if (out_cap[i] > max_cap) max_cap = out_cap[i];
     }
-    /* An input in gapped slots (the compressed side of a round trip) is
-     * gathered by the GPU: the caller's buffer is page-locked for the call and
-     * mapped, and rc_gather16 (rc_pack.hip) reads the packets over PCIe in whole
-     * 16-B granules into the device input (each packet in granules of its own,
-     * at its source alignment) -- no staging copy on the host, and the
-     * gaps between slots never cross PCIe.  ENET_RC_GPU_COPY=0: the staging
-     * path. */
+    /* An input in gapped slots (the compressed side of a round trip), from a
+     * caller buffer page-locked for the call (ENET_RC_GPU_COPY=0: through
+     * pinned staging on the host instead):
+     *  - slots at a uniform pitch (a caller's array of fixed-size buffers):
+     *    one strided DMA (hipMemcpy2DAsync: max_len bytes of each slot, rows
+     *    round_up(max_len, 16) apart on the device);
+     *  - other gaps: the buffer is mapped and rc_gather16 (rc_pack.hip) reads
+     *    the packets over PCIe in whole 16-B granules into the device input
+     *    (each packet in granules of its own, at its source alignment), so
+     *    the gaps between slots never cross PCIe. */
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
     int zc_pin = 0;
     const uint8_t *zc_dev = NULL;
     uint64_t zc_lo = 0;
-    /* Slots at a uniform pitch (a caller's array of fixed-size buffers) are
-     * one strided DMA instead (hipMemcpy2DAsync: max_len bytes of each slot,
-     * rows round_up(max_len, 16) apart on the device) */
     uint64_t pitch = 0, row = 0;
     if (!packed_in && !gbuf && allow_pin && gpu_copy() && in_bytes >= (16u << 20) && n >= 2 &&
         in_off[1] > in_off[0] && in_off[1] - in_off[0] >= max_len) {
