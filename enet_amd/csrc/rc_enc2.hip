@@ -1896,7 +1896,9 @@ DEV void wcode_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, c
     double rrt1 = rcp64(rtot1);
     code(k.low, k.range, p.u1, p.c1, p.r1, o);
     if (any_lane(p.e2)) code(k.low, k.range, p.u2, p.c2, p.r2, o);
-    code(k.low, k.range, p.e0 ? 1 + under0 : 0u, p.e0 ? 1 + cnt0 : 1u, p.e0 ? k.rrt : 1.0, o);
+    // (the root's code is the identity for the lanes without e0: skipped when
+    // no lane of the wavefront has one)
+    if (any_lane(p.e0)) code(k.low, k.range, p.e0 ? 1 + under0 : 0u, p.e0 ? 1 + cnt0 : 1u, p.e0 ? k.rrt : 1.0, o);
     if (p.e0) root3_add_write(root, p.v, cnt0, ra);
     k.rtot = rtot1;
     const bool rs0 = p.e0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || k.rtot > kTotalLimit);
