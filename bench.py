@@ -518,7 +518,7 @@ def pcie_inclusive(coder, d, o, l, args):
            "bit_exact": ok, "note": "enet_rc_*_batch_host from pageable caller buffers, page-locked for the call: "
                    "a back-to-back input DMA'd directly, slots at a uniform pitch one strided DMA, other gapped "
                    "inputs gathered by a GPU kernel over PCIe; kernels; outputs that fill their slots DMA'd into "
-                   "place, others packed on the device and scattered into the caller's slots by a GPU kernel "
+                   "place, others written from their device slots into the caller's slots by a GPU kernel "
                    "over PCIe; best of 3"}
     pc, pd, pok = measure(lambda k: torch.zeros(k, dtype=torch.uint8).pin_memory().numpy())
     res["pinned_caller"] = {"value": round(nb / (pc + pd) / GIB, 4), "compress_GiBps": round(nb / pc / GIB, 4),

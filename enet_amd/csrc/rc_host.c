@@ -817,6 +817,38 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
             return 0;
         }
     }
+    /* the results straight from their device slots into the caller's slots
+     * by the GPU (rc_slot_copy writing the mapped, page-locked caller buffer
+     * over PCIe): no packing pass and no host scatter.  ENET_RC_GPU_COPY=0:
+     * packed on the device, D2H and scattered on the host. */
+    if (allow_pin && gpu_copy() && out_bytes >= (16u << 20)) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (out_off[i] < lo) lo = out_off[i];
+            if (out_off[i] + out_cap[i] > hi) hi = out_off[i] + out_cap[i];
+        }
+        const int op = hi > lo ? host_pin(out + lo, hi - lo) : 0;
+        void *dp = NULL;
+        if (op && hipHostGetDevicePointer(&dp, (void *) (out + lo), 0) == hipSuccess && dp) {
+            err = (hipError_t) rc_hip_slot_copy(d + a_out, (const uint64_t *) (d + a_ooff),
+                                                (const uint32_t *) (d + a_olen), (uint32_t) n, (uint8_t *) dp - lo,
+                                                (void *) c->stream);
+            const hipError_t e2 = hipStreamSynchronize(c->stream);
+            host_unpin(out + lo, op);
+            if (err == hipSuccess) err = e2;
+            if (err != hipSuccess) return (int) err;
+            memcpy(out_len, h + a_olen, n * 4);
+            if (prof) {
+                tp[5] = now_ms();
+                fprintf(stderr, "enet_rc host %s n=%zu in=%.1f MB (GPU slot copy): stage+H2D enqueue %.3f, "
+                        "H2D drain %.3f, kernels %.3f, slot copy %.3f, total %.3f ms\n", decompress ? "dec" : "enc",
+                        n, in_bytes / 1e6, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[5] - tp[3], tp[5] - tp[0]);
+            }
+            return 0;
+        }
+        (void) hipGetLastError();
+        host_unpin(out + lo, op);
+    }
     rc = rc_hip_pack(d + a_out, (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_olen), (uint32_t) n,
                      c->d_bsum, c->d_pack, (void *) c->stream);
     if (rc != 0) return rc;
@@ -827,36 +859,6 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     if (prof) tp[4] = now_ms();
     if (packed > out_bytes) return (int) hipErrorUnknown;
     memcpy(out_len, h + a_olen, n * 4);
-    /* the packed results into the caller's slots by the GPU (rc_pack.hip's
-     * copy kernel writing the mapped, page-locked caller buffer over PCIe):
-     * no host scatter.  ENET_RC_GPU_COPY=0: D2H + scatter on the host. */
-    if (allow_pin && gpu_copy() && packed >= (16u << 20)) {
-        uint64_t lo = UINT64_MAX, hi = 0;
-        for (size_t i = 0; i < n; ++i) {
-            if (out_off[i] < lo) lo = out_off[i];
-            if (out_off[i] + out_cap[i] > hi) hi = out_off[i] + out_cap[i];
-        }
-        const int op = hi > lo ? host_pin(out + lo, hi - lo) : 0;
-        void *dp = NULL;
-        if (op && hipHostGetDevicePointer(&dp, (void *) (out + lo), 0) == hipSuccess && dp) {
-            err = (hipError_t) rc_hip_unpack(c->d_pack, (uint8_t *) dp - lo, (const uint64_t *) (d + a_ooff),
-                                             (const uint32_t *) (d + a_olen), (uint32_t) n, c->d_bsum,
-                                             (void *) c->stream);
-            const hipError_t e2 = hipStreamSynchronize(c->stream);
-            host_unpin(out + lo, op);
-            if (err == hipSuccess) err = e2;
-            if (prof) {
-                tp[5] = now_ms();
-                fprintf(stderr, "enet_rc host %s n=%zu in=%.1f MB out=%.1f MB (GPU copies): stage+H2D enqueue %.3f, "
-                        "H2D drain %.3f, kernels %.3f, pack+lens %.3f, scatter %.3f, total %.3f ms\n",
-                        decompress ? "dec" : "enc", n, in_bytes / 1e6, packed / 1e6, tp[1] - tp[0], tp[2] - tp[1],
-                        tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[5] - tp[0]);
-            }
-            return err == hipSuccess ? 0 : (int) err;
-        }
-        (void) hipGetLastError();
-        host_unpin(out + lo, op);
-    }
     uint64_t *poff = (uint64_t *) malloc((n + 1) * sizeof(uint64_t));
     if (!poff) return (int) hipErrorOutOfMemory;
     uint64_t acc = 0;

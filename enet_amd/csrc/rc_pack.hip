@@ -217,3 +217,31 @@ extern "C" int rc_hip_gather16(const uint8_t* src, const uint64_t* soff, uint8_t
                        doff, len, n);
     return static_cast<int>(hipGetLastError());
 }
+
+// Each packet's produced bytes from its device slot into the same offset of
+// another buffer (rc_host.c: the results of a host batch written by the GPU
+// straight into the caller's mapped, page-locked slots over PCIe), one
+// wavefront per packet: no packing pass, no prefix sums.
+extern "C" __global__ __launch_bounds__(kThreads)
+void rc_slot_copy(const uint8_t* src, const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* dst)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t waves = gridDim.x * (kThreads / 64);
+    for (uint32_t i = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); i < n; i += waves)
+        copy_bytes(src + off[i], dst + off[i], len[i], lane);
+}
+
+extern "C" int rc_hip_slot_copy(const uint8_t* src, const uint64_t* off, const uint32_t* len, uint32_t n,
+                                uint8_t* dst, void* stream)
+{
+    if (n == 0) return 0;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    uint32_t blocks = (n + kThreads / 64 - 1) / (kThreads / 64);
+    const uint32_t cap = static_cast<uint32_t>(cus) * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(rc_slot_copy, dim3(blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream), src, off, len,
+                       n, dst);
+    return static_cast<int>(hipGetLastError());
+}
