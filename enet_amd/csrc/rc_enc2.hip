@@ -1350,6 +1350,21 @@ DEV uint64_t match_bits(uint32_t key, const KeyBits& kb, uint64_t e, uint32_t& l
     return e;
 }
 
+// match_bits as masks: the lanes of e with this lane's key (returned) and,
+// in ltm, the lanes of e with a smaller key -- counts over any subset of e
+// are then popcounts
+DEV uint64_t match_bits_lt(uint32_t key, const KeyBits& kb, uint64_t e, uint64_t& ltm)
+{
+    ltm = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const bool one = (key >> b) & 1u;
+        ltm |= one ? (e & ~kb.b[b]) : 0ull;
+        e &= one ? kb.b[b] : ~kb.b[b];
+    }
+    return e;
+}
+
 // cnt[key] += 1 for every lane with ok: one LDS atomic per distinct key (its
 // lowest lane adds the group's size).  RET: returns the lane's slot, the old
 // value plus its rank among the lanes with its key (lane order).
@@ -1450,15 +1465,18 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
             wave_sync();
             if (ah) amask[a] = 0ull;
             const uint64_t ctx2 = am2 & mine;
-            uint32_t less2;
-            const uint64_t same2m = match_bits(v, kv, ctx2, less2);
+            // my bucket's lanes with my v, and with a smaller v: both contexts' counts
+            uint64_t ltv;
+            const uint64_t eqv = match_bits_lt(v, kv, mine, ltv);
+            const uint64_t same2m = eqv & ctx2;
+            const uint32_t less2 = popc64(ltv & ctx2 & below);
             const bool f2 = act && (same2m & below) != 0;
             const uint64_t F2 = __builtin_amdgcn_ballot_w64(f2);
             const uint32_t t2 = popc64(ctx2 & below), same2 = popc64(same2m & below);
             const uint32_t dist2 = popc64(ctx2 & below & ~F2);
             const uint64_t vis1 = mine & ~F2;                                      // the bucket's order-1 visitors
-            uint32_t less1;
-            const uint64_t same1m = match_bits(v, kv, vis1, less1);
+            const uint64_t same1m = eqv & vis1;
+            const uint32_t less1 = popc64(ltv & vis1 & below);
             const bool f1 = act && !f2 && (same1m & below) != 0;
             const uint64_t F1 = __builtin_amdgcn_ballot_w64(f1);
             if (act) {
