@@ -58,8 +58,10 @@ typedef struct {
     void     *enc2_wide;
     uint64_t  enc2_wide_cap;  /* bytes */
     uint32_t *enc2_wlist;     /* [n_cap] */
-    /* the fast decoder in front of the v3 lane decoder: 6 = record-light (rc_dec6.hip, default),
-       4 = bucket-history (rc_dec4.hip; ENET_RC_DEC=4), 0 = none (ENET_RC_DEC4=0 or ENET_RC_DEC=0);
+    /* the fast decoder in front of the v3 lane decoder: 6 = record-light on one wavefront per
+       SIMD (rc_dec6.hip, default), 7 = record-light with helper wavefronts (rc_dec7.hip;
+       ENET_RC_DEC=7 with lane_active == 64), 4 = bucket-history (rc_dec4.hip; ENET_RC_DEC=4),
+       0 = none (ENET_RC_DEC4=0 or ENET_RC_DEC=0);
        the packets it leaves go to enc2_list / counters[3] */
     uint32_t  dec4;
     /* rc_dec6.hip: per packet, the positions the decoder took to start a new bigram (its
@@ -105,6 +107,11 @@ int rc_hip_dec4_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32
  * packets off its fast path or failing the check are listed in ws->enc2_list, count in
  * ws->counters[3]. */
 int rc_hip_dec6_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
+/* rc_dec6.hip's check alone (after rc_decompress_dec6 or rc_decompress_dec7). */
+int rc_hip_dec6_verify_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
+/* Record-light decoder with a helper wavefront per SIMD (rc_dec7.hip), then the check;
+ * needs lane_active == 64.  Same lists as rc_hip_dec6_launch. */
+int rc_hip_dec7_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
 uint32_t rc_hip_lane3_region_bytes(uint32_t max_len);

@@ -493,7 +493,7 @@ DEV void src_refill(ByteSrc& s, bool en)
     src_adv(s);
 }
 
-DEV void src_init(ByteSrc& s, const uint8_t* p, uint32_t len)
+DEV void src_init(ByteSrc& s, const uint8_t* p, uint32_t len, bool settle = true)
 {
     s.lo = reinterpret_cast<uintptr_t>(p);
     s.hi = s.lo + len;
@@ -518,7 +518,7 @@ DEV void src_init(ByteSrc& s, const uint8_t* p, uint32_t len)
     src_refill(s, true);
     // settle the chunk loads before the step loop: a load still pending at
     // the loop header makes the compiler wait for vmcnt(0) at every step
-    __builtin_amdgcn_s_waitcnt(0);
+    if (settle) __builtin_amdgcn_s_waitcnt(0);
 }
 
 // next byte (encoder input; the caller refills once per step)

@@ -27,6 +27,47 @@ static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n)
 }
 #endif
 
+#ifdef DEC7
+#ifndef DEC6
+static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n)
+{
+    static uint8_t seen[65536];
+    memset(seen, 0, sizeof seen);
+    uint32_t c = 0;
+    for (uint32_t j = 1; j < n; ++j) {
+        const uint32_t b = (x[j - 1] << 8) | x[j];
+        c += seen[b] ? 0u : 1u;
+        seen[b] = 1;
+    }
+    return c;
+}
+#endif
+#include "../../enet_amd/csrc/rc_dec7.hip"
+// the decoder's two sides for one lane: the main lane runs the packet, and the
+// helper runs one pass after every main step and whenever the main lane waits
+static uint8_t g_lds7[lds7_bytes(1)] __attribute__((aligned(16)));
+static uint8_t g_tab7[RC_DEC6_TAB_BYTES] __attribute__((aligned(16)));   // bucket records (never cleared)
+static Help7 g_h7;
+static Store7 g_s7;
+static Lds7 g_x7;
+static const rc_batch_dev* g_b7 = nullptr;
+static uint32_t g_kicks7 = 0, g_period7 = 1, g_rng7 = 12345;
+// period p > 1: the helper runs at about one in p of its chances (pseudo-random),
+// so answers, input chunks and ring space arrive late, as on the GPU
+extern "C" void lane_host_dec7_period(uint32_t p) { g_period7 = p ? p : 1; }
+namespace {
+static void dec7_host_kick()
+{
+    ++g_kicks7;
+    bool fin = false;
+    g_rng7 = g_rng7 * 1103515245u + 12345u;
+    if (g_period7 <= 1 || (g_rng7 >> 16) % g_period7 == 0) store7_iter(g_x7, g_tab7, g_s7, fin);
+    g_rng7 = g_rng7 * 1103515245u + 12345u;
+    if (g_period7 <= 1 || (g_rng7 >> 16) % g_period7 == 0) help7_iter(*g_b7, g_x7, g_tab7, g_h7, fin);
+}
+}  // namespace
+#endif
+
 #define REGION_BYTES rc_hip_lane3_region_bytes
 #define COMPRESS_ONE compress_one3
 #define DECOMPRESS_ONE decompress_one3
@@ -70,6 +111,26 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     // the record-light decoder and its check; a packet it leaves or that fails the check goes to the lanes
     if (decompress) {
         decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6);
+        if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
+            counters[3] = 1; g_dec6_unverified++;
+        }
+        if (!counters[3] && (claims[0] >> 31)) *out_len = 0;
+        if (!counters[3]) return 0;
+    }
+#endif
+
+#ifdef DEC7
+    // the record-light decoder with its helper, and the check, as on the GPU
+    if (decompress) {
+        g_b7 = &b;
+        g_x7 = lds7(g_lds7, 0, 1);
+        *reinterpret_cast<uint2*>(g_x7.mctl) = make_uint2(0u, kNoPkt7);
+        g_x7.hctl[0] = 0u;
+        g_x7.hctl[1] = 0u;
+        help7_init(g_h7);
+        g_s7.tail = 0u;
+        Main7 m = {0u, 0u, 0u, 0u};
+        main7_packet(b, ws, 0, g_x7, m);
         if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
             counters[3] = 1; g_dec6_unverified++;
         }

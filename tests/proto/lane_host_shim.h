@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <algorithm>
 #define __device__
+#define __host__
 #define __forceinline__ inline
 struct uint4 { uint32_t x, y, z, w; };
 struct uint2 { uint32_t x, y; };

@@ -21,6 +21,8 @@ VARIANTS = {
     # default: two-pass encoder (rc_enc2.hip) and record-light decoder with its
     # check (rc_dec6.hip) in front of the v3 lane kernels (rc_lane3.hip)
     "lane3": {"ENET_RC_KERNEL": "lane3"},
+    # the record-light decoder with helper wavefronts (rc_dec7.hip) instead
+    "dec7": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "7"},
     # the bucket-history decoder (rc_dec4.hip) in front of the lane kernels instead
     "dec4": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "4"},
     # the two-pass encoder's slow paths forced (every position exceptional,
