@@ -174,7 +174,13 @@ static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
             hipDeviceSynchronize();
             if (c->ws.enc2_wide) hipFree(c->ws.enc2_wide);
             c->ws.enc2_wide = NULL; c->ws.enc2_wide_cap = 0;
-            if (hipMalloc(&c->ws.enc2_wide, wwant) != hipSuccess) return -1;
+            /* the wide mode is optional: without its stream (an allocation that
+               failed) low-entropy packets take the lane kernels */
+            if (hipMalloc(&c->ws.enc2_wide, wwant) != hipSuccess) {
+                c->ws.enc2_wide = NULL;
+                (void) hipGetLastError();
+                return 0;
+            }
             c->ws.enc2_wide_cap = wwant;
         }
     }
@@ -559,9 +565,12 @@ static int pack_reserve(rc_ctx *c, size_t bytes, size_t blocks)
  * 80 MB the first time, microseconds after), so that a host batch skips the
  * copy through pinned staging.  1: registered here (host_unpin after the
  * transfers), 2: the caller's memory is page-locked already (its own
- * hipHostMalloc / hipHostRegister, e.g. a long-lived receive buffer): DMA'd
- * directly, left registered; 0: not usable (the call failed) -- the staging
- * path then. */
+ * hipHostMalloc / hipHostRegister, e.g. a long-lived receive buffer) and the
+ * whole range lies inside that one allocation or registration: DMA'd
+ * directly, left registered; 0: not usable (the call failed, or the range
+ * only touches memory some other caller registered, whose registration may
+ * end during our transfer) -- the staging path then.  The batch calls on
+ * host pointers page-lock caller memory for the length of the call. */
 static int host_pin(const void *p, size_t bytes)
 {
     static int off = -1;
@@ -569,11 +578,14 @@ static int host_pin(const void *p, size_t bytes)
     if (off || bytes < (1u << 20)) return 0;
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost) {
-        /* page-locked by the caller: usable if the whole range is */
-        hipPointerAttribute_t ae;
-        if (hipPointerGetAttributes(&ae, (const uint8_t *) p + bytes - 1) == hipSuccess &&
-            ae.type == hipMemoryTypeHost)
+        /* page-locked by the caller: usable only if one allocation holds the range */
+        void *start = NULL;
+        size_t size = 0;
+        if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t) p) == hipSuccess &&
+            hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t) p) == hipSuccess &&
+            (uintptr_t) p >= (uintptr_t) start && (uintptr_t) p + bytes <= (uintptr_t) start + size)
             return 2;
+        (void) hipGetLastError();
         return 0;
     }
     (void) hipGetLastError();
@@ -925,7 +937,10 @@ int enet_rc_compress_gather_batch_host(void *context, const ENetBuffer *buffers,
     uint32_t *len = (uint32_t *) malloc(n * sizeof(uint32_t));
     if (!len) return (int) hipErrorOutOfMemory;
     for (size_t i = 0; i < n; ++i) {
-        const size_t l = first[i + 1] >= first[i] ? gather_len(buffers + first[i], first[i + 1] - first[i]) : 0;
+        /* the lists must not run backwards: the copy threads flatten
+           first[i + 1] - first[i] buffers of packet i */
+        if (first[i + 1] < first[i]) { free(len); return (int) hipErrorInvalidValue; }
+        const size_t l = gather_len(buffers + first[i], first[i + 1] - first[i]);
         if (l > 0xFFFFFFFFu) { free(len); return (int) hipErrorInvalidValue; }
         len[i] = (uint32_t) l;
     }

@@ -1,5 +1,6 @@
 // rc_lane_common.h -- per-lane building blocks shared by the lane kernels
-// (rc_lane.hip: model v2; rc_lane3.hip: model v3): the order-0 model in LDS,
+// (rc_lane3.hip) and the fast decoders (rc_dec4.hip, rc_dec6.hip, rc_dec7.hip)
+// and encoder (rc_enc2.hip): the order-0 model in LDS,
 // byte-parallel (SWAR) helpers, dense 256-symbol context blocks, the byte
 // streams and the range coder.  Semantics follow compress.c (cited per item).
 #pragma once

@@ -1,5 +1,5 @@
 // TEST ONLY: host build of the lane kernels' per-lane compress/decompress
-// (rc_lane3.hip) and, with -DDEC4, the bucket-history decoder (rc_dec4.hip).
+// (rc_lane3.hip) and, with -DDEC4 / -DDEC6 / -DDEC7, the fast decoder in front of them.
 #define RC_LANE_HOST_TEST 1
 #include <stdlib.h>
 #include <string.h>
@@ -46,9 +46,7 @@ static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n)
 // the decoder's two sides for one lane: the main lane runs the packet, and the
 // helper runs one pass after every main step and whenever the main lane waits
 static uint8_t g_lds7[lds7_bytes(1)] __attribute__((aligned(16)));
-static uint8_t g_tab7[RC_DEC6_TAB_BYTES] __attribute__((aligned(16)));   // bucket records (never cleared)
 static Help7 g_h7;
-static Store7 g_s7;
 static Lds7 g_x7;
 static const rc_batch_dev* g_b7 = nullptr;
 static uint32_t g_kicks7 = 0, g_period7 = 1, g_rng7 = 12345;
@@ -61,9 +59,7 @@ static void dec7_host_kick()
     ++g_kicks7;
     bool fin = false;
     g_rng7 = g_rng7 * 1103515245u + 12345u;
-    if (g_period7 <= 1 || (g_rng7 >> 16) % g_period7 == 0) store7_iter(g_x7, g_tab7, g_s7, fin);
-    g_rng7 = g_rng7 * 1103515245u + 12345u;
-    if (g_period7 <= 1 || (g_rng7 >> 16) % g_period7 == 0) help7_iter(*g_b7, g_x7, g_tab7, g_h7, fin);
+    if (g_period7 <= 1 || (g_rng7 >> 16) % g_period7 == 0) help7_iter(*g_b7, g_x7, g_h7, fin);
 }
 }  // namespace
 #endif
@@ -126,10 +122,8 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
         g_x7 = lds7(g_lds7, 0, 1);
         *reinterpret_cast<uint2*>(g_x7.mctl) = make_uint2(0u, kNoPkt7);
         g_x7.hctl[0] = 0u;
-        g_x7.hctl[1] = 0u;
         help7_init(g_h7);
-        g_s7.tail = 0u;
-        Main7 m = {0u, 0u, 0u, 0u};
+        Main7 m = {0u, 0u, 0u};
         main7_packet(b, ws, 0, g_x7, m);
         if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
             counters[3] = 1; g_dec6_unverified++;

@@ -19,7 +19,8 @@ SO = os.path.join(ROOT, "tests", "proto", "liblanehost.so")
 
 # v3: the lane kernels alone; v4: the bucket-history decoder (rc_dec4.hip) in front of them;
 # v6: the record-light decoder (rc_dec6.hip) and its check in front of them, as on the GPU;
-# v7: rc_dec7.hip's main and helper sides (the helper run after every main step) and the check
+# v7: rc_dec7.hip's main side and a scalar restatement of its serving side (run after every
+# main step, or at random late) and the check
 @pytest.fixture(scope="module", params=["v3", "v4", "v6", "v7"])
 def lane(request):
     so = SO.replace("liblanehost", "liblanehost" + request.param[1])

@@ -57,17 +57,20 @@ def main():
     res["stalled lanes per loop step"] = round(b[16 + 9] / max(b[16 + 8], 1), 2)
     res["stepping lanes per loop step"] = round(b[16 + 10] / max(b[16 + 8], 1), 2)
     res["idle loop steps per wave"] = round(b[16 + 11] / max(waves, 1), 1)
-    res["ring-full lanes per loop step"] = round(b[16 + 6] / max(b[16 + 8], 1), 2)
     res["done lanes per loop step"] = round(b[16 + 7] / max(b[16 + 8], 1), 2)
     res["lanes with c used up per loop step"] = round(b[16 + 5] / max(b[16 + 8], 1), 2)
     hw = waves   # one helper wavefront per main wavefront
     res["helper passes per wave"] = round(b[32] / hw, 1)
     res["helper idle passes per wave"] = round(b[33] / hw, 1)
     res["helper cycles per wave"] = round(b[34] / hw, 1)
-    res["helper lanes served per wave"] = round(b[35] / hw, 1)
+    res["helper requests served per wave"] = round(b[35] / hw, 1)
     res["helper serve cycles per wave"] = round(b[36] / hw, 1)
     res["helper ring passes per wave"] = round(b[37] / hw, 1)
-    res["helper record-load wait cycles per wave"] = round(b[38] / hw, 1)
+    res["helper cycles to the loads' arrival per wave"] = round(b[38] / hw, 1)
+    res["helper compaction cycles per wave"] = round(b[39] / hw, 1)
+    res["helper decode cycles per wave"] = round(b[40] / hw, 1)
+    res["helper chain iterations per wave"] = round(b[41] / hw, 1)
+    res["ring-full lanes per loop step"] = None
     print(json.dumps({"dec7": res, "roundtrip_ok": ok, "lanes_handed_on": handed, "workload": wl}, indent=1))
 
 
