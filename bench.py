@@ -42,7 +42,8 @@ def parse():
     p.add_argument("--packets", type=int, default=65536)
     p.add_argument("--size", type=int, default=1200)
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="cpu_baseline threads (0: every CPU in this process's affinity mask)")
     p.add_argument("--no-pcie", action="store_true")
     p.add_argument("--no-crc", action="store_true", help="skip the CRC-32 kernel line")
     p.add_argument("--no-rccl", action="store_true")
@@ -586,9 +587,11 @@ def dominant_kernel(decompress, handed_off=0, n=1):
     if os.environ.get("ENET_RC_KERNEL", "lane3") == "wave":
         return "rc_decompress_wave" if decompress else "rc_compress_wave"
     if decompress:
-        dk = os.environ.get("ENET_RC_DEC", "6")
+        dk = os.environ.get("ENET_RC_DEC", "8")
+        if os.environ.get("ENET_RC_LANES", "64") != "64" and dk == "8":
+            dk = "6"
         fast = os.environ.get("ENET_RC_DEC4", "1") != "0" and dk != "0"
-        name = "rc_decompress_dec4" if dk == "4" else "rc_decompress_dec6"
+        name = {"4": "rc_decompress_dec4", "6": "rc_decompress_dec6", "7": "rc_decompress_dec7"}.get(dk, "rc_decompress_dec6s")
         return name if fast and 2 * handed_off < n else "rc_decompress_lane3"
     if os.environ.get("ENET_RC_ENC2", "1") == "0" or 2 * handed_off >= n:
         return "rc_compress_lane3"
@@ -614,15 +617,46 @@ def measured_traffic(kernel, workload, packets):
     return k.get("hbm_bytes_per_launch"), "profiles/traffic_latest.json (" + t.get("source", "") + ")"
 
 
+def cpu_threads_available():
+    """The host CPUs this process may use: its affinity mask, capped by the
+    cgroup's CPU quota (cpu.max) -- the GPU box's CPU share, not
+    os.cpu_count()'s whole machine."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts and parts[0] != "max":
+                n = min(n, max(1, int(int(parts[0]) // int(parts[1]))))
+            elif path.endswith("cfs_quota_us") and parts and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as g:
+                    n = min(n, max(1, int(parts[0]) // int(g.read().split()[0])))
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    return n
+
+
 def cpu_baseline(d, o, l, threads):
-    """Reference compress.c (oracle/_ref, built from the reference sources) or,
-    if absent, the oracle restatement, timed round trip on host cores: on one
-    thread over a bounded sample (the first 8192 packets of the batch), and
-    on `threads` threads (one context each; the GPU box's CPU share is 16,
-    os.cpu_count() there reports the whole machine) over the whole batch."""
+    """Reference compress.c (oracle/_ref/libenet_ref.so, built from the
+    reference sources by `make -C oracle ref` in the build container and
+    shipped with the tree), timed round trip on host cores: on one thread over
+    a bounded sample (the first 8192 packets of the batch), and on `threads`
+    threads (default: every CPU in this process's affinity mask; one context
+    each) over the whole batch.  ENET_RC_CPU_BASELINE=port times the oracle
+    restatement instead; without either the leg fails rather than silently
+    timing something else."""
     from oracle.pyoracle import cpu_roundtrip, have_reference
-    kind = "reference" if have_reference() else "port"
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    want = os.environ.get("ENET_RC_CPU_BASELINE", "reference")
+    if want == "reference" and not have_reference():
+        raise RuntimeError("oracle/_ref/libenet_ref.so is missing: build it with `make -C oracle ref` "
+                           "(or set ENET_RC_CPU_BASELINE=port to time the restatement)")
+    kind = "reference" if want == "reference" else "port"
+    avail = cpu_threads_available()
+    threads = max(1, min(threads or avail, avail))
     try:
         model = [x for x in open("/proc/cpuinfo").read().splitlines() if x.startswith("model name")][0].split(":")[1].strip()
     except Exception:
@@ -644,7 +678,7 @@ def cpu_baseline(d, o, l, threads):
                       f"per thread; single_thread: its first {single['packets']} packets on one thread",
             "compress_GiBps": multi["compress_GiBps"], "decompress_GiBps": multi["decompress_GiBps"],
             "mismatches": multi["mismatches"] + single["mismatches"], "single_thread": single,
-            "host_cpus_visible": os.cpu_count(), "cpu": model}
+            "host_cpus_available": avail, "host_cpus_visible": os.cpu_count(), "cpu": model}
 
 
 if __name__ == "__main__":

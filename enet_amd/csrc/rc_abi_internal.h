@@ -58,10 +58,12 @@ typedef struct {
     void     *enc2_wide;
     uint64_t  enc2_wide_cap;  /* bytes */
     uint32_t *enc2_wlist;     /* [n_cap] */
-    /* the fast decoder in front of the v3 lane decoder: 6 = record-light on one wavefront per
-       SIMD (rc_dec6.hip, default), 7 = record-light with helper wavefronts (rc_dec7.hip;
-       ENET_RC_DEC=7 with lane_active == 64), 4 = bucket-history (rc_dec4.hip; ENET_RC_DEC=4),
-       0 = none (ENET_RC_DEC4=0 or ENET_RC_DEC=0);
+    /* the fast decoder in front of the v3 lane decoder: 8 = record-light with its input through
+       LDS slots a helper wavefront refills (rc_dec6.hip rc_decompress_dec6s, default with
+       lane_active == 64), 6 = the same loading its own input (rc_decompress_dec6; ENET_RC_DEC=6,
+       or lane_active != 64), 7 = record-light with serving wavefronts (rc_dec7.hip;
+       ENET_RC_DEC=7), 4 = bucket-history (rc_dec4.hip; ENET_RC_DEC=4), 0 = none (ENET_RC_DEC4=0
+       or ENET_RC_DEC=0);
        the packets it leaves go to enc2_list / counters[3] */
     uint32_t  dec4;
     /* rc_dec6.hip: per packet, the positions the decoder took to start a new bigram (its

@@ -61,6 +61,7 @@
 #include "lane_host_shim.h"   // tests/proto: host build of the per-lane logic (test only)
 #endif
 #include <stdint.h>
+#include <type_traits>
 
 #include "rc_abi_internal.h"
 #include "rc_udiv.h"
@@ -68,6 +69,7 @@
 #include "rc_root3.h"
 #include "rc_bucket4.h"
 #include "rc_dec6_rare.h"
+#include "rc_slot.h"
 
 namespace {
 
@@ -86,16 +88,29 @@ constexpr uint32_t kDummy6 = 12288;              // the slot of the stores that 
 
 DEV void bail6(const rc_workspace_dev& ws, uint32_t pkt) { bail(ws, pkt); }
 
+// Src: ByteSrc (the stream's chunks loaded by the lane, rc_decompress_dec6) or
+// SlotSrc (through the LDS slot a helper wavefront refills, rc_slot.h,
+// rc_decompress_dec6s).
+template <class Src>
 DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* root,
-                         uint8_t* stats, uint8_t* tab)
+                         uint8_t* stats, uint8_t* tab, Src& in)
 {
+    constexpr bool kSlot = std::is_same<Src, SlotSrc>::value;
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
     if (len == 0) { bt.out_len[pkt] = 0; ws.claims[pkt] = 0; return; }     // compress.c:513
     ByteSink o;
     sink_init(o, bt.out + bt.out_off[pkt], cap);
-    ByteSrc in;
-    src_init(in, bt.in + bt.in_off[pkt], len);
+    uint32_t code;
+    if constexpr (kSlot) {
+        code = slot_init(in, bt.in + bt.in_off[pkt], len, pkt);
+    } else {
+        src_init(in, bt.in + bt.in_off[pkt], len);
+        code = static_cast<uint32_t>(in.la >> 32);            // compress.c:344-350 (0 past the end)
+        in.la <<= 32;
+        in.na -= 4;
+        src_refill(in, true);
+    }
     Root R;
     root3_clear<false>(root, R);
     {
@@ -106,10 +121,6 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     uint32_t rtot = 1 + 256;
     double rrt = rcp64(rtot);
     uint32_t low = 0, range = ~0u;
-    uint32_t code = static_cast<uint32_t>(in.la >> 32);            // compress.c:344-350 (0 past the end)
-    in.la <<= 32;
-    in.na -= 4;
-    src_refill(in, true);
 
     uint32_t order = 0, a = 0, p = 0, nodes = 1, claims = 0, x0 = 0;
     uint32_t hl[4] = {0u, 0u, 0u, 0u}, nh = 0;   // elements decoded at order 2: p | a << 8 | v << 16
@@ -130,7 +141,14 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     for (;;) {
         {
             // ------------------------------------------------------ a common step
-            src_fill(in, true);
+            uint32_t shc = 0;                                  // (SlotSrc: h_ctl and the slot, used at the end)
+            uint4 ssl = make_uint4(0u, 0u, 0u, 0u);
+            if constexpr (kSlot) {
+                shc = *in.hctl;
+                ssl = *reinterpret_cast<const uint4*>(in.slot);
+            } else {
+                src_fill(in, true);
+            }
             sink_flush(o);
             const bool go = !done && !stall;
 #ifdef DEC6_STATS_PREFETCH
@@ -215,7 +233,8 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             }
 #endif
             PROF(0)
-            src_adv(in);
+            if constexpr (kSlot) slot_step_end(in, ssl, shc);
+            else src_adv(in);
             PROF(5)
         }
         ++s;
@@ -224,7 +243,14 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // ------------------------------------------------------------ rare phase
         for (uint32_t it = 0; it < kRareIters6 && any_lane(stall && !done); ++it) {
             const bool rs = stall && !done;
-            src_fill(in, true);
+            uint32_t shc = 0;
+            uint4 ssl = make_uint4(0u, 0u, 0u, 0u);
+            if constexpr (kSlot) {
+                shc = *in.hctl;
+                ssl = *reinterpret_cast<const uint4*>(in.slot);
+            } else {
+                src_fill(in, true);
+            }
             sink_flush(o);
 #ifndef DEC6_NO_DRAIN
             __builtin_amdgcn_s_waitcnt(0);            // (the blind stores of this lane's records)
@@ -326,7 +352,8 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             repeat = sym ? !nb : repeat;
             // the step after a hit has a visited order-2 context: another rare step
             stall = rs ? (sym && !lv && !fl && order >= 2 && repeat) : stall;
-            src_adv(in);
+            if constexpr (kSlot) slot_step_end(in, ssl, shc);
+            else src_adv(in);
             PROF(3)
         }
         // (nothing of the rare phase left in flight: a record load pending on some
@@ -372,10 +399,52 @@ void rc_decompress_dec6(rc_batch_dev b, rc_workspace_dev ws)
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * RC_DEC6_TAB_BYTES;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
+    ByteSrc in;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
         const uint32_t pkt = order ? order[i] : i;
-        decompress_one6(b, ws, pkt, root, stats, tab);
+        decompress_one6(b, ws, pkt, root, stats, tab, in);
     }
+}
+
+// The same with the lanes' input through LDS (rc_slot.h): waves 0-3 decode,
+// wave w + 4 (on wave w's SIMD) keeps their slots filled.  LDS per lane:
+// root | slot (the root's pad) | bucket bytes, then m_ctl / m_pkt, h_ctl.
+constexpr uint32_t kLanes6s = 256;
+extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_dev b, rc_workspace_dev ws)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = threadIdx.x >> 6;
+    const bool helper = wave >= 4;
+    const uint32_t L = (wave & 3) * 64 + (threadIdx.x & 63);
+    uint8_t* root = smem + L * kLds6;
+    uint8_t* stats = root + kStats6;
+    uint8_t* slotp = root + 256;
+    uint32_t* mctl = reinterpret_cast<uint32_t*>(smem + kLanes6s * kLds6) + 2 * L;
+    uint32_t* hctl = reinterpret_cast<uint32_t*>(smem + kLanes6s * kLds6 + 8 * kLanes6s) + L;
+    const uint32_t slot = blockIdx.x * kLanes6s + L;
+    if (!helper) *reinterpret_cast<uint2*>(mctl) = make_uint2(0u, slot < b.n ? kNoPktS : kFinS);
+    else *hctl = 0u;
+    __syncthreads();
+    if (helper) {
+        SlotHelp h;
+        slot_help_init(h);
+        for (;;) {
+            bool fin = false;
+            const bool busy = slot_help_iter(b, mctl, hctl, slotp, h, fin);
+            if (fin) break;
+            if (!busy) __builtin_amdgcn_s_sleep(2);
+        }
+        return;
+    }
+    uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * RC_DEC6_TAB_BYTES;
+    const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
+    SlotSrc in;
+    in.gen = 0; in.mctl = mctl; in.hctl = hctl; in.slot = slotp;
+    for (uint32_t i = slot; i < b.n; i += gridDim.x * kLanes6s) {
+        const uint32_t pkt = order ? order[i] : i;
+        decompress_one6(b, ws, pkt, root, stats, tab, in);
+    }
+    mctl[1] = kFinS;
 }
 
 // Counts the distinct bigrams of each packet rc_decompress_dec6 decoded and
@@ -449,6 +518,14 @@ extern "C" int rc_hip_dec6_verify_launch(const rc_batch_dev* b, const rc_workspa
 extern "C" int rc_hip_dec6_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (ws->dec4 == 8 && ws->lane_active == 64) {
+        // (the slot variant: 12 B more per lane for the control words)
+        const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12);
+        hipLaunchKernelGGL(rc_decompress_dec6s, dim3(blocks), dim3(512), lds, st, *b, *ws);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return static_cast<int>(e);
+        return rc_hip_dec6_verify_launch(b, ws, stream);
+    }
     const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kLds6;
     hipLaunchKernelGGL(rc_decompress_dec6, dim3(blocks), dim3(256), lds, st, *b, *ws);
     const hipError_t e = hipGetLastError();

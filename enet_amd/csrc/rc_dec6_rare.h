@@ -155,8 +155,9 @@ DEV uint32_t pval6(const uint32_t* pl, uint32_t j)
 // distinct values: READ, then an escape (false) or the symbol the code selects
 // (true: v, its interval under/count -- coded by the caller).  fail: the
 // code is past the context's symbols (compress.c:416).
+template <class Src>
 DEV bool sub_decode6(const uint32_t* pl, uint32_t g, uint32_t t, uint32_t d, bool en, uint32_t& low,
-                     uint32_t& code, uint32_t& range, ByteSrc& in, uint32_t& v, uint32_t& under, uint32_t& count,
+                     uint32_t& code, uint32_t& range, Src& in, uint32_t& v, uint32_t& under, uint32_t& count,
                      bool& fail)
 {
     const uint32_t esc = kSubEscDelta * d, tot = en ? esc + kSubDelta * t : 1u;

@@ -247,12 +247,14 @@ void *enet_range_coder_create(void)
         c->enc2_wide_on = !(ew && strcmp(ew, "0") == 0);
         c->enc2_stream_max = env_mb_cap("ENET_RC_ENC2_STREAM_MB", ENC2_STREAM_MAX);
         c->enc2_wide_max = env_mb_cap("ENET_RC_ENC2_WIDE_MB", ENC2_WIDE_MAX);
-        /* the fast decoder: rc_dec6.hip unless ENET_RC_DEC=7 (rc_dec7.hip, with
-           64 packets per wavefront) or ENET_RC_DEC=4 (rc_dec4.hip); none with
-           ENET_RC_DEC=0 or ENET_RC_DEC4=0 */
+        /* the fast decoder: rc_dec6.hip with its input through LDS slots (8,
+           rc_decompress_dec6s; 64 packets per wavefront) unless ENET_RC_DEC=6
+           (its own chunk loads, rc_decompress_dec6), 7 (rc_dec7.hip) or 4
+           (rc_dec4.hip); none with ENET_RC_DEC=0 or ENET_RC_DEC4=0 */
         const char *d4 = getenv("ENET_RC_DEC4");
         const char *dk = getenv("ENET_RC_DEC");
-        c->ws.dec4 = 6;
+        c->ws.dec4 = c->ws.lane_active == 64 ? 8 : 6;
+        if (dk && strcmp(dk, "6") == 0) c->ws.dec4 = 6;
         if (dk && strcmp(dk, "7") == 0 && c->ws.lane_active == 64) c->ws.dec4 = 7;
         if (dk && strcmp(dk, "4") == 0) c->ws.dec4 = 4;
         if ((dk && strcmp(dk, "0") == 0) || (d4 && strcmp(d4, "0") == 0)) c->ws.dec4 = 0;

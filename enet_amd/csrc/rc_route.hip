@@ -139,7 +139,7 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
         // the fast decoder takes what it can (rc_dec6.hip, or rc_dec4.hip);
         // the lanes decode only the packets it lists
         const int rc = ws->dec4 == 7 ? rc_hip_dec7_launch(b, &w, blocks, stream)
-                     : ws->dec4 == 6 ? rc_hip_dec6_launch(b, &w, blocks, stream)
+                     : (ws->dec4 == 6 || ws->dec4 == 8) ? rc_hip_dec6_launch(b, &w, blocks, stream)
                                      : rc_hip_dec4_launch(b, &w, blocks, stream);
         if (rc != 0) return rc;
         w.sub_list = ws->enc2_list;

@@ -1,0 +1,228 @@
+// rc_slot.h -- a decoder lane's compressed stream through LDS, refilled by a
+// helper wavefront on the same SIMD (rc_dec6.hip's rc_decompress_dec6s).
+//
+// rc_lane_common.h's ByteSrc reloads the next 16-B chunk of the stream with a
+// global load every step, and the step after waits for it: vmcnt retires
+// loads and stores in order, so the reload waits behind the step's record and
+// output stores (rc_dec6: 0.78 k of 5.5 k cycles per packet-step).  Here the
+// lane's next chunk sits in a 16-B LDS slot, put there by lane l of a helper
+// wavefront (wave w + 4 of the workgroup, which shares wave w's SIMD and
+// otherwise sleeps): the decoding lane takes it when its current chunk is used
+// up and asks for the one after.  Past the packet's first two chunks the
+// decoding wavefront issues no global load for its input at all.
+//
+// Words (each written by one side only):
+//   m_ctl = wanted chunk (12 bits) << 16 | packet generation (4 bits) << 28,
+//   m_pkt = the packet (kNoPktS before the first, kFinS when the lane is done),
+//   h_ctl = the slot's chunk << 16 | its generation << 28.
+// The decoding side waits only for the helper, the helper only for its own
+// loads: no deadlock.
+#pragma once
+
+namespace {
+
+constexpr uint32_t kFinS = 0xFFFFFFFFu;
+constexpr uint32_t kNoPktS = 0xFFFFFFFEu;
+
+#ifndef RC_LANE_HOST_TEST
+#define SLOT_IDLE() __builtin_amdgcn_s_sleep(1)
+#else
+static void slot_host_kick();     // tests/proto/lane_host.cpp: one helper pass
+#define SLOT_IDLE() slot_host_kick()
+#endif
+
+struct SlotSrc {
+    uint64_t la;                  // lookahead: the next na bytes, first in bits 63..56
+    uint32_t na, q, j, lo15;      // bytes in la; next dword of c; c is chunk j; packet start & 15
+    uint4 c;
+    uint32_t want, gen;
+    uint32_t* mctl;               // [0] m_ctl, [1] m_pkt
+    const uint32_t* hctl;
+    const uint8_t* slot;
+};
+
+DEV void slot_publish(const SlotSrc& s) { s.mctl[0] = ((s.want & 0xFFFu) << 16) | (s.gen << 28); }
+
+// one dword into the lookahead where it has room for it and c has one
+DEV void slot_fill(SlotSrc& s, bool en)
+{
+    const bool need = en && s.na <= 4 && s.q < 4;
+    const uint32_t d = bswap(sel4(s.q, s.c));
+    const uint32_t sh = need ? 32 - 8 * s.na : 0u;
+    s.la |= need ? (static_cast<uint64_t>(d) << sh) : 0ull;
+    s.na += need ? 4u : 0u;
+    s.q += need ? 1u : 0u;
+}
+
+// c used up: the slot's chunk if it is chunk j + 1 (hc: h_ctl as read, sl: the slot)
+DEV void slot_take(SlotSrc& s, const uint4& sl, uint32_t hc, bool en)
+{
+    const bool ready = ((hc >> 16) & 0xFFFu) == ((s.j + 1) & 0xFFFu) && (hc >> 28) == s.gen;
+    const bool t = en && s.q == 4 && ready;
+    s.c.x = t ? sl.x : s.c.x; s.c.y = t ? sl.y : s.c.y; s.c.z = t ? sl.z : s.c.z; s.c.w = t ? sl.w : s.c.w;
+    s.q = t ? 0u : s.q;
+    s.j += t ? 1u : 0u;
+    s.want = t ? s.j + 1 : s.want;
+}
+
+// the end of a step: the next chunk if the slot holds it, the lookahead topped up
+DEV void slot_step_end(SlotSrc& s, const uint4& sl, uint32_t hc)
+{
+    slot_take(s, sl, hc, s.q == 4);
+    slot_fill(s, true);
+    slot_fill(s, true);
+    slot_publish(s);
+#ifdef RC_LANE_HOST_TEST
+    slot_host_kick();
+#endif
+}
+
+
+// at least one byte in the lookahead where `en` (the rare paths): from c, or
+// from the slot once the helper has put the next chunk there
+DEV void slot_need1(SlotSrc& s, bool en)
+{
+    bool w = en && s.na == 0 && s.q == 4;
+    while (rare_lane(w)) {
+        const uint32_t hc = *s.hctl;
+        const uint4 sl = *reinterpret_cast<const uint4*>(s.slot);
+        slot_take(s, sl, hc, w);
+        slot_publish(s);
+        w = w && s.q == 4;
+        if (any_lane(w)) SLOT_IDLE();
+    }
+    slot_fill(s, en && s.na == 0);
+}
+
+DEV uint32_t slot_shift_in(SlotSrc& s, uint32_t code, uint32_t k)
+{
+    const uint32_t t = static_cast<uint32_t>(s.la >> 32);
+    const uint32_t in = static_cast<uint32_t>((static_cast<uint64_t>(t) << (8 * k)) >> 32);
+    s.la = k >= 8 ? 0ull : s.la << (8 * k);
+    s.na -= k;
+    return (code << (8 * k)) | in;
+}
+
+// compress.c:354-371 where `en` (rc_lane_common.h dec_code over the slot source)
+DEV void dec_code(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count, SlotSrc& in,
+                  bool en)
+{
+    low = en ? low + under * range : low;
+    range = en ? range * count : range;
+    const uint32_t k = en ? settled_bytes(low, range) : 0u;
+    const bool fast = k <= in.na;
+    const uint32_t kk = fast ? k : 0u;
+    code = slot_shift_in(in, code, kk);
+    low <<= 8 * kk;
+    range <<= 8 * kk;
+    bool more = en && (!fast || range < kBot);
+    if (rare_lane(more)) {
+        do {
+            const bool carry = (low ^ (low + range)) >= kTop;
+            const bool stop = carry && range >= kBot;
+            more = more && !stop;
+            if (!any_lane(more)) break;
+            range = (more && carry) ? ((0u - low) & (kBot - 1)) : range;
+            slot_need1(in, more);
+            code = slot_shift_in(in, code, more ? 1u : 0u);
+            range = more ? range << 8 : range;
+            low = more ? low << 8 : low;
+        } while (rare_lane(more));
+    }
+}
+
+DEV void dec_code_late(uint32_t& low, uint32_t& code, uint32_t& range, uint32_t under, uint32_t count, SlotSrc& in,
+                       bool en)
+{
+    dec_code(low, code, range, under, count, in, en);
+}
+
+// The packet's first chunks (the decoding lane's only global loads for its
+// input) and the seed (compress.c:344-350): three dwords from the one holding
+// the first byte, so chunks 0 and 1 hold them.  Publishes the packet and the
+// first wanted chunk.
+DEV void slot_adv0(SlotSrc& s, const uint4& c1)
+{
+    const bool adv = s.q == 4 && s.j == 0;
+    s.c.x = adv ? c1.x : s.c.x; s.c.y = adv ? c1.y : s.c.y; s.c.z = adv ? c1.z : s.c.z; s.c.w = adv ? c1.w : s.c.w;
+    s.j += adv ? 1u : 0u;
+    s.q = adv ? 0u : s.q;
+}
+
+DEV uint32_t slot_init(SlotSrc& s, const uint8_t* p, uint32_t len, uint32_t pkt)
+{
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + len;
+    const uintptr_t base = lo & ~static_cast<uintptr_t>(15);
+    const uint4 c0 = chunk_load(lo, hi, base, true);
+    const uint4 c1 = chunk_load(lo, hi, base + 16, true);
+    s.lo15 = static_cast<uint32_t>(lo & 15);
+    const uint32_t sk = static_cast<uint32_t>(lo & 3);
+    s.q = s.lo15 >> 2;
+    s.c = c0;
+    s.j = 0;
+    s.la = static_cast<uint64_t>(bswap(sel4(s.q, s.c)) << (8 * sk)) << 32;
+    s.na = 4 - sk;
+    s.q += 1;
+    slot_adv0(s, c1);
+    slot_fill(s, true);
+    const uint32_t code = static_cast<uint32_t>(s.la >> 32);
+    s.la <<= 32;
+    s.na -= 4;
+    slot_adv0(s, c1);
+    slot_fill(s, true);
+    slot_adv0(s, c1);
+    s.gen = s.gen % 15u + 1u;
+    s.want = s.j + 1;
+    *reinterpret_cast<uint2*>(s.mctl) = make_uint2(((s.want & 0xFFFu) << 16) | (s.gen << 28), pkt);
+    // (settled here: a load pending at the step loop's header makes the compiler
+    // wait for vmcnt(0) at every step)
+    __builtin_amdgcn_s_waitcnt(0);
+    return code;
+}
+
+// ------------------------------------------------------------------ helper
+struct SlotHelp {
+    uint32_t have, hgen, cgen, pub, len;
+    uintptr_t ib;
+};
+
+DEV void slot_help_init(SlotHelp& h) { h.have = 0; h.hgen = 0; h.cgen = 0; h.pub = 0; h.len = 0; h.ib = 0; }
+
+// One pass over the helper's lanes: a new packet's input range, the wanted
+// chunk into the slot, h_ctl.  Returns whether it loaded anything; fin_all:
+// every decoding lane of the wavefront is done.
+DEV bool slot_help_iter(const rc_batch_dev& bt, const uint32_t* mctl, uint32_t* hctl, uint8_t* slot, SlotHelp& h,
+                        bool& fin_all)
+{
+    const uint2 m = *reinterpret_cast<const uint2*>(mctl);
+    const bool fin = m.y == kFinS;
+    const uint32_t want = (m.x >> 16) & 0xFFFu, mgen = m.x >> 28;
+    const bool np = !fin && m.y != kNoPktS && mgen != h.cgen;
+    if (any_lane(np)) {
+        if (np) {
+            h.len = bt.in_len[m.y];
+            h.ib = reinterpret_cast<uintptr_t>(bt.in + bt.in_off[m.y]);
+            h.cgen = mgen;
+        }
+    }
+    const bool inq = !fin && h.cgen != 0 && mgen == h.cgen && (want != h.have || h.hgen != h.cgen);
+    bool busy = false;
+    if (any_lane(inq)) {
+        busy = true;
+        const uintptr_t base = h.ib & ~static_cast<uintptr_t>(15);
+        const uint4 c = chunk_load(h.ib, h.ib + h.len, base + 16 * static_cast<uintptr_t>(want), inq);
+        if (inq) *reinterpret_cast<uint4*>(slot) = c;
+        h.have = inq ? want : h.have;
+        h.hgen = inq ? h.cgen : h.hgen;
+    }
+    const uint32_t hc = (h.have << 16) | (h.hgen << 28);
+    if (hc != h.pub) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the slot written before the word that announces it
+        *hctl = hc;
+        h.pub = hc;
+    }
+    fin_all = !any_lane(!fin);
+    return busy;
+}
+
+}  // namespace

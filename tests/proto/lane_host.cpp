@@ -10,6 +10,18 @@
 #ifdef DEC6
 #include "../../enet_amd/csrc/rc_dec6.hip"
 static uint8_t g_lds6[528] __attribute__((aligned(16)));   // root + bucket bytes
+// -DDEC6S: the lane's input through the LDS slot (rc_slot.h), the helper's
+// pass run after every step and whenever the lane waits
+static uint32_t g_ctl6s[3];
+static SlotHelp g_sh6;
+static const rc_batch_dev* g_b6s = nullptr;
+namespace {
+static void slot_host_kick()
+{
+    bool fin = false;
+    if (g_b6s) slot_help_iter(*g_b6s, g_ctl6s, g_ctl6s + 2, g_lds6 + 256, g_sh6, fin);
+}
+}  // namespace
 static uint8_t g_tab6[RC_DEC6_TAB_BYTES] __attribute__((aligned(16)));   // bucket records (never cleared)
 
 // rc_dec6_verify on the host: distinct bigrams of the output
@@ -106,7 +118,18 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
 #ifdef DEC6
     // the record-light decoder and its check; a packet it leaves or that fails the check goes to the lanes
     if (decompress) {
-        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6);
+#ifndef DEC6S
+        ByteSrc src6;
+        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, src6);
+#else
+        g_b6s = &b;
+        g_ctl6s[0] = 0u; g_ctl6s[1] = kNoPktS; g_ctl6s[2] = 0u;
+        slot_help_init(g_sh6);
+        SlotSrc src6;
+        src6.gen = 0; src6.mctl = g_ctl6s; src6.hctl = g_ctl6s + 2; src6.slot = g_lds6 + 256;
+        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, src6);
+        g_b6s = nullptr;
+#endif
         if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
             counters[3] = 1; g_dec6_unverified++;
         }

@@ -19,8 +19,11 @@ torch = pytest.importorskip("torch")
 
 VARIANTS = {
     # default: two-pass encoder (rc_enc2.hip) and record-light decoder with its
-    # check (rc_dec6.hip) in front of the v3 lane kernels (rc_lane3.hip)
+    # check, its input through LDS slots (rc_dec6.hip rc_decompress_dec6s, rc_slot.h),
+    # in front of the v3 lane kernels (rc_lane3.hip)
     "lane3": {"ENET_RC_KERNEL": "lane3"},
+    # rc_dec6.hip loading its own input
+    "dec6": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "6"},
     # the record-light decoder with helper wavefronts (rc_dec7.hip) instead
     "dec7": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "7"},
     # the bucket-history decoder (rc_dec4.hip) in front of the lane kernels instead

@@ -21,16 +21,19 @@ SO = os.path.join(ROOT, "tests", "proto", "liblanehost.so")
 # v6: the record-light decoder (rc_dec6.hip) and its check in front of them, as on the GPU;
 # v7: rc_dec7.hip's main side and a scalar restatement of its serving side (run after every
 # main step, or at random late) and the check
-@pytest.fixture(scope="module", params=["v3", "v4", "v6", "v7"])
+# v6s: rc_dec6.hip with its input through the LDS slot (rc_slot.h; the helper run after every step)
+@pytest.fixture(scope="module", params=["v3", "v4", "v6", "v6s", "v7"])
 def lane(request):
-    so = SO.replace("liblanehost", "liblanehost" + request.param[1])
+    so = SO.replace("liblanehost", "liblanehost" + request.param[1:])
     csrc = os.path.join(ROOT, "enet_amd", "csrc")
     src = [os.path.join(ROOT, "tests", "proto", "lane_host.cpp")] + \
-        [os.path.join(csrc, f) for f in ("rc_lane3.hip", "rc_dec4.hip", "rc_dec6.hip", "rc_dec7.hip", "rc_dec6_rare.h", "rc_bucket4.h",
+        [os.path.join(csrc, f) for f in ("rc_lane3.hip", "rc_dec4.hip", "rc_dec6.hip", "rc_dec7.hip", "rc_dec6_rare.h",
+                                         "rc_slot.h", "rc_bucket4.h",
                                          "rc_lane_common.h", "rc_root3.h")]
     if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in src):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared"] +
-                              {"v3": [], "v4": ["-DDEC4"], "v6": ["-DDEC6"], "v7": ["-DDEC7"]}[request.param] +
+                              {"v3": [], "v4": ["-DDEC4"], "v6": ["-DDEC6"], "v6s": ["-DDEC6", "-DDEC6S"],
+                               "v7": ["-DDEC7"]}[request.param] +
                               ["-I", csrc, "-I", os.path.join(ROOT, "tests", "proto"), "-o", so, src[0]])
     lib = C.CDLL(so)
     lib.lane_host_run.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
@@ -79,7 +82,7 @@ def test_lane_logic_decompress_fixtures(lane):
         if c["ret"]:
             assert r[1] == c["expect"]
     assert 0 < exact < 2000
-    if lane.version in ("v4", "v6", "v7"):     # most fixtures are garbage or low-entropy: those are left to the lanes
+    if lane.version in ("v4", "v6", "v6s", "v7"):     # most fixtures are garbage or low-entropy: those are left to the lanes
         assert 0 < lane.left < len(cases) - 1000, (lane.left, len(cases))
 
 
