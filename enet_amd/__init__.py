@@ -19,7 +19,7 @@ from typing import Optional, Sequence
 from ._lib import ENetBuffer, get_lib
 
 __all__ = ["RangeCoder", "MultiCoder", "compress_batch", "decompress_batch", "get_lib", "ENetBuffer",
-           "multi_split"]
+           "multi_split", "multi_plan"]
 
 
 class RangeCoder:
@@ -247,6 +247,30 @@ def multi_split(in_len, parts: int):
     if rc != 0:
         raise ValueError("enet_rc_multi_split: bad arguments")
     return first
+
+
+def multi_plan(in_len, in_off, out_off, out_cap, parts: int, device: bool = False):
+    """enet_rc_multi_plan (host arrays) or, device=True, enet_rc_multi_plan_device
+    (CUDA tensors: uint32/int32 lengths and caps, int64 offsets): first[0..parts]
+    and each part's (lowest in_off, highest in_off + in_len, lowest out_off,
+    highest out_off + out_cap), as an array of 5 parts + 1 uint64 words."""
+    import numpy as np
+    plan = np.zeros(5 * parts + 1, np.uint64)
+    lib = get_lib()
+    if device:
+        n = in_len.numel()
+        rc = lib.enet_rc_multi_plan_device(in_len.data_ptr(), in_off.data_ptr(), out_off.data_ptr(),
+                                           out_cap.data_ptr(), n, parts, plan.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"enet_rc_multi_plan_device failed: HIP error {rc}")
+        return plan
+    arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+            ((in_len, np.uint32), (in_off, np.uint64), (out_off, np.uint64), (out_cap, np.uint32))]
+    rc = lib.enet_rc_multi_plan(arrs[0].ctypes.data, arrs[1].ctypes.data, arrs[2].ctypes.data, arrs[3].ctypes.data,
+                                len(arrs[0]), parts, plan.ctypes.data)
+    if rc != 0:
+        raise ValueError("enet_rc_multi_plan: bad arguments")
+    return plan
 
 
 class MultiCoder:

@@ -81,6 +81,9 @@ def _load() -> C.CDLL:
     lib.enet_rc_multi_devices.argtypes = [vp]
     lib.enet_rc_multi_split.restype = C.c_int
     lib.enet_rc_multi_split.argtypes = [vp, sz, sz, vp]
+    for name in ("enet_rc_multi_plan", "enet_rc_multi_plan_device"):
+        getattr(lib, name).restype = C.c_int
+        getattr(lib, name).argtypes = [vp, vp, vp, vp, sz, sz, vp]
     for name, args in (("enet_rc_multi_compress_batch_host", batch_host),
                        ("enet_rc_multi_decompress_batch_host", batch_host),
                        ("enet_rc_multi_compress_batch_device", batch_dev[:-1]),

@@ -163,7 +163,6 @@ int rc_hip_dgram_launch(int stage, const rc_dgram_dev *g, void *stream);
  * packed (rc_pack.hip); bsum: ceil(n / 1024) + 1 words, bsum[last] = total. */
 int rc_hip_pack(const uint8_t *out, const uint64_t *out_off, const uint32_t *out_len, uint32_t n,
                 uint64_t *bsum, uint8_t *packed, void *stream);
-/* The reverse: packed (back to back) -> out[out_off[i] .. +out_len[i]). */
 /* packets [src + soff[i], +len[i]) -> dst + doff[i] in whole 16-B granules
  * (doff[i] has the source address's alignment mod 16, its granules belong
  * to packet i alone); src may
@@ -174,8 +173,20 @@ int rc_hip_gather16(const uint8_t *src, const uint64_t *soff, uint8_t *dst, cons
  * wavefront per packet; dst may be mapped host memory (rc_pack.hip) */
 int rc_hip_slot_copy(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint8_t *dst,
                      void *stream);
+/* The reverse of rc_hip_pack: packed (back to back) -> out[out_off[i] .. +out_len[i]). */
 int rc_hip_unpack(const uint8_t *packed, uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                   uint32_t n, uint64_t *bsum, void *stream);
+
+/* rc_multi.c's split on the device holding the batch (rc_multi_plan.hip):
+ * plan (5 parts + 1 words, device) = first[0 .. parts], then per part the
+ * lowest in_off, highest in_off + in_len, lowest out_off, highest out_off +
+ * out_cap; ws: rc_hip_multi_plan_ws(n) words.  1 <= parts <= 64, n >= 1. */
+size_t rc_hip_multi_plan_ws(size_t n);
+int rc_hip_multi_plan(const uint32_t *in_len, const uint64_t *in_off, const uint64_t *out_off,
+                      const uint32_t *out_cap, uint64_t n, uint32_t parts, uint64_t *ws, uint64_t *plan,
+                      void *stream);
+/* a[i] -= la, b[i] -= lb for i < cnt (a part's offsets rebased on its device) */
+int rc_hip_multi_rebase(uint64_t *a, uint64_t la, uint64_t *b, uint64_t lb, uint64_t cnt, void *stream);
 
 /* Kernel introspection for bench/profiling. */
 const char *rc_hip_fast_kernel_name(int decompress, uint32_t kernel);

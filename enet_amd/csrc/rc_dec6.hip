@@ -125,6 +125,9 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     uint32_t order = 0, a = 0, p = 0, nodes = 1, claims = 0, x0 = 0;
     uint32_t hl[4] = {0u, 0u, 0u, 0u}, nh = 0;   // elements decoded at order 2: p | a << 8 | v << 16
     bool repeat = false;                      // this step's order-2 context has been visited
+    // ... once, with one symbol (escapes 5, total 7): the common step codes its escape itself
+    bool o2s = false;
+    bool e2d = false;                         // that escape coded, the order-1 READ left to the rare step
     bool stall = false, done = false, off = false, fail = false;
 
     PROF_DECL
@@ -157,7 +160,18 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const uint32_t st = (go && order >= 1) ? stats[p] : 0u;
 #endif
             const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
-            bool need = go && order >= 2 && repeat;
+            bool need = go && order >= 2 && repeat && !o2s;
+            // order 2 when its context holds one visit: an escape is coded here, the
+            // context's one symbol stalls the lane (compress.c:536-568 over total 7)
+            bool e2 = false;
+            const bool c2s = go && order >= 2 && repeat && o2s;
+            if (any_lane(c2s)) {
+                const uint32_t r2 = udiv16d(range, 7u, 1.0 / 7.0);
+                e2 = c2s && code - low < 5u * r2;
+                need = need || (c2s && !e2);
+                range = e2 ? r2 : range;
+                dec_code(low, code, range, 0u, 5u, in, e2);
+            }
             // order 1 (compress.c:536-568): READ; an escape is coded here, a hit stalls the lane
             const bool o1 = go && !need && order >= 1 && t1 > 0;
             const uint32_t esc1 = kSubEscDelta * d1, tot1 = o1 ? esc1 + kSubDelta * t1 : 1u;
@@ -224,6 +238,8 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             p = sym ? v : p;
             order += (sym && order < 2) ? 1u : 0u;
             repeat = sym ? false : repeat;
+            o2s = sym ? false : o2s;
+            e2d = go ? (e2 && need) : e2d;
             stall = stall || need;
 #ifdef DEC6_STATS_PREFETCH
             stn = stats[p];                           // (the next step's bucket byte, read ahead)
@@ -288,7 +304,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             int at = -1;
             uint32_t v = 0, hu = 0, hc = 0;
             bool sf = false;
-            const bool c2 = rs && !over && order >= 2 && t2 > 0;
+            const bool c2 = rs && !over && !e2d && order >= 2 && t2 > 0;
             if (any_lane(c2)) {
                 if (sub_decode6(pl, g2, t2, d2, c2, low, code, range, in, v, hu, hc, sf)) at = 2;
             }
@@ -350,8 +366,13 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             p = sym ? v : p;
             order += (sym && order < 2) ? 1u : 0u;
             repeat = sym ? !nb : repeat;
-            // the step after a hit has a visited order-2 context: another rare step
-            stall = rs ? (sym && !lv && !fl && order >= 2 && repeat) : stall;
+            // the step after a hit has a visited order-2 context (p, v): its visits are
+            // the elements of bucket p with value v.  One visit: one symbol, the
+            // common step's; more: another rare step.
+            const bool one = sym && popc(eqv) == 1;
+            o2s = rs ? one : o2s;
+            e2d = rs ? false : e2d;
+            stall = rs ? (sym && !lv && !fl && order >= 2 && repeat && !one) : stall;
             if constexpr (kSlot) slot_step_end(in, ssl, shc);
             else src_adv(in);
             PROF(3)

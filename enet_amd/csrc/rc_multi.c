@@ -11,9 +11,12 @@
  *   host pointers:   one host thread per device runs that context's
  *                    host-pointer batch (pinned staging, H2D, kernels, D2H)
  *                    on its own range;
- *   device pointers: the batch lives on the first listed device (the root);
- *                    every other device's range is copied to it over the
- *                    peer link (hipMemcpyPeerAsync: xGMI between MI355X),
+ *   device pointers: the batch lives on the first listed device (the root),
+ *                    which computes the split and each range's byte extents
+ *                    (rc_multi_plan.hip; the host reads back 5 words per
+ *                    device, nothing per packet); every other device's range
+ *                    is copied to it over the peer link (hipMemcpyPeerAsync:
+ *                    xGMI between MI355X), its offsets rebased there,
  *                    coded there, packed back to back (rc_pack.hip) and
  *                    copied back, then unpacked into the root's output slots
  *                    -- only the produced bytes cross the link, and nothing
@@ -47,6 +50,11 @@ typedef struct {
     rc_dev d[RC_MULTI_MAX];
     uint8_t *stage;                 /* root: the other devices' packed results */
     size_t stage_cap;
+    uint64_t *d_plan;               /* root: the split's plan and scan words (rc_multi_plan.hip) */
+    size_t plan_cap;
+    uint64_t *h_plan;               /* pinned: the plan as read back; then each device's packed bytes */
+    uint64_t *h_packed;
+    hipEvent_t ready;               /* root: the caller's inputs (its null stream) */
 } rc_multi;
 
 int enet_rc_multi_split(const uint32_t *in_len, size_t n, size_t parts, uint64_t *first)
@@ -79,10 +87,13 @@ void enet_rc_multi_destroy(void *multi)
         if (m->d[k].done) hipEventDestroy(m->d[k].done);
         enet_range_coder_destroy(m->d[k].ctx);
     }
-    if (m->stage && m->n) {
+    if (m->n) {
         hipSetDevice(m->d[0].device);
-        hipFree(m->stage);
+        if (m->stage) hipFree(m->stage);
+        if (m->d_plan) hipFree(m->d_plan);
+        if (m->ready) hipEventDestroy(m->ready);
     }
+    if (m->h_plan) hipHostFree(m->h_plan);
     hipSetDevice(prev);
     free(m);
 }
@@ -102,6 +113,13 @@ void *enet_rc_multi_create(const int *devices, size_t n_devices)
         m->n = k + 1;
         if (hipEventCreateWithFlags(&m->d[k].done, hipEventDisableTiming) != hipSuccess) goto fail;
     }
+    hipSetDevice(devices[0]);
+    if (hipEventCreateWithFlags(&m->ready, hipEventDisableTiming) != hipSuccess) goto fail;
+    if (hipHostMalloc((void **) &m->h_plan, (5 * RC_MULTI_MAX + 1 + RC_MULTI_MAX) * 8, 0) != hipSuccess) {
+        m->h_plan = NULL;
+        goto fail;
+    }
+    m->h_packed = m->h_plan + 5 * RC_MULTI_MAX + 1;
     /* direct peer access between the root and every other device (xGMI);
      * where it is unavailable (same device, no link) copies are staged by the
      * runtime, which is slower but correct */
@@ -213,14 +231,63 @@ int enet_rc_multi_decompress_batch_host(void *multi, const uint8_t *in, const ui
 
 static size_t al16(size_t x) { return (x + 15) & ~(size_t) 15; }
 
+/* The split with the byte ranges each part covers: first[0 .. parts] as
+ * enet_rc_multi_split, then per part k at plan[parts + 1 + 4k]: the lowest
+ * in_off, highest in_off + in_len, lowest out_off, highest out_off + out_cap
+ * (UINT64_MAX, 0, UINT64_MAX, 0 when the part is empty).  Host restatement
+ * of rc_multi_plan.hip, which computes it on the root device. */
+int enet_rc_multi_plan(const uint32_t *in_len, const uint64_t *in_off, const uint64_t *out_off,
+                       const uint32_t *out_cap, size_t n, size_t parts, uint64_t *plan)
+{
+    if (!plan || (n && (!in_off || !out_off || !out_cap))) return -1;
+    if (enet_rc_multi_split(in_len, n, parts, plan) != 0) return -1;
+    uint64_t *ext = plan + parts + 1;
+    for (size_t k = 0; k < parts; ++k) {
+        uint64_t *e = ext + 4 * k;
+        e[0] = UINT64_MAX; e[1] = 0; e[2] = UINT64_MAX; e[3] = 0;
+        for (uint64_t i = plan[k]; i < plan[k + 1]; ++i) {
+            if (in_off[i] < e[0]) e[0] = in_off[i];
+            if (in_off[i] + in_len[i] > e[1]) e[1] = in_off[i] + in_len[i];
+            if (out_off[i] < e[2]) e[2] = out_off[i];
+            if (out_off[i] + out_cap[i] > e[3]) e[3] = out_off[i] + out_cap[i];
+        }
+    }
+    return 0;
+}
+
+/* root-side buffers of the plan: the device's scan words and plan, the pinned
+ * copy the host reads */
+static int plan_reserve(rc_multi *m, size_t n)
+{
+    const size_t need = rc_hip_multi_plan_ws(n) + 5 * RC_MULTI_MAX + 1;
+    if (need <= m->plan_cap) return 0;
+    if (m->d_plan) { hipStreamSynchronize((hipStream_t) rc_ctx_stream(m->d[0].ctx)); hipFree(m->d_plan); }
+    m->d_plan = NULL; m->plan_cap = 0;
+    if (hipMalloc((void **) &m->d_plan, need * 8) != hipSuccess) return -1;
+    m->plan_cap = need;
+    return 0;
+}
+
+/* The plan on the root's stream (behind the caller's inputs) and its one
+ * small read-back: the only host wait before the ranges go out. */
+static int device_plan(rc_multi *m, const uint64_t *in_off, const uint32_t *in_len, size_t n,
+                       const uint64_t *out_off, const uint32_t *out_cap, void *rst)
+{
+    if (plan_reserve(m, n) != 0) return (int) hipErrorOutOfMemory;
+    uint64_t *dplan = m->d_plan, *ws = m->d_plan + 5 * RC_MULTI_MAX + 1;
+    int rc = rc_hip_multi_plan(in_len, in_off, out_off, out_cap, n, (uint32_t) m->n, ws, dplan, rst);
+    if (rc) return rc;
+    hipError_t err = hipMemcpyAsync(m->h_plan, dplan, (5 * m->n + 1) * 8, hipMemcpyDeviceToHost, (hipStream_t) rst);
+    if (err == hipSuccess) err = hipStreamSynchronize((hipStream_t) rst);
+    return (int) err;
+}
+
 /* one non-root device's share: layout of its buffer */
 typedef struct {
     size_t lo, cnt;                 /* packet range */
     uint64_t lo_in, pay;            /* input bytes [lo_in, lo_in + pay) of the root's in */
-    uint64_t slots;                 /* output slot bytes (rebased extent) */
+    uint64_t lo_out, slots;         /* output slot bytes [lo_out, lo_out + slots) */
     size_t a_ioff, a_ilen, a_out, a_ooff, a_ocap, a_olen, a_pack, total;
-    uint64_t packed;                /* bytes produced (read back after the kernels) */
-    uint64_t *h_off;                /* rebased in_off | out_off (host) */
 } share;
 
 static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const uint64_t *in_off,
@@ -233,22 +300,26 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
     int prev = 0;
     hipGetDevice(&prev);
     const int root = m->d[0].device;
+    void *rst = rc_ctx_stream(m->d[0].ctx);
     hipError_t err = hipSetDevice(root);
-    /* the caller's inputs are ready on any stream of the root */
-    if (err == hipSuccess) err = hipDeviceSynchronize();
-    uint64_t *h_ioff = (uint64_t *) malloc(n * 8), *h_ooff = (uint64_t *) malloc(n * 8);
-    uint32_t *h_ilen = (uint32_t *) malloc(n * 4), *h_ocap = (uint32_t *) malloc(n * 4);
+    /* the caller's inputs are complete on the root's null stream (which waits
+     * for every blocking stream): the root's stream waits for that, the host
+     * does not */
+    if (err == hipSuccess) err = hipEventRecord(m->ready, 0);
+    if (err == hipSuccess) err = hipStreamWaitEvent((hipStream_t) rst, m->ready, 0);
+    if (err != hipSuccess) { hipSetDevice(prev); return (int) err; }
+    int rc = 0;
+    if (m->n == 1) {                /* one device: the plain batch */
+        rc = rc_ctx_run_device(m->d[0].ctx, decompress, in, in_off, in_len, n, max_len, out, out_off, out_cap,
+                               out_len, rst);
+        err = hipStreamSynchronize((hipStream_t) rst);
+        hipSetDevice(prev);
+        return rc ? rc : (int) err;
+    }
+    rc = device_plan(m, in_off, in_len, n, out_off, out_cap, rst);
+    const uint64_t *first = m->h_plan, *ext = m->h_plan + m->n + 1;
     share sh[RC_MULTI_MAX];
     memset(sh, 0, sizeof sh);
-    int rc = 0;
-    if (!h_ioff || !h_ooff || !h_ilen || !h_ocap) rc = (int) hipErrorOutOfMemory;
-    if (!rc && err == hipSuccess) err = hipMemcpy(h_ioff, in_off, n * 8, hipMemcpyDeviceToHost);
-    if (!rc && err == hipSuccess) err = hipMemcpy(h_ooff, out_off, n * 8, hipMemcpyDeviceToHost);
-    if (!rc && err == hipSuccess) err = hipMemcpy(h_ilen, in_len, n * 4, hipMemcpyDeviceToHost);
-    if (!rc && err == hipSuccess) err = hipMemcpy(h_ocap, out_cap, n * 4, hipMemcpyDeviceToHost);
-    if (!rc && err != hipSuccess) rc = (int) err;
-    uint64_t first[RC_MULTI_MAX + 1];
-    if (!rc && enet_rc_multi_split(h_ilen, n, m->n, first) != 0) rc = (int) hipErrorInvalidValue;
     /* phase 1: scatter, code, pack -- every device enqueued before any wait */
     for (size_t k = 0; k < m->n && !rc; ++k) {
         rc_dev *d = &m->d[k];
@@ -258,20 +329,16 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
         if (s->cnt == 0) continue;
         void *st = rc_ctx_stream(d->ctx);
         if (k == 0) {               /* the root codes its range in place */
+            if ((err = hipSetDevice(root)) != hipSuccess) { rc = (int) err; break; }
             rc = rc_ctx_run_device(d->ctx, decompress, in, in_off + s->lo, in_len + s->lo, s->cnt, max_len, out,
                                    out_off + s->lo, out_cap + s->lo, out_len + s->lo, st);
             continue;
         }
-        uint64_t lo_in = UINT64_MAX, hi_in = 0, lo_out = UINT64_MAX, hi_out = 0;
-        for (size_t i = s->lo; i < s->lo + s->cnt; ++i) {
-            if (h_ioff[i] < lo_in) lo_in = h_ioff[i];
-            if (h_ioff[i] + h_ilen[i] > hi_in) hi_in = h_ioff[i] + h_ilen[i];
-            if (h_ooff[i] < lo_out) lo_out = h_ooff[i];
-            if (h_ooff[i] + h_ocap[i] > hi_out) hi_out = h_ooff[i] + h_ocap[i];
-        }
-        s->lo_in = lo_in;
-        s->pay = hi_in - lo_in;
-        s->slots = hi_out - lo_out;
+        const uint64_t *e = ext + 4 * k;
+        s->lo_in = e[0];
+        s->pay = e[1] - e[0];
+        s->lo_out = e[2];
+        s->slots = e[3] - e[2];
         s->a_ioff = al16(s->pay);
         s->a_ilen = s->a_ioff + s->cnt * 8;
         s->a_out = al16(s->a_ilen + s->cnt * 4);
@@ -280,15 +347,9 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
         s->a_olen = al16(s->a_ocap + s->cnt * 4);
         s->a_pack = al16(s->a_olen + s->cnt * 4);
         s->total = s->a_pack + s->slots + 16;
-        s->h_off = (uint64_t *) malloc(2 * s->cnt * 8);
-        if (!s->h_off) { rc = (int) hipErrorOutOfMemory; break; }
-        for (size_t i = 0; i < s->cnt; ++i) {
-            s->h_off[i] = h_ioff[s->lo + i] - lo_in;
-            s->h_off[s->cnt + i] = h_ooff[s->lo + i] - lo_out;
-        }
         if ((err = hipSetDevice(d->device)) != hipSuccess) { rc = (int) err; break; }
         if (s->total > d->buf_cap) {
-            hipDeviceSynchronize();
+            hipStreamSynchronize((hipStream_t) st);
             if (d->buf) hipFree(d->buf);
             d->buf = NULL; d->buf_cap = 0;
             if (hipMalloc((void **) &d->buf, s->total) != hipSuccess) { rc = (int) hipErrorOutOfMemory; break; }
@@ -297,16 +358,17 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
         uint8_t *b = d->buf;
         uint64_t *bsum = rc_ctx_bsum(d->ctx, s->cnt);
         if (!bsum) { rc = (int) hipErrorOutOfMemory; break; }
-        err = hipMemcpyPeerAsync(b, d->device, in + lo_in, root, s->pay, (hipStream_t) st);
-        if (err == hipSuccess) err = hipMemcpyPeerAsync(b + s->a_ilen, d->device, in_len + s->lo, root, s->cnt * 4,
-                                                        (hipStream_t) st);
-        if (err == hipSuccess) err = hipMemcpyPeerAsync(b + s->a_ocap, d->device, out_cap + s->lo, root, s->cnt * 4,
-                                                        (hipStream_t) st);
-        if (err == hipSuccess) err = hipMemcpyAsync(b + s->a_ioff, s->h_off, s->cnt * 8, hipMemcpyHostToDevice,
-                                                    (hipStream_t) st);
-        if (err == hipSuccess) err = hipMemcpyAsync(b + s->a_ooff, s->h_off + s->cnt, s->cnt * 8,
-                                                    hipMemcpyHostToDevice, (hipStream_t) st);
+        /* the range's bytes and metadata over the peer link; offsets rebased there */
+        hipStream_t hs = (hipStream_t) st;
+        err = hipMemcpyPeerAsync(b, d->device, in + s->lo_in, root, s->pay, hs);
+        if (err == hipSuccess) err = hipMemcpyPeerAsync(b + s->a_ioff, d->device, in_off + s->lo, root, s->cnt * 8, hs);
+        if (err == hipSuccess) err = hipMemcpyPeerAsync(b + s->a_ilen, d->device, in_len + s->lo, root, s->cnt * 4, hs);
+        if (err == hipSuccess) err = hipMemcpyPeerAsync(b + s->a_ooff, d->device, out_off + s->lo, root, s->cnt * 8, hs);
+        if (err == hipSuccess) err = hipMemcpyPeerAsync(b + s->a_ocap, d->device, out_cap + s->lo, root, s->cnt * 4, hs);
         if (err != hipSuccess) { rc = (int) err; break; }
+        rc = rc_hip_multi_rebase((uint64_t *) (b + s->a_ioff), s->lo_in, (uint64_t *) (b + s->a_ooff), s->lo_out,
+                                 s->cnt, st);
+        if (rc) break;
         rc = rc_ctx_run_device(d->ctx, decompress, b, (const uint64_t *) (b + s->a_ioff),
                                (const uint32_t *) (b + s->a_ilen), s->cnt, max_len, b + s->a_out,
                                (const uint64_t *) (b + s->a_ooff), (const uint32_t *) (b + s->a_ocap),
@@ -316,27 +378,26 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
                          (uint32_t) s->cnt, bsum, b + s->a_pack, st);
         if (rc) break;
         /* the lengths to the root now; the packed bytes once their total is known */
-        err = hipMemcpyPeerAsync(out_len + s->lo, root, b + s->a_olen, d->device, s->cnt * 4, (hipStream_t) st);
+        err = hipMemcpyPeerAsync(out_len + s->lo, root, b + s->a_olen, d->device, s->cnt * 4, hs);
         if (err == hipSuccess)
-            err = hipMemcpyAsync(&s->packed, bsum + (s->cnt + 1023) / 1024, 8, hipMemcpyDeviceToHost, (hipStream_t) st);
+            err = hipMemcpyAsync(&m->h_packed[k], bsum + (s->cnt + 1023) / 1024, 8, hipMemcpyDeviceToHost, hs);
         if (err != hipSuccess) { rc = (int) err; break; }
     }
     /* phase 2: gather -- each device's packed bytes to the root's staging,
-     * unpacked into the output slots on the root's stream */
+     * unpacked into the output slots on the root's stream behind an event */
     uint64_t stage_need = 0, stage_at[RC_MULTI_MAX];
     for (size_t k = 1; k < m->n && !rc; ++k) {
         if (sh[k].cnt == 0) continue;
         if ((err = hipSetDevice(m->d[k].device)) != hipSuccess ||
             (err = hipStreamSynchronize((hipStream_t) rc_ctx_stream(m->d[k].ctx))) != hipSuccess) { rc = (int) err; break; }
-        if (sh[k].packed > sh[k].slots) { rc = (int) hipErrorUnknown; break; }
+        if (m->h_packed[k] > sh[k].slots) { rc = (int) hipErrorUnknown; break; }
         stage_at[k] = stage_need;
-        stage_need += al16(sh[k].packed);
+        stage_need += al16(m->h_packed[k]);
     }
-    void *rst = rc_ctx_stream(m->d[0].ctx);
     if (!rc && stage_need) {
         hipSetDevice(root);
         if (stage_need > m->stage_cap) {
-            hipDeviceSynchronize();
+            hipStreamSynchronize((hipStream_t) rst);
             if (m->stage) hipFree(m->stage);
             m->stage = NULL; m->stage_cap = 0;
             if (hipMalloc((void **) &m->stage, stage_need) != hipSuccess) rc = (int) hipErrorOutOfMemory;
@@ -349,8 +410,9 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
             if (s->cnt == 0) continue;
             hipSetDevice(m->d[k].device);
             void *st = rc_ctx_stream(m->d[k].ctx);
-            err = s->packed ? hipMemcpyPeerAsync(m->stage + stage_at[k], root, m->d[k].buf + s->a_pack, m->d[k].device,
-                                                 s->packed, (hipStream_t) st) : hipSuccess;
+            const uint64_t packed = m->h_packed[k];
+            err = packed ? hipMemcpyPeerAsync(m->stage + stage_at[k], root, m->d[k].buf + s->a_pack, m->d[k].device,
+                                              packed, (hipStream_t) st) : hipSuccess;
             if (err == hipSuccess) err = hipEventRecord(m->d[k].done, (hipStream_t) st);
             if (err == hipSuccess) { hipSetDevice(root); err = hipStreamWaitEvent((hipStream_t) rst, m->d[k].done, 0); }
             if (err != hipSuccess) { rc = (int) err; break; }
@@ -364,11 +426,24 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
         hipSetDevice(m->d[k].device);
         err = hipStreamSynchronize((hipStream_t) rc_ctx_stream(m->d[k].ctx));
         if (!rc && err != hipSuccess) rc = (int) err;
-        free(sh[k].h_off);
     }
-    free(h_ioff); free(h_ooff); free(h_ilen); free(h_ocap);
     hipSetDevice(prev);
     return rc;
+}
+
+/* The device plan alone (tests: against enet_rc_multi_plan): device pointers
+ * on the current device, plan (5 parts + 1 words) to host memory. */
+int enet_rc_multi_plan_device(const uint32_t *in_len, const uint64_t *in_off, const uint64_t *out_off,
+                              const uint32_t *out_cap, size_t n, size_t parts, uint64_t *plan)
+{
+    if (!plan || n == 0 || parts == 0 || parts > RC_MULTI_MAX) return (int) hipErrorInvalidValue;
+    const size_t words = rc_hip_multi_plan_ws(n) + 5 * parts + 1;
+    uint64_t *d = NULL;
+    if (hipMalloc((void **) &d, words * 8) != hipSuccess) return (int) hipErrorOutOfMemory;
+    int rc = rc_hip_multi_plan(in_len, in_off, out_off, out_cap, n, (uint32_t) parts, d + 5 * parts + 1, d, NULL);
+    hipError_t err = rc ? hipSuccess : hipMemcpy(plan, d, (5 * parts + 1) * 8, hipMemcpyDeviceToHost);
+    hipFree(d);
+    return rc ? rc : (int) err;
 }
 
 int enet_rc_multi_compress_batch_device(void *multi, const uint8_t *in, const uint64_t *in_off,

@@ -221,6 +221,17 @@ size_t enet_rc_multi_devices(void *multi);
  * parts + 1 entries); the smallest index whose prefix sum of in_len reaches
  * k / parts of the total.  0, or -1 on bad arguments.  Host-only. */
 int enet_rc_multi_split(const uint32_t *in_len, size_t n, size_t parts, uint64_t *first);
+/* The split with each part's byte ranges: first[0 .. parts] as above, then
+ * per part k at plan[parts + 1 + 4k]: lowest in_off, highest in_off + in_len,
+ * lowest out_off, highest out_off + out_cap (UINT64_MAX, 0, UINT64_MAX, 0
+ * when empty); plan holds 5 parts + 1 words.  Host pointers, host-only; 0 or
+ * -1.  enet_rc_multi_plan_device computes the same on the current device
+ * from device pointers (as the device-pointer calls below do; n >= 1) and
+ * copies the plan to host memory; 0 or a hipError_t. */
+int enet_rc_multi_plan(const uint32_t *in_len, const uint64_t *in_off, const uint64_t *out_off,
+                       const uint32_t *out_cap, size_t n, size_t parts, uint64_t *plan);
+int enet_rc_multi_plan_device(const uint32_t *in_len, const uint64_t *in_off, const uint64_t *out_off,
+                              const uint32_t *out_cap, size_t n, size_t parts, uint64_t *plan);
 /* HOST pointers, as enet_rc_*_batch_host: one host thread per device copies
  * its range in, codes it and copies it out; returns with the results. */
 int enet_rc_multi_compress_batch_host(void *multi, const uint8_t *in, const uint64_t *in_off,
@@ -229,11 +240,12 @@ int enet_rc_multi_compress_batch_host(void *multi, const uint8_t *in, const uint
 int enet_rc_multi_decompress_batch_host(void *multi, const uint8_t *in, const uint64_t *in_off,
                                         const uint32_t *in_len, size_t n, uint8_t *out,
                                         const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
-/* DEVICE pointers on devices[0]: every other device's range is copied to it
- * over the peer link (hipMemcpyPeerAsync, xGMI), coded there, packed back to
- * back and copied back, then unpacked into the root's slots (only bytes
- * [out_off[i], +out_len[i]) are written).  Waits for the root device before
- * starting and returns with the results in place. */
+/* DEVICE pointers on devices[0]: the split is computed there; every other
+ * device's range is copied to it over the peer link (hipMemcpyPeerAsync,
+ * xGMI), coded there, packed back to back and copied back, then unpacked into
+ * the root's slots (only bytes [out_off[i], +out_len[i]) are written).  The
+ * inputs must be complete on the root's null stream (HIP's default stream,
+ * which waits for every blocking stream); returns with the results in place. */
 int enet_rc_multi_compress_batch_device(void *multi, const uint8_t *in, const uint64_t *in_off,
                                         const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
                                         const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);

@@ -7,7 +7,7 @@ multi-GPU node, over a same-device "peer" copy)."""
 import numpy as np
 import pytest
 
-from enet_amd import multi_split, shard, synth
+from enet_amd import multi_plan, multi_split, shard, synth
 
 
 @pytest.mark.parametrize("n,parts", [(0, 3), (1, 4), (7, 8), (1000, 1), (1000, 3), (65536, 8), (100000, 5)])
@@ -29,6 +29,55 @@ def test_split_bad_arguments():
         multi_split(np.zeros(4, np.uint32), 0)
     with pytest.raises(ValueError):
         multi_split(np.zeros(4, np.uint32), 65)
+
+
+def _plan_case(n, seed):
+    """ragged lengths (zeros included), offsets in no particular order, caps 2N + 64"""
+    rng = np.random.default_rng(seed)
+    ln = rng.integers(0, 1400, size=n).astype(np.uint32)
+    ln[rng.random(n) < 0.05] = 0
+    ioff = rng.permutation(np.arange(n, dtype=np.uint64) * 1500) + 3
+    cap = (2 * ln.astype(np.uint64) + 64).astype(np.uint32)
+    ooff = rng.permutation(np.arange(n, dtype=np.uint64) * 3000)
+    return ln, ioff, ooff, cap
+
+
+def _plan_numpy(ln, ioff, ooff, cap, parts):
+    first = multi_split(ln, parts)
+    ext = []
+    for k in range(parts):
+        a, b = int(first[k]), int(first[k + 1])
+        if a == b:
+            ext += [2 ** 64 - 1, 0, 2 ** 64 - 1, 0]
+        else:
+            ext += [int(ioff[a:b].min()), int((ioff[a:b] + ln[a:b]).max()),
+                    int(ooff[a:b].min()), int((ooff[a:b] + cap[a:b]).max())]
+    return [int(x) for x in first] + ext
+
+
+@pytest.mark.parametrize("n,parts", [(1, 1), (1, 5), (7, 8), (1000, 3), (5000, 64), (70000, 8)])
+def test_plan_host_mirror(n, parts):
+    """enet_rc_multi_plan (the host restatement of rc_multi_plan.hip) against numpy"""
+    ln, ioff, ooff, cap = _plan_case(n, n + parts)
+    assert [int(x) for x in multi_plan(ln, ioff, ooff, cap, parts)] == _plan_numpy(ln, ioff, ooff, cap, parts)
+    z = np.zeros(n, np.uint32)           # no payload: every split point 0
+    got = multi_plan(z, ioff, ooff, cap, parts)
+    assert [int(x) for x in got[:parts]] == [0] * parts and int(got[parts]) == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,parts", [(1, 1), (1, 5), (7, 8), (1000, 3), (5000, 64), (70000, 8), (300000, 3)])
+def test_plan_device_matches_host(n, parts):
+    """rc_multi_plan.hip (the split rc_multi.c computes on the root) against its host restatement"""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ln, ioff, ooff, cap = _plan_case(n, n * 3 + parts)
+    for lens in (ln, np.zeros(n, np.uint32)):
+        dev = [torch.from_numpy(a.astype(t)).cuda() for a, t in
+               ((lens, np.int32), (ioff, np.int64), (ooff, np.int64), (cap, np.int32))]
+        got = multi_plan(*dev, parts, device=True)
+        assert np.array_equal(got, multi_plan(lens, ioff, ooff, cap, parts)), (n, parts)
 
 
 def _oracle(d, o, l):
