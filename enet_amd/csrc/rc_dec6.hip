@@ -93,7 +93,7 @@ DEV void bail6(const rc_workspace_dev& ws, uint32_t pkt) { bail(ws, pkt); }
 // rc_decompress_dec6s).
 template <class Src>
 DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* root,
-                         uint8_t* stats, uint8_t* tab, Src& in)
+                         uint8_t* stats, uint8_t* tab, const uint8_t* itab, Src& in)
 {
     constexpr bool kSlot = std::is_same<Src, SlotSrc>::value;
     const uint32_t len = bt.in_len[pkt];
@@ -208,7 +208,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const uint32_t v = root3_search(root, R, sym ? cd0 - 1 : 0u, under0, cnt0);
             dec_code_late(low, code, range, 1 + under0, 1 + cnt0, in, sym);
             if (sym) {
-                root3_add<false>(root, R, v, cnt0);
+                root3_add_inc(root, R, itab, v, cnt0);
                 rtot = (rtot + kRootDelta) & 0xFFFF;
             }
             if (rare_lane(sym && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit))) {
@@ -326,7 +326,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             v = sym0 ? v0 : v;
             dec_code(low, code, range, sym0 ? 1 + under0 : hu, sym0 ? 1 + cnt0 : hc, in, sym);
             if (sym0) {
-                root3_add<false>(root, R, v, cnt0);
+                root3_add_inc(root, R, itab, v, cnt0);
                 rtot = (rtot + kRootDelta) & 0xFFFF;
             }
             if (rare_lane(sym0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit))) {
@@ -412,24 +412,28 @@ void rc_decompress_dec6(rc_batch_dev b, rc_workspace_dev ws)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t act = ws.lane_active;
     const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-    if (l >= act) return;
     const uint32_t local = wave * act + l;
     uint8_t* root = smem + local * kLds6;
     uint8_t* stats = root + kStats6;
+    uint8_t* itab = smem + 4 * act * kLds6;          // root3_inc_init's table, 16 x 32 B
+    if (threadIdx.x < 16) root3_inc_init(itab, threadIdx.x);
+    __syncthreads();
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * RC_DEC6_TAB_BYTES;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
+    if (l >= act) return;
     ByteSrc in;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
         const uint32_t pkt = order ? order[i] : i;
-        decompress_one6(b, ws, pkt, root, stats, tab, in);
+        decompress_one6(b, ws, pkt, root, stats, tab, itab, in);
     }
 }
 
 // The same with the lanes' input through LDS (rc_slot.h): waves 0-3 decode,
 // wave w + 4 (on wave w's SIMD) keeps their slots filled.  LDS per lane:
-// root | slot (the root's pad) | bucket bytes, then m_ctl / m_pkt, h_ctl.
+// root | slot (the root's pad) | bucket bytes, then m_ctl / m_pkt, h_ctl;
+// then root3_inc_init's table (16 x 32 B).
 constexpr uint32_t kLanes6s = 256;
 extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_dev b, rc_workspace_dev ws)
 {
@@ -442,9 +446,11 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
     uint8_t* slotp = root + 256;
     uint32_t* mctl = reinterpret_cast<uint32_t*>(smem + kLanes6s * kLds6) + 2 * L;
     uint32_t* hctl = reinterpret_cast<uint32_t*>(smem + kLanes6s * kLds6 + 8 * kLanes6s) + L;
+    uint8_t* itab = smem + kLanes6s * (kLds6 + 12);
     const uint32_t slot = blockIdx.x * kLanes6s + L;
     if (!helper) *reinterpret_cast<uint2*>(mctl) = make_uint2(0u, slot < b.n ? kNoPktS : kFinS);
     else *hctl = 0u;
+    if (threadIdx.x < 16) root3_inc_init(itab, threadIdx.x);
     __syncthreads();
     if (helper) {
         SlotHelp h;
@@ -463,7 +469,7 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
     in.gen = 0; in.mctl = mctl; in.hctl = hctl; in.slot = slotp;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * kLanes6s) {
         const uint32_t pkt = order ? order[i] : i;
-        decompress_one6(b, ws, pkt, root, stats, tab, in);
+        decompress_one6(b, ws, pkt, root, stats, tab, itab, in);
     }
     mctl[1] = kFinS;
 }
@@ -541,13 +547,13 @@ extern "C" int rc_hip_dec6_launch(const rc_batch_dev* b, const rc_workspace_dev*
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (ws->dec4 == 8 && ws->lane_active == 64) {
         // (the slot variant: 12 B more per lane for the control words)
-        const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12);
+        const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12) + 512;
         hipLaunchKernelGGL(rc_decompress_dec6s, dim3(blocks), dim3(512), lds, st, *b, *ws);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return static_cast<int>(e);
         return rc_hip_dec6_verify_launch(b, ws, stream);
     }
-    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kLds6;
+    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kLds6 + 512;
     hipLaunchKernelGGL(rc_decompress_dec6, dim3(blocks), dim3(256), lds, st, *b, *ws);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);

@@ -142,6 +142,18 @@ DEV void root3_add(uint8_t* r, Root& R, uint32_t v, uint32_t cnt)
     root3_store_d<COPY>(r, R);
 }
 
+// decoder update with the block-wide increment table (root3_inc_init): count[v]
+// and the registers D by two LDS reads and eight adds (no carry can cross a
+// half: D <= 64256) instead of cum_add's compares
+DEV void root3_add_inc(uint8_t* r, Root& R, const uint8_t* itab, uint32_t v, uint32_t cnt)
+{
+    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
+    const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (v >> 4));
+    const uint4 i0 = ip[0], i1 = ip[1];
+    R.d[0] += i0.x; R.d[1] += i0.y; R.d[2] += i0.z; R.d[3] += i0.w;
+    R.d[4] += i1.x; R.d[5] += i1.y; R.d[6] += i1.z; R.d[7] += i1.w;
+}
+
 // Decoder: the symbol whose interval holds code (code < root total - 1):
 // g = #{t : D[t] <= code} by packed saturating compares, then halving on byte
 // sums inside group g.  Returns v; under = its cumulative frequency, cnt = count[v].

@@ -10,6 +10,13 @@
 #ifdef DEC6
 #include "../../enet_amd/csrc/rc_dec6.hip"
 static uint8_t g_lds6[528] __attribute__((aligned(16)));   // root + bucket bytes
+static uint8_t g_itab6[512] __attribute__((aligned(16)));  // root3_inc_init's table
+static const uint8_t* itab6()
+{
+    static bool init = false;
+    if (!init) { for (uint32_t g = 0; g < 16; ++g) root3_inc_init(g_itab6, g); init = true; }
+    return g_itab6;
+}
 // -DDEC6S: the lane's input through the LDS slot (rc_slot.h), the helper's
 // pass run after every step and whenever the lane waits
 static uint32_t g_ctl6s[3];
@@ -120,14 +127,14 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     if (decompress) {
 #ifndef DEC6S
         ByteSrc src6;
-        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, src6);
+        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, itab6(), src6);
 #else
         g_b6s = &b;
         g_ctl6s[0] = 0u; g_ctl6s[1] = kNoPktS; g_ctl6s[2] = 0u;
         slot_help_init(g_sh6);
         SlotSrc src6;
         src6.gen = 0; src6.mctl = g_ctl6s; src6.hctl = g_ctl6s + 2; src6.slot = g_lds6 + 256;
-        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, src6);
+        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, itab6(), src6);
         g_b6s = nullptr;
 #endif
         if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
