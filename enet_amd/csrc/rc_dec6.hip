@@ -88,6 +88,30 @@ constexpr uint32_t kDummy6 = 12288;              // the slot of the stores that 
 
 DEV void bail6(const rc_workspace_dev& ws, uint32_t pkt) { bail(ws, pkt); }
 
+// compress.c:148-157 (FREE_SYMBOLS) after the byte at output position n - 1:
+// a fresh model -- the root, every bucket byte (the records past a bucket's
+// count are never read), order 0 -- while the coder runs on.  The check
+// (rc_dec6_verify) counts bigrams per model segment: rst records where each
+// segment after the first starts (12 bits each, the count in bits 24-25).
+DEV void reset6(uint8_t* root, uint8_t* stats, Root& R, uint32_t& rtot, double& rrt, uint32_t& order, uint32_t& a,
+                uint32_t& p, uint32_t& nodes, uint32_t& nh, bool& repeat, bool& o2s, bool& e2d, uint32_t& seg0,
+                uint32_t& rst, uint32_t n)
+{
+    root3_clear<false>(root, R);
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) reinterpret_cast<uint4*>(stats)[i] = z;
+    rtot = 1 + 256;
+    rrt = rcp64(rtot);
+    order = 0; a = 0; p = 0; nodes = 1; nh = 0;
+    repeat = false; o2s = false; e2d = false;
+    rst = (rst | (n << (12 * (rst >> 24)))) + (1u << 24);
+    seg0 = n;
+}
+
+// another segment fits the record: at most two resets, starts below 4096
+DEV bool can_reset6(uint32_t rst, uint32_t n) { return (rst >> 24) < 2 && n < 4096; }
+
 // Src: ByteSrc (the stream's chunks loaded by the lane, rc_decompress_dec6) or
 // SlotSrc (through the LDS slot a helper wavefront refills, rc_slot.h,
 // rc_decompress_dec6s).
@@ -98,7 +122,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     constexpr bool kSlot = std::is_same<Src, SlotSrc>::value;
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
-    if (len == 0) { bt.out_len[pkt] = 0; ws.claims[pkt] = 0; return; }     // compress.c:513
+    if (len == 0) { bt.out_len[pkt] = 0; ws.claims[pkt] = 0; ws.dec6_resets[pkt] = 0; return; }     // compress.c:513
     ByteSink o;
     sink_init(o, bt.out + bt.out_off[pkt], cap);
     uint32_t code;
@@ -129,6 +153,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     bool o2s = false;
     bool e2d = false;                         // that escape coded, the order-1 READ left to the rare step
     bool stall = false, done = false, off = false, fail = false;
+    uint32_t seg0 = 0, rst = 0;               // the model segment's first output position; resets (reset6)
 
     PROF_DECL
     // One loop of common steps; every kBlock6 steps (or once no lane can take
@@ -229,7 +254,8 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             x0 = (sym && order == 0) ? v : x0;
             const bool fl = sym && o.n >= o.cap;                           // compress.c:617
             claims += (o1v && !fl) ? 1u : 0u;
-            const bool lv = past || full || (sym && nodes >= kMaxNodes);
+            const bool rs0 = sym && nodes >= kMaxNodes;                    // compress.c:148-157
+            const bool lv = past || full || (rs0 && !can_reset6(rst, o.n + 1));
             off = off || lv;
             fail = fail || fl;
             done = done || eos || lv || fl;
@@ -241,6 +267,9 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             o2s = sym ? false : o2s;
             e2d = go ? (e2 && need) : e2d;
             stall = stall || need;
+            if (rare_lane(rs0 && !done)) {
+                if (rs0 && !done) reset6(root, stats, R, rtot, rrt, order, a, p, nodes, nh, repeat, o2s, e2d, seg0, rst, o.n);
+            }
 #ifdef DEC6_STATS_PREFETCH
             stn = stats[p];                           // (the next step's bucket byte, read ahead)
             {
@@ -274,7 +303,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const uint32_t st = rs && order >= 1 ? stats[p] : 0u;
             const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
             Hist6 H;
-            rec_build(tab, p, rs ? t1 : 0u, hl, nh, x0, o.n, rs, H);
+            rec_build(tab, p, rs ? t1 : 0u, hl, nh, x0, o.n - seg0, rs, H);
             const bool over = false;
             PROF(1)
 #ifdef RC_PROFILE
@@ -356,8 +385,9 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const bool hfull = h2 && nh >= 4;
             nh += h2 ? 1u : 0u;
             const bool fl = sym && o.n >= o.cap;
+            const bool rs0 = rs && sym && nodes >= kMaxNodes;               // compress.c:148-157
             const bool lv = over || sf || past || hfull || tfull || (o1v && !n1 && (st >> 5) >= 7) ||
-                            (sym && nodes >= kMaxNodes);
+                            (rs0 && !can_reset6(rst, o.n + 1));
             off = off || (rs && lv);
             fail = fail || (rs && fl);
             done = done || (rs && (eos || lv || fl));
@@ -373,6 +403,12 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             o2s = rs ? one : o2s;
             e2d = rs ? false : e2d;
             stall = rs ? (sym && !lv && !fl && order >= 2 && repeat && !one) : stall;
+            if (rare_lane(rs0 && !done)) {
+                if (rs0 && !done) {
+                    reset6(root, stats, R, rtot, rrt, order, a, p, nodes, nh, repeat, o2s, e2d, seg0, rst, o.n);
+                    stall = false;
+                }
+            }
             if constexpr (kSlot) slot_step_end(in, ssl, shc);
             else src_adv(in);
             PROF(3)
@@ -395,6 +431,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     }
     PROF_FLUSH(16)
     if (off) { bail6(ws, pkt); ws.claims[pkt] = 0xFFFFFFFFu; return; }
+    ws.dec6_resets[pkt] = rst;
     // an output that does not fit returns 0 (compress.c:617) once the check has
     // passed: until then out_len holds the bytes decoded (bit 31 of the claims)
     sink_finish(o, true);
@@ -492,34 +529,46 @@ extern "C" __global__ __launch_bounds__(256) void rc_dec6_verify(rc_batch_dev b,
         const uint32_t want = cl & 0x7FFFFFFFu;
         const uint32_t n = b.out_len[pkt];
         const uintptr_t lo = reinterpret_cast<uintptr_t>(b.out + b.out_off[pkt]);
-        const uintptr_t base = lo & ~static_cast<uintptr_t>(15);
-#pragma unroll
-        for (uint32_t i = 0; i < 512 / 64; ++i) set4[i * 64 + l] = make_uint4(0u, 0u, 0u, 0u);
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t chunks = n > 1 ? static_cast<uint32_t>((lo + n - base + 15) >> 4) : 0u;
-        for (uint32_t c = l; c < chunks; c += 64) {
-            const uintptr_t a = base + 16 * c;
-            const uint4 w = *reinterpret_cast<const uint4*>(a);
-            uint32_t prev = a > lo ? *reinterpret_cast<const uint8_t*>(a - 1) : 0u;
-            const uint32_t d[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (uint32_t t = 0; t < 16; ++t) {
-                const uint32_t x = (d[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-                const uintptr_t at = a + t;                   // position at - lo
-                if (at > lo && at < lo + n) {
-                    const uint32_t bg = (prev << 8) | x;
-                    atomicOr(&set[bg >> 5], 1u << (bg & 31));
-                }
-                prev = x;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
+        // the model segments (compress.c:148-157): bigrams are counted within each,
+        // the pair across a reset belongs to neither
+        const uint32_t rst = ws.dec6_resets[pkt], nseg = (rst >> 24) + 1;
         uint32_t cnt = 0;
+        for (uint32_t sg = 0; sg < nseg; ++sg) {
+            const uint32_t s0 = sg ? (rst >> (12 * (sg - 1))) & 0xFFFu : 0u;
+            const uint32_t s1 = sg + 1 < nseg ? (rst >> (12 * sg)) & 0xFFFu : n;
 #pragma unroll
-        for (uint32_t i = 0; i < 512 / 64; ++i) {
-            const uint4 q = set4[i * 64 + l];
-            cnt += static_cast<uint32_t>(__builtin_popcount(q.x) + __builtin_popcount(q.y) +
-                                         __builtin_popcount(q.z) + __builtin_popcount(q.w));
+            for (uint32_t i = 0; i < 512 / 64; ++i) set4[i * 64 + l] = make_uint4(0u, 0u, 0u, 0u);
+            __builtin_amdgcn_wave_barrier();
+            const uintptr_t slo = lo + s0;
+            const uintptr_t sb = slo & ~static_cast<uintptr_t>(15);
+            const uint32_t m = s1 > s0 ? s1 - s0 : 0u;
+            const uint32_t chunks = m > 1 ? static_cast<uint32_t>((slo + m - sb + 15) >> 4) : 0u;
+            for (uint32_t c = l; c < chunks; c += 64) {
+                const uintptr_t a = sb + 16 * c;
+                const uint4 w = *reinterpret_cast<const uint4*>(a);
+                uint32_t prev = a > slo ? *reinterpret_cast<const uint8_t*>(a - 1) : 0u;
+                const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (uint32_t t = 0; t < 16; ++t) {
+                    const uint32_t x = (d[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                    const uintptr_t at = a + t;                   // position at - lo
+                    if (at > slo && at < slo + m) {
+                        const uint32_t bg = (prev << 8) | x;
+                        atomicOr(&set[bg >> 5], 1u << (bg & 31));
+                    }
+                    prev = x;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            uint32_t sc = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 512 / 64; ++i) {
+                const uint4 q = set4[i * 64 + l];
+                sc += static_cast<uint32_t>(__builtin_popcount(q.x) + __builtin_popcount(q.y) +
+                                            __builtin_popcount(q.z) + __builtin_popcount(q.w));
+            }
+            cnt += sc;
+            __builtin_amdgcn_wave_barrier();
         }
         for (int sft = 32; sft >= 1; sft >>= 1) cnt += static_cast<uint32_t>(__shfl_xor(static_cast<int>(cnt), sft));
         if (l == 0 && (cnt != want || (ws.dec6_debug & 1))) {

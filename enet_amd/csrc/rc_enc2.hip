@@ -1126,12 +1126,12 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
 }
 
 // coder: one position from its entry (record words; the root's under,
-// count and total at the position)
-DEV void code_pos(CodeState& k, Ring& o, const uint4& qe, bool en, const double* rtab, uintptr_t dummy)
+// count and total at the position) and its prepared sub-context codes p (the
+// part's four prepared before its first code: their LDS reads and reciprocals
+// are off the chain through low and range)
+DEV void code_pos(CodeState& k, Ring& o, const uint4& qe, const Pre& p, double r0, uintptr_t dummy)
 {
     const uint32_t n0 = o.n;
-    const Pre p = prep_tab(qe.x, qe.y, en, rtab);
-    const double r0 = rcp64(p.e0 ? qe.w : 1u);
     code(k.low, k.range, p.u1, p.c1, p.r1, o);
     if (any_lane(p.e2)) code(k.low, k.range, p.u2, p.c2, p.r2, o);
     code(k.low, k.range, p.e0 ? 1 + (qe.z & 0xFFFF) : 0u, p.e0 ? 1 + (qe.z >> 16) : 1u, r0, o);
@@ -1224,10 +1224,14 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
         const uint4 q2 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 2, lane));
         const uint4 q3 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 3, lane));
         const uint32_t i = 4 * s;
-        code_pos(k, o, q0, i < len, rtab, dummy);
-        code_pos(k, o, q1, i + 1 < len, rtab, dummy);
-        code_pos(k, o, q2, i + 2 < len, rtab, dummy);
-        code_pos(k, o, q3, i + 3 < len, rtab, dummy);
+        const Pre p0 = prep_tab(q0.x, q0.y, i < len, rtab), p1 = prep_tab(q1.x, q1.y, i + 1 < len, rtab);
+        const Pre p2 = prep_tab(q2.x, q2.y, i + 2 < len, rtab), p3 = prep_tab(q3.x, q3.y, i + 3 < len, rtab);
+        const double r00 = rcp64(p0.e0 ? q0.w : 1u), r01 = rcp64(p1.e0 ? q1.w : 1u);
+        const double r02 = rcp64(p2.e0 ? q2.w : 1u), r03 = rcp64(p3.e0 ? q3.w : 1u);
+        code_pos(k, o, q0, p0, r00, dummy);
+        code_pos(k, o, q1, p1, r01, dummy);
+        code_pos(k, o, q2, p2, r02, dummy);
+        code_pos(k, o, q3, p3, r03, dummy);
         C2P_WORK
         lds_barrier();                                // (the helpers may overwrite this part now)
         C2P_WAIT

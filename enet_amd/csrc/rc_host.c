@@ -71,7 +71,8 @@ static int ws_reserve(rc_ctx *c, size_t n)
     size_t cap = c->ws.n_cap ? c->ws.n_cap : 1024;
     while (cap < n) cap *= 2;
     uint32_t *fl = NULL, *ord = NULL, *el = NULL, *wl = NULL, *cl = NULL;
-    if (hipMalloc((void **) &cl, cap * sizeof(uint32_t)) != hipSuccess) return -1;
+    /* claims and the decoder's reset positions side by side */
+    if (hipMalloc((void **) &cl, 2 * cap * sizeof(uint32_t)) != hipSuccess) return -1;
     if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(cl); return -1; }
     if (hipMalloc((void **) &ord, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(cl); hipFree(fl); return -1; }
     if (hipMalloc((void **) &el, cap * sizeof(uint32_t)) != hipSuccess) {
@@ -89,6 +90,7 @@ static int ws_reserve(rc_ctx *c, size_t n)
         hipFree(c->ws.claims);
     }
     c->ws.claims = cl;
+    c->ws.dec6_resets = cl + cap;
     c->ws.flag_list = fl;
     c->ws.order = ord;
     c->ws.enc2_list = el;

@@ -31,16 +31,22 @@ static void slot_host_kick()
 }  // namespace
 static uint8_t g_tab6[RC_DEC6_TAB_BYTES] __attribute__((aligned(16)));   // bucket records (never cleared)
 
-// rc_dec6_verify on the host: distinct bigrams of the output
-static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n)
+// rc_dec6_verify on the host: distinct bigrams of the output, per model
+// segment (rst: the segments' starts after the first, as rc_dec6.hip records them)
+static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n, uint32_t rst = 0)
 {
     static uint8_t seen[65536];
-    memset(seen, 0, sizeof seen);
     uint32_t c = 0;
-    for (uint32_t j = 1; j < n; ++j) {
-        const uint32_t b = (x[j - 1] << 8) | x[j];
-        c += seen[b] ? 0u : 1u;
-        seen[b] = 1;
+    const uint32_t nseg = (rst >> 24) + 1;
+    for (uint32_t sg = 0; sg < nseg; ++sg) {
+        const uint32_t s0 = sg ? (rst >> (12 * (sg - 1))) & 0xFFFu : 0u;
+        const uint32_t s1 = sg + 1 < nseg ? (rst >> (12 * sg)) & 0xFFFu : n;
+        memset(seen, 0, sizeof seen);
+        for (uint32_t j = s0 + 1; j < s1; ++j) {
+            const uint32_t b = (x[j - 1] << 8) | x[j];
+            c += seen[b] ? 0u : 1u;
+            seen[b] = 1;
+        }
     }
     return c;
 }
@@ -108,11 +114,12 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
         memset(region, 0, need);                                   // like the device pool (epoch 0 = unused)
     }
     uint64_t ioff = 0, ooff = 0;
-    uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0}, bails[2] = {0, 0}, claims[1] = {0};
+    uint32_t flags[2] = {0, 0}, counters[4] = {0, 0, 0, 0}, bails[2] = {0, 0}, claims[1] = {0}, resets[1] = {0};
     rc_batch_dev b = { in, &ioff, &len, out, &ooff, &cap, out_len, 1, max_len };
     rc_workspace_dev ws = {};
     ws.flag_list = flags; ws.counters = counters; ws.enc2_list = bails; ws.lane_region = need; ws.lane_pool = region; ws.lane_active = 64;
     ws.claims = claims;
+    ws.dec6_resets = resets;
     *out_len = 0xFFFFFFFFu;
 #ifdef DEC4
     // the bucket-history decoder first; a packet it leaves goes to the lanes (as on the GPU)
@@ -137,7 +144,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
         decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, itab6(), src6);
         g_b6s = nullptr;
 #endif
-        if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
+        if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len, resets[0])) {
             counters[3] = 1; g_dec6_unverified++;
         }
         if (!counters[3] && (claims[0] >> 31)) *out_len = 0;

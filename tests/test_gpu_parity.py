@@ -288,6 +288,27 @@ def test_long_packets_and_model_reset(coder):
         assert r == (len(p), p)
 
 
+def test_mtu_packets_model_reset_on_fast_decoder(coder):
+    """Random packets of 1920-4096 bytes go through compress.c's model reset
+    (4094 nodes, compress.c:148-157) once or twice: the record-light decoder
+    resets its model itself (rc_dec6.hip reset6) and its check counts bigrams
+    per model segment, so on the default variants none is left to the lane
+    kernels.  Bit-exact against the oracle."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(0x4D54)
+    sizes = [4096] * 64 + [int(x) for x in rng.integers(1920, 4097, size=448)]
+    pk = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in sizes]
+    comp = [port.compress(p, 2 * len(p) + 64)[1] for p in pk]
+    back = _run(coder, True, comp, [4096] * len(comp), max_len=max(len(c) for c in comp))
+    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+        assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
+    assert all(b == (len(p), p) for b, p in zip(back, pk))
+    # output limits inside the second segment
+    back = _run(coder, True, comp[:64], [3000] * 64, max_len=max(len(c) for c in comp))
+    assert all(b == port.decompress(c, 3000) for b, c in zip(back, comp[:64]))
+
+
 def test_random_fuzz_vs_oracle(coder):
     from oracle.pyoracle import Coder
     port = Coder("port")

@@ -105,6 +105,34 @@ def test_dec4_takes_random_packets(lane):
     assert lane.left == 0
 
 
+def test_dec6_model_reset(lane):
+    """The record-light decoder through compress.c's model reset (4094 nodes,
+    compress.c:148-157): random packets of 1900-4096 bytes (one or two resets)
+    decoded by dec6 itself, checked per model segment, against the oracle at
+    output limits on either side of a reset; corrupt streams stay correct."""
+    if lane.version not in ("v6", "v6s"):
+        pytest.skip("dec6 only")
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(29)
+    valid_left = 0
+    sizes = [1900, 1950, 2100, 2731, 3000, 4095, 4096] + list(rng.integers(1920, 4097, size=8))
+    for n in sizes:
+        p = rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes()
+        r, c = port.compress(p, 2 * len(p) + 64)
+        lane.left = 0
+        for lim in (len(p), len(p) - 1, 2000, 4096):
+            got = lane(1, c, lim, max_len=4096)
+            assert got == port.decompress(c, lim), (n, lim)
+        valid_left += lane.left
+        bad = bytearray(c)
+        bad[len(bad) * 3 // 4] ^= 0x21
+        got = lane(1, bytes(bad), 4096, max_len=4096)
+        if got[0] != "exact":
+            assert got == port.decompress(bytes(bad), 4096)
+    assert valid_left == 0, valid_left
+
+
 def test_lane_logic_region_overflow_routes_exact(lane):
     # a tiny region (max_len hint 16) cannot hold a 1200-byte random packet's model
     # (v3 keeps single-symbol order-2 contexts inline, so it needs a small
