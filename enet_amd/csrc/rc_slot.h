@@ -65,11 +65,12 @@ DEV void slot_take(SlotSrc& s, const uint4& sl, uint32_t hc, bool en)
     s.want = t ? s.j + 1 : s.want;
 }
 
-// the end of a step: the next chunk if the slot holds it, the lookahead topped up
+// the end of a step: the next chunk if the slot holds it, the lookahead topped
+// up by a dword (a step takes about one byte; one that takes more than the
+// lookahead holds waits in dec_code's slow path)
 DEV void slot_step_end(SlotSrc& s, const uint4& sl, uint32_t hc)
 {
     slot_take(s, sl, hc, s.q == 4);
-    slot_fill(s, true);
     slot_fill(s, true);
     slot_publish(s);
 #ifdef RC_LANE_HOST_TEST
