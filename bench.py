@@ -148,6 +148,16 @@ def run_workload(coder, dev, stream, kind, n, size, rank, steps, warmup, dist=No
     roofline = {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "alg_bytes_per_launch": alg,
                 "launch_ms": round(t_dom * 1e3, 4)}
+    traffic, tsrc = measured_traffic(kname, kind, n)
+    roofline["traffic"] = traffic
+    roofline["traffic_source"] = tsrc
+    if traffic:
+        # what the kernel actually moves: PMC HBM bytes per launch (separate
+        # rocprofv3 --pmc passes of this workload) over this launch time
+        rate = traffic / t_dom / 1e9
+        roofline["traffic_GBps"] = round(rate, 1)
+        roofline["traffic_frac_of_peak"] = round(rate / HBM_PEAK_GBPS, 4)
+        roofline["traffic_over_alg"] = round(traffic / alg, 2)
     summary = {
         "workload": WORKLOADS[kind], "packets": n, "value": round(in_bytes * world * steps / elapsed / GIB, 4),
         "unit": "GiB/s", "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": warmup,
@@ -184,18 +194,8 @@ def main():
     d, o, l, din, doff, dlen = raw["d"], raw["o"], raw["l"], raw["din"], raw["doff"], raw["dlen"]
     n, in_bytes, max_len = raw["n"], raw["in_bytes"], raw["max_len"]
     roofline = main_line["roofline"]
-    traffic, tsrc = measured_traffic(roofline["kernel"], args.workload, n)
-    roofline["traffic"] = traffic
-    roofline["traffic_source"] = tsrc
     roofline["compress_ms"] = main_line["compress_ms"]
     roofline["decompress_ms"] = main_line["decompress_ms"]
-    if traffic:
-        # what the kernel actually moves: PMC HBM bytes per launch (a separate
-        # rocprofv3 --pmc pass of this command) over this launch time
-        rate = traffic / raw["t_dom"] / 1e9
-        roofline["traffic_GBps"] = round(rate, 1)
-        roofline["traffic_frac_of_peak"] = round(rate / HBM_PEAK_GBPS, 4)
-        roofline["traffic_over_alg"] = round(traffic / roofline["alg_bytes_per_launch"], 2)
 
     result = {
         "metric": "GiB/s device-resident range-coder (de)compress, 64Ki×1200B pkts, 1/2/4/8 GPU",
@@ -604,9 +604,10 @@ def dominant_kernel(decompress, handed_off=0, n=1):
 
 def measured_traffic(kernel, workload, packets):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/traffic_latest.json, written by tools/traffic.py from
-    separate --pmc passes of this same bench command), or None."""
-    path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    summary of this workload (profiles/traffic_<workload>.json, written by
+    tools/traffic.py from separate --pmc passes of the same bench workload,
+    tools/evidence.sh), or None."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
     try:
         with open(path) as f:
             t = json.load(f)
@@ -617,7 +618,7 @@ def measured_traffic(kernel, workload, packets):
     k = t.get("kernels", {}).get(kernel)
     if not k:
         return None, None
-    return k.get("hbm_bytes_per_launch"), "profiles/traffic_latest.json (" + t.get("source", "") + ")"
+    return k.get("hbm_bytes_per_launch"), f"profiles/traffic_{workload}.json (" + t.get("source", "") + ")"
 
 
 def cpu_threads_available():

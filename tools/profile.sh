@@ -19,6 +19,7 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
            "TCC_EA0_WRREQ TCC_EA0_WRREQ_64B" \
            "SQ_WAVES SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_IFETCH"; do
   i=$((i+1))
+  echo "pmc pass $((i)) $grp"
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o run -- $B --steps 1 --warmup 0 "$@" > $OUT/bench_pmc$i.log 2>&1 || echo "pmc group $i failed: $grp" >> $OUT/errors.txt
 done
 echo done
