@@ -1028,7 +1028,7 @@ DEV void main7_packet(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
-    if (len == 0) { bt.out_len[pkt] = 0; ws.claims[pkt] = 0; return; }     // compress.c:513
+    if (len == 0) { bt.out_len[pkt] = 0; ws.claims[pkt] = 0; ws.dec6_resets[pkt] = 0; return; }     // compress.c:513
     uint8_t* root = x.lane;
     uint8_t* stats = x.lane + kStats7;
     // a new packet: generation, first wanted chunk (published once the stream is set up)
@@ -1194,6 +1194,7 @@ DEV void main7_packet(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32
     sink_finish(o, true);
     bt.out_len[pkt] = o.n;
     ws.claims[pkt] = claims | (fail ? 0x80000000u : 0u);
+    ws.dec6_resets[pkt] = 0;                          // (one model segment: rc_dec6_verify's layout)
 }
 
 }  // namespace

@@ -32,12 +32,15 @@
 // tests/proto/twopass.py restates both passes and the record format in
 // Python (checked against the oracle on the CPU, tests/test_twopass_model.py).
 //
-// Fast path: 1 <= N <= 1919 (no model reset, compress.c:148-157) and no
-// bucket over 64 positions (every statistic <= 63, so no count reaches the
-// rescale threshold, compress.c:313).  Packets with a bigger bucket go to the
-// wide mode (rc_enc2_wscan / rc_enc2_wcode, below: explicit intervals, dense
-// walks with rescales); longer packets are listed for the lane kernels,
-// which run after the passes on that list only.
+// Fast path: 1 <= N <= 4096 and no bucket over 64 positions (every
+// statistic <= 63, so no count reaches the rescale threshold,
+// compress.c:313).  A packet over 1919 B can reach the model reset
+// (compress.c:148-157): the scan takes it in windows, one per model segment
+// (reset_after), and the code pass resets the root where a record carries
+// kRst.  Packets with a bigger bucket go to the wide mode (rc_enc2_wscan /
+// rc_enc2_wcode, below: explicit intervals, dense walks with rescales) when
+// they are at most 1919 B; the rest are listed for the lane kernels, which
+// run after the passes on that list only.
 //
 // Record of position i: two words (w0, w1)
 //   w0 bits 0-2 type, 3-8 tA, 9-14 dA, 16-27 ext
@@ -95,6 +98,7 @@ struct E2Prof {};
 namespace {
 
 constexpr uint32_t kE2MaxLen = 1919;          // compress.c:148-157: no reset below 1920 B
+constexpr uint32_t kE2SlotMax = 4096;         // longest packet of the narrow scan (windows past a reset)
 constexpr uint32_t kE2Bucket = 64;            // statistics <= 63
 constexpr uint32_t kScanThreads = 64;         // one wavefront per packet, four buckets per lane
 constexpr uint32_t kSkipFallback = 0xFFFFFFFFu;   // first word of a slot: lane kernels
@@ -104,7 +108,7 @@ constexpr uint32_t kSkipWide = 0xFFFFFFFDu;       // the wide kernels (the small
 struct E2Params {
     uint8_t*        stream;     // record stream, one slot per packet of the chunk
     uint64_t        slot_bytes;
-    uint32_t        slot_len;   // longest packet a slot holds: min(max_len or 4096, kE2MaxLen)
+    uint32_t        slot_len;   // longest packet a slot holds: min(max_len or 4096, kE2SlotMax)
     uint32_t        lo, hi;     // chunk: batch indices [lo, hi)
     const uint32_t* order;      // batch index -> packet (length-binned), or null
     const uint32_t* bins;       // bins[RC_LEN_BINS] != 0: order not built (uniform batch)
@@ -437,6 +441,75 @@ DEV ScanPf scan_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t idx)
     return f;
 }
 
+// first word of a model segment's position-0 record after a reset (w0 bit 15: unused by the types)
+constexpr uint32_t kRst = 1u << 15;
+constexpr uint32_t kMaxNodesE2 = 4096 - 2;       // compress.c:150
+
+// The nodes compress.c creates at each position of a window scanned as a
+// packet (compress.c:68-88 via :286-337): position 0 the root's; a position
+// found nowhere (its record visits the root) creates the root's node at the
+// byte's first root visit, its order-1 node (position >= 1) and its order-2
+// node (>= 2); an order-1 hit its order-2 node (>= 2); an order-2 hit none.
+// Returns the window position after whose byte the node count reaches 4094
+// (compress.c:148-157), or n.  After the scan's walks (every element's
+// found flags final); the window's bytes in s.x and the bucket ends in s.cnt
+// are reused.
+template <class S>
+DEV uint32_t reset_after(S& s, uint32_t n, uint32_t x0, uint32_t t)
+{
+    uint8_t* inc = s.x;                                   // per position: nodes | 0x80 = root visit
+    const uint4 e4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
+    const uint4 b4 = *reinterpret_cast<const uint4*>(&s.start[4 * t]);
+    wave_sync();
+    *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(~0u, ~0u, ~0u, ~0u);   // the first root visit per byte
+    wave_sync();
+    if (t == 0) { s.cnt[x0] = 0u; inc[0] = 1; }
+#pragma unroll 1
+    for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t be = pick4(r, e4);
+        for (uint32_t k = pick4(r, b4); k < be; ++k) {
+            const uint32_t w = s.e[k], pos = w & 2047;
+            const bool rv = (w & (kF2 | kF1)) == 0;
+            const uint32_t c = rv ? (pos >= 1 ? 1u : 0u) + (pos >= 2 ? 1u : 0u) : ((w & kF2) ? 0u : (pos >= 2 ? 1u : 0u));
+            inc[pos] = static_cast<uint8_t>(c | (rv ? 0x80u : 0u));
+            if (rv) atomicMin(&s.cnt[(w >> 11) & 255], pos);
+        }
+    }
+    wave_sync();
+#pragma unroll 1
+    for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t be = pick4(r, e4);
+        for (uint32_t k = pick4(r, b4); k < be; ++k) {
+            const uint32_t w = s.e[k], pos = w & 2047;
+            if ((w & (kF2 | kF1)) == 0 && s.cnt[(w >> 11) & 255] == pos) inc[pos] = static_cast<uint8_t>(inc[pos] + 1);
+        }
+    }
+    wave_sync();
+    // positions 32 t .. 32 t + 31: their sum, the prefix over the lanes, the first crossing
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t q = 0; q < 32; ++q) {
+        const uint32_t pos = 32 * t + q;
+        sum += pos < n ? (inc[pos] & 0x7Fu) : 0u;
+    }
+    uint32_t acc = 1 + wave_incl_scan(sum) - sum;        // nodes before position 32 t (the root: 1)
+    uint32_t hit = n;
+    if (acc + sum >= kMaxNodesE2) {
+#pragma unroll 1
+        for (uint32_t q = 0; q < 32; ++q) {
+            const uint32_t pos = 32 * t + q;
+            if (pos >= n) break;
+            acc += inc[pos] & 0x7Fu;
+            if (acc >= kMaxNodesE2) { hit = pos; break; }
+        }
+    }
+    // the lowest lane's crossing
+    const uint64_t m = __builtin_amdgcn_ballot_w64(hit < n);
+    const uint32_t r = m ? __builtin_amdgcn_readlane(hit, static_cast<uint32_t>(__builtin_ctzll(m))) : n;
+    wave_sync();
+    return r;
+}
+
 // Same-address LDS atomics in lane order within an instruction and in
 // program order across instructions, for a full conflict (twice) and for
 // partial ones (4 words, lanes interleaved, blocked and hashed onto them).
@@ -483,12 +556,12 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
     ScanPf pf = scan_prefetch(b, e, e.lo + blockIdx.x);
     for (uint32_t idx = e.lo + blockIdx.x; idx < e.hi; idx += gridDim.x) {
         const ScanPf cur = pf;
-        const uint32_t pkt = cur.pkt, n = cur.n, mis = cur.mis;
+        const uint32_t pkt = cur.pkt, len = cur.n;
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
-        // compress.c:257 / possible model reset, or longer than the caller's
-        // max_len (its slot holds 8 B per position up to slot_len only)
-        if (n == 0 || n > e.slot_len) {
-            if (n == 0) {
+        // compress.c:257, or longer than the caller's max_len (its slot holds
+        // 8 B per position up to slot_len only)
+        if (len == 0 || len > e.slot_len) {
+            if (len == 0) {
                 if (t == 0) { slot[0] = kSkipDone; b.out_len[pkt] = 0; }
             } else {
                 fb_add(s, e, slot, pkt, t);
@@ -496,9 +569,23 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
             pf = scan_prefetch(b, e, idx + gridDim.x);
             continue;
         }
-        // the packet into LDS (prefetched): aligned 16-B chunks, x = s.x + 16 + misalignment
-        *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = cur.r0;
-        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = cur.r1;
+        // A packet longer than kE2MaxLen can reach compress.c's model reset
+        // (:148-157): it is scanned in windows, each starting a model segment
+        // (the window a packet of its own) and as long as the LDS holds; the
+        // nodes the window's positions create give the byte after which the
+        // model resets, the next window starts after it (its position 0
+        // record carries kRst), and the records this window wrote past that
+        // byte are rewritten by the next.
+        uint32_t s0 = 0, mis = cur.mis;
+        uint4 c0 = cur.r0, c1 = cur.r1;
+        bool fetched = false;
+        const uintptr_t src0 = reinterpret_cast<uintptr_t>(b.in + const_load(b.in_off, pkt));
+#pragma unroll 1
+        for (;;) {
+        const uint32_t n = min(len - s0, 2048u - mis);
+        // the window into LDS: aligned 16-B chunks, x = s.x + 16 + misalignment
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = c0;
+        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = c1;
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = z;
         if (t < 16) *reinterpret_cast<uint4*>(&s.excm[4 * t]) = z;
@@ -552,9 +639,10 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
         const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
         const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
         if (any_lane(mx > kE2Bucket)) {
-            big_add(s, e, slot, pkt, idx, t);
-            pf = scan_prefetch(b, e, idx + gridDim.x);
-            continue;
+            if (len > kE2MaxLen) fb_add(s, e, slot, pkt, t);     // (the wide kernels do not reset)
+            else big_add(s, e, slot, pkt, idx, t);
+            if (!fetched) pf = scan_prefetch(b, e, idx + gridDim.x);
+            break;
         }
         const uint32_t a0 = (c4.x + 3) & ~3u, a1 = (c4.y + 3) & ~3u, a2 = (c4.z + 3) & ~3u, a3 = (c4.w + 3) & ~3u;
         const uint32_t mine = a0 + a1 + a2 + a3;
@@ -575,7 +663,7 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
         // walked in full below.  (A per-position check of the predecessor
         // slot cost 4 % of the encoder and could not see a later position
         // taking an earlier slot, whose write comes after the check.)
-        uint2* rec = reinterpret_cast<uint2*>(slot);
+        uint2* rec = reinterpret_cast<uint2*>(slot) + s0;
         for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
             // (branch-free as above: reads, then atomics and starts, then writes)
             uint32_t b3[4], ew[4], w[4], k[4], bb[4], st[4];
@@ -617,7 +705,8 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
         const uint32_t x0 = x[0];
         wave_sync();
         const bool disorder = !ordered;                // (wave-uniform)
-        pf = scan_prefetch(b, e, idx + gridDim.x);     // (the bytes in LDS are not read past here)
+        if (!fetched) pf = scan_prefetch(b, e, idx + gridDim.x);     // (the bytes in LDS are not read past here)
+        fetched = true;
         E2P(3)
         // buckets with exceptional positions: compacted over the lanes, one
         // per lane, each walked in full
@@ -655,9 +744,24 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
                 walk_from(s, bs, kk, ~0u, rec);
             }
         }
-        if (t == 0) rec[0] = make_uint2(0u, x0 << 24);  // position 0: root only
+        if (t == 0) rec[0] = make_uint2(s0 ? kRst : 0u, x0 << 24);  // position 0: root only (after a reset)
         wave_sync();                              // LDS reuse by the next packet
         E2P(5)
+        if (len <= kE2MaxLen) break;              // (no reset: <= 2 * 1918 + 256 nodes, compress.c:150)
+        const uint32_t r = reset_after(s, n, x0, t);
+        if (r >= n) {                             // no reset in the window
+            if (s0 + n < len) fb_add(s, e, slot, pkt, t);   // a segment longer than the window: lane kernels
+            break;
+        }
+        s0 += r + 1;
+        if (s0 >= len) break;                     // (the reset after the last byte changes nothing)
+        // the next window's bytes (not prefetched: only long packets get here)
+        const uintptr_t src = src0 + s0, a16 = src & ~static_cast<uintptr_t>(15);
+        mis = static_cast<uint32_t>(src & 15);
+        const uint32_t last = (mis + (len - s0) - 1) >> 4;
+        c0 = gload16(a16 + 16 * min(t, last));
+        c1 = gload16(a16 + 16 * min(t + kScanThreads, last));
+        }
     }
     fb_flush(s, e, t);
     wb_flush(s, e, t);
@@ -810,7 +914,7 @@ DEV void sub_interval(uint32_t t, uint32_t d, uint32_t same, uint32_t less, bool
 struct Pre {
     uint32_t u1, c1, u2, c2, v;
     double r1, r2;
-    bool e2, e0;
+    bool e2, e0, rst;           // rst: the model resets before this position (kRst)
 };
 
 DEV Pre prep(uint32_t w0, uint32_t w1, bool en)
@@ -831,6 +935,7 @@ DEV Pre prep(uint32_t w0, uint32_t w1, bool en)
     p.c2 = p.e2 ? ct2 : 1u;
     p.r2 = rcp64(p.e2 ? tt2 : 1u);
     p.v = w1 >> 24;
+    p.rst = en && (w0 & kRst) != 0;
     return p;
 }
 
@@ -855,6 +960,7 @@ DEV Pre prep_tab(uint32_t w0, uint32_t w1, bool en, const double* rtab)
     p.c2 = p.e2 ? ct2 : 1u;
     p.r2 = rtab[p.e2 ? tt2 : 1u];
     p.v = w1 >> 24;
+    p.rst = en && (w0 & kRst) != 0;
     return p;
 }
 
@@ -871,6 +977,14 @@ DEV void code_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, co
 {
     E2Q(0)
     const uint32_t n0 = o.n;
+    if (rare_lane(p.rst)) {                           // compress.c:148-157, after the previous byte
+        if (p.rst) {
+            Root R;
+            root3_clear<true>(root, R);
+            k.rtot = 1 + 256;
+            k.rrt = rcp64(k.rtot);
+        }
+    }
     // the root lookup needs only v: LDS reads whose latency overlaps the
     // sub-context codes
     uint32_t under0, cnt0;
@@ -1048,6 +1162,11 @@ DEV bool root_codes(uint32_t w0) { const uint32_t typ = w0 & 7; return typ <= 1 
 DEV void help_pos(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, uint32_t w0, uint32_t w1, bool en,
                   uint32_t& rtot, uint8_t* qe)
 {
+    if (en && (w0 & kRst)) {                          // compress.c:148-157, after the previous byte
+        Root R;
+        root3_clear<true>(root, R);
+        rtot = 1 + 256;
+    }
     const uint32_t v = w1 >> 24;
     uint32_t under0, cnt0;
     root3_lookup(root, mtab, v, under0, cnt0);
@@ -1092,6 +1211,7 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
     uint32_t t = rtot;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
+        rs = rs || (i + j < len && (w0[j] & kRst));     // a model reset in the part: position by position
         root3_lookup_sum(lk[j], v[j], under[j], cnt[j]);
 #pragma unroll
         for (uint32_t q = 0; q < j; ++q) {
@@ -1102,7 +1222,7 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
         t = e0[j] ? ((t + kRootDelta) & 0xFFFF) : t;
         rs = rs || (e0[j] && (1 + cnt[j] > 0xFF - 2 * kRootDelta + 1 || t > kTotalLimit));
     }
-    if (any_lane(rs)) {                               // (rare) position by position, rescales included
+    if (any_lane(rs)) {                               // (rare) position by position, rescales and resets included
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
             help_pos(root, mtab, itab, w0[j], w1[j], i + j < len, rtot, q_entry(smem, part, j, lane));
@@ -2019,7 +2139,7 @@ extern "C" int rc_enc2_prof_read(unsigned long long* out, int reset)
 // bytes of one packet's record slot for packets of up to max_len bytes
 extern "C" uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len)
 {
-    const uint64_t l = max_len < kE2MaxLen ? max_len : kE2MaxLen;
+    const uint64_t l = max_len < kE2SlotMax ? max_len : kE2SlotMax;
     return ((8 * l + 15) & ~15ull) + 96;              // 8 B per position, + the chunks read ahead
 }
 
@@ -2048,7 +2168,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     E2Params e;
     e.stream = static_cast<uint8_t*>(ws->enc2_stream);
     e.slot_bytes = slot;
-    e.slot_len = ml < kE2MaxLen ? ml : kE2MaxLen;
+    e.slot_len = ml < kE2SlotMax ? ml : kE2SlotMax;
     e.dummy = static_cast<uint8_t*>(ws->enc2_stream) + ws->enc2_cap;   // (allocated past the stream)
     e.order = ws->order;
     e.bins = ws->bins;

@@ -309,6 +309,37 @@ def test_mtu_packets_model_reset_on_fast_decoder(coder):
     assert all(b == port.decompress(c, 3000) for b, c in zip(back, comp[:64]))
 
 
+def test_mtu_packets_model_reset_on_fast_encoder(coder):
+    """Packets of 1920-4096 bytes reach compress.c's model reset (4094 nodes,
+    compress.c:148-157): the two-pass encoder scans them in windows, one per
+    model segment (rc_enc2.hip reset_after), and its code pass resets the
+    root where a record carries kRst; on the default variants none is left
+    to the lane kernels.  Random, de Bruijn and small-alphabet packets
+    (several resets, resets late in a window), bit-exact against the oracle,
+    and back."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(0x454E)
+    sizes = [4096] * 96 + [1920, 1921, 2047, 2048, 2049, 3071, 4095] + [int(x) for x in rng.integers(1920, 4097, size=320)]
+    pk = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in sizes]
+    narrow = len(pk)
+    pk += [synth.de_bruijn_bytes(n) for n in (1920, 2600, 4096)]
+    pk += [rng.integers(0, 40, size=4096, dtype=np.uint8).tobytes() for _ in range(8)]
+    caps = [2 * len(p) + 64 for p in pk]
+    res = _run(coder, False, pk[:narrow], caps[:narrow])
+    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+        assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
+    res += _run(coder, False, pk[narrow:], caps[narrow:])
+    for p, c, r in zip(pk, caps, res):
+        assert r == port.compress(p, out_limit=c), len(p)
+    # output limits that cut a packet inside its second model segment
+    cut = _run(coder, False, pk[:32], [2100] * 32)
+    for p, r in zip(pk[:32], cut):
+        assert r == port.compress(p, out_limit=2100)
+    back = _run(coder, True, [r[1] for r in res], [4096] * len(res), max_len=max(len(r[1]) for r in res))
+    assert all(b == (len(p), p) for b, p in zip(back, pk))
+
+
 def test_random_fuzz_vs_oracle(coder):
     from oracle.pyoracle import Coder
     port = Coder("port")
