@@ -112,6 +112,77 @@ DEV void reset6(uint8_t* root, uint8_t* stats, Root& R, uint32_t& rtot, double& 
 // another segment fits the record: at most two resets, starts below 4096
 DEV bool can_reset6(uint32_t rst, uint32_t n) { return (rst >> 24) < 2 && n < 4096; }
 
+// ---- output: one byte per step (rc_lane_common.h's ByteSink, specialised).
+// Bytes gather in a dword (acc, nb of them); a full dword shifts into the
+// 16-B window w (a shift register: its dwords in output order, the window's
+// lead dwords before an unaligned start counted in ws from the start); a
+// full window waits in wp for its store at the top of the next step.  At
+// most one window completes per step, and every step (common or rare)
+// flushes the previous one first.
+struct ByteSink1 {
+    uint32_t acc, nb, ws;
+    uint4 w, wp;
+    bool pend;
+    uintptr_t waddr, wpaddr, lo;
+    uint32_t n, cap;
+};
+
+DEV void sink1_init(ByteSink1& o, uint8_t* p, uint32_t cap)
+{
+    o.lo = reinterpret_cast<uintptr_t>(p);
+    o.waddr = o.lo & ~static_cast<uintptr_t>(15);
+    o.wpaddr = o.waddr;
+    o.ws = static_cast<uint32_t>(o.lo & 15) >> 2;     // (lead bytes before an unaligned start are never stored)
+    o.nb = static_cast<uint32_t>(o.lo & 3);
+    o.acc = 0;
+    o.w = make_uint4(0u, 0u, 0u, 0u);
+    o.wp = o.w;
+    o.pend = false;
+    o.n = 0;
+    o.cap = cap;
+}
+
+DEV void sink1_flush(ByteSink1& o)
+{
+    sink_store(o.wpaddr, o.wp, o.lo, o.pend);
+    o.pend = false;
+}
+
+DEV void sink1_put(ByteSink1& o, uint32_t v, bool en)
+{
+    o.acc |= en ? (v << (8 * o.nb)) : 0u;
+    o.nb += en ? 1u : 0u;
+    o.n += en ? 1u : 0u;
+    const bool mv = o.nb == 4;
+    o.w.x = mv ? o.w.y : o.w.x; o.w.y = mv ? o.w.z : o.w.y; o.w.z = mv ? o.w.w : o.w.z; o.w.w = mv ? o.acc : o.w.w;
+    o.acc = mv ? 0u : o.acc;
+    o.nb = mv ? 0u : o.nb;
+    o.ws += mv ? 1u : 0u;
+    const bool full = o.ws == 4;
+    o.wp.x = full ? o.w.x : o.wp.x; o.wp.y = full ? o.w.y : o.wp.y;
+    o.wp.z = full ? o.w.z : o.wp.z; o.wp.w = full ? o.w.w : o.wp.w;
+    o.wpaddr = full ? o.waddr : o.wpaddr;
+    o.pend = o.pend || full;
+    o.ws = full ? 0u : o.ws;
+    o.waddr += full ? 16 : 0;
+}
+
+// the pending window, then the partial one: its ws dwords (the last ws of the
+// shift register) and the nb bytes of acc
+DEV void sink1_finish(ByteSink1& o)
+{
+    sink1_flush(o);
+    const uint32_t ws = o.ws;
+    const uint32_t d[4] = {o.w.x, o.w.y, o.w.z, o.w.w};
+    uint32_t q[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t k = 4 - ws + j;                // (j < ws: dword k of the shift register)
+        q[j] = j < ws ? (k == 0 ? d[0] : k == 1 ? d[1] : k == 2 ? d[2] : d[3]) : (j == ws ? o.acc : 0u);
+    }
+    sink_bytes(o.waddr, make_uint4(q[0], q[1], q[2], q[3]), 0ull, 4 * ws + o.nb, o.lo);
+}
+
 // Src: ByteSrc (the stream's chunks loaded by the lane, rc_decompress_dec6) or
 // SlotSrc (through the LDS slot a helper wavefront refills, rc_slot.h,
 // rc_decompress_dec6s).
@@ -123,8 +194,8 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
     if (len == 0) { bt.out_len[pkt] = 0; ws.claims[pkt] = 0; ws.dec6_resets[pkt] = 0; return; }     // compress.c:513
-    ByteSink o;
-    sink_init(o, bt.out + bt.out_off[pkt], cap);
+    ByteSink1 o;
+    sink1_init(o, bt.out + bt.out_off[pkt], cap);
     uint32_t code;
     if constexpr (kSlot) {
         code = slot_init(in, bt.in + bt.in_off[pkt], len, pkt);
@@ -177,7 +248,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             } else {
                 src_fill(in, true);
             }
-            sink_flush(o);
+            sink1_flush(o);
             const bool go = !done && !stall;
 #ifdef DEC6_STATS_PREFETCH
             const uint32_t st = (go && order >= 1) ? stn : 0u;
@@ -259,7 +330,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             off = off || lv;
             fail = fail || fl;
             done = done || eos || lv || fl;
-            sink_put(o, v, 1, sym && !lv && !fl);
+            sink1_put(o, v, sym && !lv && !fl);
             a = sym ? p : a;
             p = sym ? v : p;
             order += (sym && order < 2) ? 1u : 0u;
@@ -296,7 +367,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             } else {
                 src_fill(in, true);
             }
-            sink_flush(o);
+            sink1_flush(o);
 #ifndef DEC6_NO_DRAIN
             __builtin_amdgcn_s_waitcnt(0);            // (the blind stores of this lane's records)
 #endif
@@ -391,7 +462,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             off = off || (rs && lv);
             fail = fail || (rs && fl);
             done = done || (rs && (eos || lv || fl));
-            sink_put(o, v, 1, sym && !lv && !fl);
+            sink1_put(o, v, sym && !lv && !fl);
             a = sym ? p : a;
             p = sym ? v : p;
             order += (sym && order < 2) ? 1u : 0u;
@@ -434,7 +505,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     ws.dec6_resets[pkt] = rst;
     // an output that does not fit returns 0 (compress.c:617) once the check has
     // passed: until then out_len holds the bytes decoded (bit 31 of the claims)
-    sink_finish(o, true);
+    sink1_finish(o);
     bt.out_len[pkt] = o.n;
     ws.claims[pkt] = claims | (fail ? 0x80000000u : 0u);
 }
