@@ -368,8 +368,13 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
                 src_fill(in, true);
             }
             sink1_flush(o);
-#ifndef DEC6_NO_DRAIN
-            __builtin_amdgcn_s_waitcnt(0);            // (the blind stores of this lane's records)
+            // (no drain before the record loads: a lane's loads of its records come
+            // after its stores to them in program order, which the memory pipeline
+            // keeps -- as for any store and later load of one address by one thread,
+            // between which the compiler puts no wait either; vmcnt retires the
+            // loads behind those stores in any case.  -DDEC6_DRAIN: s_waitcnt(0) here)
+#ifdef DEC6_DRAIN
+            __builtin_amdgcn_s_waitcnt(0);
 #endif
             const uint32_t st = rs && order >= 1 ? stats[p] : 0u;
             const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
