@@ -83,7 +83,8 @@ typedef struct {
 } rc_workspace_dev;
 
 #define RC_SMALL_AUTO 0xFFFFFFFFu
-#define RC_DEC6_TAB_BYTES 12416u  /* per lane: 256 buckets x (a 16-B and a 32-B record), a dummy slot */
+#define RC_DEC6_TAB_BYTES 16512u  /* per lane: 256 buckets x (a 16-B and a 48-B record), 128 B of dummy slots
+                                     (the 16-B records of all lanes first, then the rest: rc_dec6_rare.h) */
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */
 #define RC_KERNEL_WAVE 1u   /* one packet per wavefront */

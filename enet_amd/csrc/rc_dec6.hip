@@ -22,7 +22,7 @@
 //
 // Every element also goes, with a blind 2-B store (no read), into the lane's
 // bucket records: a 16-B record per bucket for its first 8 order-1 elements
-// (4 KB per lane, 268 MB for 65536 lanes), a 32-B one for the next 16, touched
+// (4 KB per lane, 268 MB for 65536 lanes), a 48-B one for the next 20, touched
 // only by buckets that grow that big.  A random partial write costs about
 // what its footprint costs in the 256-MB Infinity Cache
 // (tools/mb/membench6.hip: 0.77 us per step over 268 MB, 2.2 us over 1 GB).  A step that
@@ -47,7 +47,7 @@
 // lists those that differ for the lane kernels, which decode them again.
 //
 // Off the fast path (listed for the lane kernels from the start): a bucket
-// with more than 24 order-1 visits or more than 7 order-1 hits (no rescale is
+// with more than 28 order-1 visits or more than 7 order-1 hits (no rescale is
 // possible below that, compress.c:313), more than 4 order-2 hits, the model
 // reset (4094 nodes, compress.c:148-157), root codes past symbol 255 (the
 // exact path), an output that does not fit, or -- once a quarter of the
@@ -84,7 +84,7 @@ constexpr uint32_t kRareIters6 = DEC6_RARE_ITERS;   // rare steps per phase and 
 constexpr uint32_t kWaveBail6 = 16;
 constexpr uint32_t kStats6 = kRootStrideDec;     // the LDS bucket bytes follow the root
 constexpr uint32_t kLds6 = kRootStrideDec + 256; // 528 B per lane (33 x 16 B: b128 conflict-free)
-constexpr uint32_t kDummy6 = 12288;              // the slot of the stores that record nothing
+constexpr uint32_t kDummy6 = 256 * kTab2Rec;    // in the second table's block: the slot of the stores that record nothing
 
 DEV void bail6(const rc_workspace_dev& ws, uint32_t pkt) { bail(ws, pkt); }
 
@@ -188,7 +188,7 @@ DEV void sink1_finish(ByteSink1& o)
 // rc_decompress_dec6s).
 template <class Src>
 DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* root,
-                         uint8_t* stats, uint8_t* tab, const uint8_t* itab, Src& in)
+                         uint8_t* stats, uint8_t* tab, uint8_t* tab2, const uint8_t* itab, Src& in)
 {
     constexpr bool kSlot = std::is_same<Src, SlotSrc>::value;
     const uint32_t len = bt.in_len[pkt];
@@ -319,8 +319,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (o1v) stats[p] = static_cast<uint8_t>(st + 1);
             const bool full = o1v && t1 >= kTabCap;
             // the element into the bucket's records (a blind 2-B store; no read)
-            *GPTR(uint16_t, reinterpret_cast<uintptr_t>(tab) +
-                            (!(o1v && !full) ? kDummy6 : (t1 < 8 ? 16 * p + 2 * t1 : kTab2 + 32 * p + 2 * (t1 - 8)))) =
+            *GPTR(uint16_t, !(o1v && !full) ? reinterpret_cast<uintptr_t>(tab2) + kDummy6 : rec_addr(tab, tab2, p, t1)) =
                 static_cast<uint16_t>(a | (v << 8));
             x0 = (sym && order == 0) ? v : x0;
             const bool fl = sym && o.n >= o.cap;                           // compress.c:617
@@ -379,7 +378,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const uint32_t st = rs && order >= 1 ? stats[p] : 0u;
             const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
             Hist6 H;
-            rec_build(tab, p, rs ? t1 : 0u, hl, nh, x0, o.n - seg0, rs, H);
+            rec_build(tab, tab2, p, rs ? t1 : 0u, hl, nh, x0, o.n - seg0, rs, H);
             const bool over = false;
             PROF(1)
 #ifdef RC_PROFILE
@@ -451,7 +450,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (o1v) stats[p] = static_cast<uint8_t>(nst);
             const bool tfull = o1v && t1 >= kTabCap;
             if (o1v && !tfull)
-                *GPTR(uint16_t, reinterpret_cast<uintptr_t>(tab) + (t1 < 8 ? 16 * p + 2 * t1 : kTab2 + 32 * p + 2 * (t1 - 8))) =
+                *GPTR(uint16_t, rec_addr(tab, tab2, p, t1)) =
                     static_cast<uint16_t>(a | (v << 8));
             claims += (sym && order >= 1 && nb && o.n < o.cap) ? 1u : 0u;
             const bool h2 = sym && at == 2;
@@ -533,13 +532,15 @@ void rc_decompress_dec6(rc_batch_dev b, rc_workspace_dev ws)
     __syncthreads();
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
-    uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * RC_DEC6_TAB_BYTES;
+    uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * kTab1;
+    uint8_t* tab2 = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(ws.lane_slots) * kTab1 +
+                    static_cast<size_t>(slot) * kTab2;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
     if (l >= act) return;
     ByteSrc in;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
         const uint32_t pkt = order ? order[i] : i;
-        decompress_one6(b, ws, pkt, root, stats, tab, itab, in);
+        decompress_one6(b, ws, pkt, root, stats, tab, tab2, itab, in);
     }
 }
 
@@ -576,13 +577,15 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
         }
         return;
     }
-    uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * RC_DEC6_TAB_BYTES;
+    uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * kTab1;
+    uint8_t* tab2 = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(ws.lane_slots) * kTab1 +
+                    static_cast<size_t>(slot) * kTab2;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
     SlotSrc in;
     in.gen = 0; in.mctl = mctl; in.hctl = hctl; in.slot = slotp;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * kLanes6s) {
         const uint32_t pkt = order ? order[i] : i;
-        decompress_one6(b, ws, pkt, root, stats, tab, itab, in);
+        decompress_one6(b, ws, pkt, root, stats, tab, tab2, itab, in);
     }
     mctl[1] = kFinS;
 }

@@ -7,8 +7,14 @@
 
 namespace {
 
-constexpr uint32_t kTab2 = 4096;                 // the second table: 32-B records (elements 8..23)
-constexpr uint32_t kTabCap = 24;                 // order-1 elements a bucket's records hold
+// A lane's records: its first table (16-B records, 4 KB) in a dense array of
+// first tables, its second table (48-B records) and dummy slots apart, so
+// that the first tables every bucket touches stay one contiguous 268 MB
+// (65536 lanes) and the second tables only buckets past 8 elements touch.
+constexpr uint32_t kTab1 = 256 * 16;
+constexpr uint32_t kTab2Rec = 48;
+constexpr uint32_t kTab2 = 256 * kTab2Rec + 128;  // per lane: the second table and 128 B of dummy slots
+constexpr uint32_t kTabCap = 28;                 // order-1 elements a bucket's records hold (+ 4 order-2 hits: 32)
 
 // a bucket rebuilt from the history: elements in position order
 struct Hist6 { uint32_t A[8], V[8]; uint32_t p1, hit, k; };
@@ -39,25 +45,31 @@ DEV uint32_t eqmask6(const uint32_t* X, uint32_t u, uint32_t nd)
     return m;
 }
 
-DEV void rec_load(const uint8_t* tab, uint32_t p, uint32_t t1, bool en, uint4& r1, uint4& r2, uint4& r3)
+// the record slot of a bucket's element t (t < kTabCap)
+DEV uintptr_t rec_addr(const uint8_t* tab, const uint8_t* tab2, uint32_t p, uint32_t t)
 {
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-    r1 = z; r2 = z; r3 = z;
-#ifndef DEC6_UNCOND_LOADS
-    if (en) r1 = hload16(reinterpret_cast<uintptr_t>(tab) + 16 * p);
-    if (en && t1 > 8) {
-        r2 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p);
-        r3 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p + 16);
-    }
-#else
-    r1 = hload16(reinterpret_cast<uintptr_t>(tab) + 16 * p);
-    r2 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p);
-    r3 = hload16(reinterpret_cast<uintptr_t>(tab) + kTab2 + 32 * p + 16);
-#endif
+    return t < 8 ? reinterpret_cast<uintptr_t>(tab) + 16 * p + 2 * t
+                 : reinterpret_cast<uintptr_t>(tab2) + kTab2Rec * p + 2 * (t - 8);
 }
 
-DEV void rec_fill(const uint4& r1, const uint4& r2, const uint4& r3, uint32_t p, uint32_t t1, const uint32_t* hl,
-                  uint32_t nh, uint32_t x0, uint32_t n, Hist6& H)
+DEV void rec_load(const uint8_t* tab, const uint8_t* tab2, uint32_t p, uint32_t t1, bool en, uint4& r1, uint4& r2,
+                  uint4& r3, uint4& r4)
+{
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    r1 = z; r2 = z; r3 = z; r4 = z;
+    const uintptr_t b2 = reinterpret_cast<uintptr_t>(tab2) + kTab2Rec * p;
+    if (en) r1 = hload16(reinterpret_cast<uintptr_t>(tab) + 16 * p);
+    if (en && t1 > 8) {
+        r2 = hload16(b2);
+        r3 = hload16(b2 + 16);
+    }
+    if (rare_lane(en && t1 > 24)) {
+        if (en && t1 > 24) r4 = hload16(b2 + 32);
+    }
+}
+
+DEV void rec_fill(const uint4& r1, const uint4& r2, const uint4& r3, const uint4& r4, uint32_t p, uint32_t t1,
+                  const uint32_t* hl, uint32_t nh, uint32_t x0, uint32_t n, Hist6& H)
 {
     H.A[0] = bperm(r1.y, r1.x, 0x06040200u); H.V[0] = bperm(r1.y, r1.x, 0x07050301u);
     H.A[1] = bperm(r1.w, r1.z, 0x06040200u); H.V[1] = bperm(r1.w, r1.z, 0x07050301u);
@@ -65,7 +77,8 @@ DEV void rec_fill(const uint4& r1, const uint4& r2, const uint4& r3, uint32_t p,
     H.A[3] = bperm(r2.w, r2.z, 0x06040200u); H.V[3] = bperm(r2.w, r2.z, 0x07050301u);
     H.A[4] = bperm(r3.y, r3.x, 0x06040200u); H.V[4] = bperm(r3.y, r3.x, 0x07050301u);
     H.A[5] = bperm(r3.w, r3.z, 0x06040200u); H.V[5] = bperm(r3.w, r3.z, 0x07050301u);
-    H.A[6] = 0u; H.V[6] = 0u; H.A[7] = 0u; H.V[7] = 0u;
+    H.A[6] = bperm(r4.y, r4.x, 0x06040200u); H.V[6] = bperm(r4.y, r4.x, 0x07050301u);
+    H.A[7] = 0u; H.V[7] = 0u;
     H.p1 = (p == x0 && t1 > 0 && n >= 2) ? 1u : 0u;
     H.hit = 0u;
     uint32_t k = t1;
@@ -86,17 +99,18 @@ DEV void rec_fill(const uint4& r1, const uint4& r2, const uint4& r3, uint32_t p,
     H.k = k;
 }
 
-// The elements of bucket p from the lane's two tables of 16-B records (the
-// bucket's first 8 and next 8 order-1 elements, appended blind, a | v << 8)
+// The elements of bucket p from the lane's two tables of records (the
+// bucket's first 8 order-1 elements in a 16-B record, the next 20 in a 48-B
+// one, appended blind, a | v << 8)
 // and its order-2 hits from the hit list hl[nh] (p | a << 8 | v << 16).
 // Record bytes past t1 are stale (earlier packets): only t1 are taken.
 // Position 1 (no order-2 context) is element 0 of bucket x0.
-DEV void rec_build(const uint8_t* tab, uint32_t p, uint32_t t1, const uint32_t* hl, uint32_t nh, uint32_t x0,
-                   uint32_t n, bool en, Hist6& H)
+DEV void rec_build(const uint8_t* tab, const uint8_t* tab2, uint32_t p, uint32_t t1, const uint32_t* hl, uint32_t nh,
+                   uint32_t x0, uint32_t n, bool en, Hist6& H)
 {
-    uint4 r1, r2, r3;
-    rec_load(tab, p, t1, en, r1, r2, r3);
-    rec_fill(r1, r2, r3, p, t1, hl, nh, x0, n, H);
+    uint4 r1, r2, r3, r4;
+    rec_load(tab, tab2, p, t1, en, r1, r2, r3, r4);
+    rec_fill(r1, r2, r3, r4, p, t1, hl, nh, x0, n, H);
 }
 
 // The values of a bucket's elements as bit planes: bit j of pl[b] is bit b of

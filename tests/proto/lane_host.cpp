@@ -134,14 +134,14 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     if (decompress) {
 #ifndef DEC6S
         ByteSrc src6;
-        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, itab6(), src6);
+        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, g_tab6 + kTab1, itab6(), src6);
 #else
         g_b6s = &b;
         g_ctl6s[0] = 0u; g_ctl6s[1] = kNoPktS; g_ctl6s[2] = 0u;
         slot_help_init(g_sh6);
         SlotSrc src6;
         src6.gen = 0; src6.mctl = g_ctl6s; src6.hctl = g_ctl6s + 2; src6.slot = g_lds6 + 256;
-        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, itab6(), src6);
+        decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, g_tab6 + kTab1, itab6(), src6);
         g_b6s = nullptr;
 #endif
         if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len, resets[0])) {

@@ -133,6 +133,27 @@ def test_dec6_model_reset(lane):
     assert valid_left == 0, valid_left
 
 
+def test_dec6_bucket_capacity(lane):
+    """A bucket of 25-28 order-1 elements fills the record-light decoder's
+    second record (elements 8-27, rc_dec6_rare.h kTabCap): the decoder keeps
+    the packet; past 28 it leaves it to the lane kernels.  Against the oracle."""
+    if lane.version not in ("v6", "v6s"):
+        pytest.skip("dec6 only")
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(31)
+    for k in (20, 25, 27, 28, 29, 31):
+        x = rng.integers(8, 256, size=1200, dtype=np.uint8)
+        at = rng.choice(np.arange(2, 1199), size=k, replace=False)
+        x[at] = 7                                  # bucket 7: the k bytes after them
+        p = x.tobytes()
+        r, c = port.compress(p, 2 * len(p) + 64)
+        lane.left = 0
+        assert lane(1, c, len(p)) == port.decompress(c, len(p)), k
+        if k <= 27:                                # (an adjacent pair of 7s can add an element)
+            assert lane.left == 0, k
+
+
 def test_lane_logic_region_overflow_routes_exact(lane):
     # a tiny region (max_len hint 16) cannot hold a 1200-byte random packet's model
     # (v3 keeps single-symbol order-2 contexts inline, so it needs a small
