@@ -140,7 +140,10 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
  * ENC2_WIDE_MAX bytes, ENET_RC_ENC2_WIDE_MB=m caps it lower: packets past it
  * take the lane kernels; ENET_RC_ENC2_WIDE=0 turns the mode off).  Reserved
  * only for batches that take the lane path (run_device). */
-#define ENC2_STREAM_MAX (1ull << 30)
+/* (3 GB: a chip's worth of 4096-B packets, 65536 x 32.9 KB, in one chunk --
+ * a chunk smaller than that leaves the code pass's lanes partly idle for a
+ * whole packet's time) */
+#define ENC2_STREAM_MAX (3ull << 30)
 #define ENC2_WIDE_MAX (3ull << 30)
 
 static uint64_t env_mb_cap(const char *name, uint64_t cap)
