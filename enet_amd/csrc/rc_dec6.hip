@@ -253,7 +253,8 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
 #ifdef DEC6_STATS_PREFETCH
             const uint32_t st = (go && order >= 1) ? stn : 0u;
 #else
-            const uint32_t st = (go && order >= 1) ? stats[p] : 0u;
+            const uint32_t sraw = stats[p];                    // (read on every path: no exec mask)
+            const uint32_t st = (go && order >= 1) ? sraw : 0u;
 #endif
             const uint32_t t1 = st & 31u, d1 = t1 - (st >> 5);
             bool need = go && order >= 2 && repeat && !o2s;

@@ -33,8 +33,8 @@ static void slot_host_kick();     // tests/proto/lane_host.cpp: one helper pass
 
 struct SlotSrc {
     uint64_t la;                  // lookahead: the next na bytes, first in bits 63..56
-    uint32_t na, q, j, lo15;      // bytes in la; next dword of c; c is chunk j; packet start & 15
-    uint4 c;
+    uint32_t na, q, j, lo15;      // bytes in la; dwords of c taken; c is chunk j; packet start & 15
+    uint4 c;                      // (shifted as taken: c.x is dword q of chunk j)
     uint32_t want, gen;
     uint32_t* mctl;               // [0] m_ctl, [1] m_pkt
     const uint32_t* hctl;
@@ -43,15 +43,21 @@ struct SlotSrc {
 
 DEV void slot_publish(const SlotSrc& s) { s.mctl[0] = ((s.want & 0xFFFu) << 16) | (s.gen << 28); }
 
+DEV void slot_shift(SlotSrc& s, bool en)
+{
+    s.c.x = en ? s.c.y : s.c.x; s.c.y = en ? s.c.z : s.c.y; s.c.z = en ? s.c.w : s.c.z;
+}
+
 // one dword into the lookahead where it has room for it and c has one
 DEV void slot_fill(SlotSrc& s, bool en)
 {
     const bool need = en && s.na <= 4 && s.q < 4;
-    const uint32_t d = bswap(sel4(s.q, s.c));
+    const uint32_t d = bswap(s.c.x);
     const uint32_t sh = need ? 32 - 8 * s.na : 0u;
     s.la |= need ? (static_cast<uint64_t>(d) << sh) : 0ull;
     s.na += need ? 4u : 0u;
     s.q += need ? 1u : 0u;
+    slot_shift(s, need);
 }
 
 // c used up: the slot's chunk if it is chunk j + 1 (hc: h_ctl as read, sl: the slot)
@@ -161,9 +167,12 @@ DEV uint32_t slot_init(SlotSrc& s, const uint8_t* p, uint32_t len, uint32_t pkt)
     s.q = s.lo15 >> 2;
     s.c = c0;
     s.j = 0;
-    s.la = static_cast<uint64_t>(bswap(sel4(s.q, s.c)) << (8 * sk)) << 32;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) slot_shift(s, k < s.q);
+    s.la = static_cast<uint64_t>(bswap(s.c.x) << (8 * sk)) << 32;
     s.na = 4 - sk;
     s.q += 1;
+    slot_shift(s, true);
     slot_adv0(s, c1);
     slot_fill(s, true);
     const uint32_t code = static_cast<uint32_t>(s.la >> 32);
