@@ -317,7 +317,11 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             // by the assumption above, to order 1; nodes as compress.c creates them
             nodes += sym ? (cnt0 == 0 ? 1u : 0u) + (order >= 1 ? 1u : 0u) + (order >= 2 ? 1u : 0u) : 0u;
             const bool o1v = sym && order >= 1;
+#ifndef DEC6_STATS_PREFETCH
+            stats[p] = static_cast<uint8_t>(o1v ? st + 1 : sraw);   // (written on every path: no exec mask)
+#else
             if (o1v) stats[p] = static_cast<uint8_t>(st + 1);
+#endif
             const bool full = o1v && t1 >= kTabCap;
             // the element into the bucket's records (a blind 2-B store; no read)
             *GPTR(uint16_t, !(o1v && !full) ? reinterpret_cast<uintptr_t>(tab2) + kDummy6 : rec_addr(tab, tab2, p, t1)) =
