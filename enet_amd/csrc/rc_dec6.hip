@@ -597,24 +597,117 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
 
 // Counts the distinct bigrams of each packet rc_decompress_dec6 decoded and
 // lists the packets whose count differs from the decoder's (see the header).
-// A wavefront per packet: a 65536-bit set in LDS; each lane takes an aligned
-// 16-B chunk of the output per round (and the byte before it), sets the bits
-// of its positions' bigrams, and the set's population is the count.
+// A wavefront per packet: a 65536-bit set in LDS, cleared per packet; a lane
+// sets the bits of its positions' bigrams with LDS atomics and counts the
+// bits it found clear.  The common packet (one model segment, at most
+// 64 x kVerDw dwords) is software-pipelined two deep: its output dwords were
+// loaded -- lane l round r: dword 64 r + l -- while the wave counted the
+// packet before, and the header of the one after is in flight (vector loads
+// only, so that waiting for an atomic's return never waits for them).  Other
+// packets take verify_slow.
 constexpr uint32_t kVerifyWaves = 4;
-extern "C" __global__ __launch_bounds__(256) void rc_dec6_verify(rc_batch_dev b, rc_workspace_dev ws)
+constexpr uint32_t kVerifyBlocksPerCu = 5;      // 32 KB of LDS per workgroup
+constexpr uint32_t kVerDw = 8;                  // dwords per lane: packets to 2 KB - 4
+
+// the header words of packet k, lane l < 5: claims, out_len, out_off (2), resets
+DEV uint32_t vhead_load(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, uint32_t l)
 {
-    __shared__ uint4 bits[kVerifyWaves][512];
-    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-    uint4* set4 = bits[wave];
+    const uint32_t* src = l == 0 ? ws.claims + k
+                        : l == 1 ? b.out_len + k
+                        : l < 4 ? reinterpret_cast<const uint32_t*>(b.out_off + k) + (l - 2)
+                                : ws.dec6_resets + k;
+    return (k < b.n && l < 5) ? *src : 0u;
+}
+
+struct VHead {
+    uint32_t cl, n, rst, off, nd;   // off: lo - sb; nd: dwords from sb
+    uintptr_t lo, sb;
+    bool skip, fast;
+};
+
+DEV VHead vhead_get(const rc_batch_dev& b, uint32_t k, uint32_t hv)
+{
+    VHead h;
+    h.cl = __shfl(hv, 0);
+    h.n = __shfl(hv, 1);
+    const uint64_t oo = static_cast<uint64_t>(static_cast<uint32_t>(__shfl(hv, 2))) |
+                        static_cast<uint64_t>(static_cast<uint32_t>(__shfl(hv, 3))) << 32;
+    h.rst = __shfl(hv, 4);
+    h.skip = k >= b.n || h.cl == 0xFFFFFFFFu;                    // none, or left to the lanes already
+    h.lo = reinterpret_cast<uintptr_t>(b.out) + oo;
+    h.sb = h.lo & ~static_cast<uintptr_t>(3);
+    h.off = static_cast<uint32_t>(h.lo - h.sb);
+    h.nd = (h.off + h.n + 3) >> 2;
+    h.fast = !h.skip && (h.rst >> 24) == 0 && h.nd <= 64 * kVerDw;
+    return h;
+}
+
+DEV void vdata_load(const VHead& h, uint32_t l, uint32_t (&w)[kVerDw])
+{
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(h.sb);
+#pragma unroll
+    for (uint32_t r = 0; r < kVerDw; ++r) {
+        const uint32_t c = 64 * r + l;
+        w[r] = (h.fast && c < h.nd) ? p[c] : 0u;
+    }
+}
+
+DEV void vresult(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, uint32_t cl, uint32_t cnt, uint32_t l)
+{
+    for (int sft = 32; sft >= 1; sft >>= 1) cnt += static_cast<uint32_t>(__shfl_xor(static_cast<int>(cnt), sft));
+    const uint32_t want = cl & 0x7FFFFFFFu;
+    if (l == 0 && (cnt != want || (ws.dec6_debug & 1))) {
+        const uint32_t i = atomicAdd(&ws.counters[3], 1u);
+        ws.enc2_list[i] = k;
+    }
+    if (l == 0 && cnt == want && !(ws.dec6_debug & 1) && (cl >> 31)) b.out_len[k] = 0;     // compress.c:617
+}
+
+DEV void vclear(uint4* set4, uint32_t l)
+{
+#pragma unroll
+    for (uint32_t i = 0; i < 512 / 64; ++i) set4[i * 64 + l] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// the common packet: its dwords in w
+DEV void verify_fast(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, const VHead& h,
+                     const uint32_t (&w)[kVerDw], uint4* set4, uint32_t l)
+{
     uint32_t* set = reinterpret_cast<uint32_t*>(set4);
-    for (uint32_t pkt = blockIdx.x * kVerifyWaves + wave; pkt < b.n; pkt += gridDim.x * kVerifyWaves) {
+    vclear(set4, l);
+    uint32_t cnt = 0, last = 0;                  // last: lane 63's dword of the round before
+#pragma unroll
+    for (uint32_t r = 0; r < kVerDw; ++r) {
+        if (64 * r >= h.nd) break;
+        const uint32_t up = static_cast<uint32_t>(__shfl_up(static_cast<int>(w[r]), 1));
+        const uint32_t pw = l ? up : last;       // the dword before this lane's
+        last = static_cast<uint32_t>(__shfl(static_cast<int>(w[r]), 63));
+        const uint32_t c = 64 * r + l;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            const uint32_t x = (w[r] >> (8 * t)) & 0xFFu;
+            const uint32_t pv = t ? (w[r] >> (8 * t - 8)) & 0xFFu : pw >> 24;
+            const uint32_t pos = 4 * c + t - h.off;          // position in the packet (wraps below 0)
+            const bool in = pos >= 1 && pos < h.n;
+            // (no branch: a position outside ORs nothing into a word of the lane's own,
+            // so the four atomics issue back to back and their returns are awaited once)
+            const uint32_t bg = (pv << 8) | x, bit = 1u << (bg & 31);
+            const uint32_t old = atomicOr(&set[in ? bg >> 5 : l], in ? bit : 0u);
+            cnt += (in && !(old & bit)) ? 1u : 0u;
+        }
+    }
+    vresult(b, ws, k, h.cl, cnt, l);
+}
+
+// any other packet: per model segment (compress.c:148-157: bigrams are counted
+// within each, the pair across a reset belongs to neither), loads as it goes
+DEV void verify_slow(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t pkt, uint4* set4, uint32_t l)
+{
+    uint32_t* set = reinterpret_cast<uint32_t*>(set4);
+    {
         const uint32_t cl = ws.claims[pkt];
-        if (cl == 0xFFFFFFFFu) continue;                          // left to the lanes already
-        const uint32_t want = cl & 0x7FFFFFFFu;
         const uint32_t n = b.out_len[pkt];
         const uintptr_t lo = reinterpret_cast<uintptr_t>(b.out + b.out_off[pkt]);
-        // the model segments (compress.c:148-157): bigrams are counted within each,
-        // the pair across a reset belongs to neither
         const uint32_t rst = ws.dec6_resets[pkt], nseg = (rst >> 24) + 1;
         uint32_t cnt = 0;
         for (uint32_t sg = 0; sg < nseg; ++sg) {
@@ -654,13 +747,48 @@ extern "C" __global__ __launch_bounds__(256) void rc_dec6_verify(rc_batch_dev b,
             cnt += sc;
             __builtin_amdgcn_wave_barrier();
         }
-        for (int sft = 32; sft >= 1; sft >>= 1) cnt += static_cast<uint32_t>(__shfl_xor(static_cast<int>(cnt), sft));
-        if (l == 0 && (cnt != want || (ws.dec6_debug & 1))) {
-            const uint32_t k = atomicAdd(&ws.counters[3], 1u);
-            ws.enc2_list[k] = pkt;
-        }
-        if (l == 0 && cnt == want && !(ws.dec6_debug & 1) && (cl >> 31)) b.out_len[pkt] = 0;     // compress.c:617
-        __builtin_amdgcn_wave_barrier();
+        vresult(b, ws, pkt, cl, cnt, l);
+    }
+}
+
+DEV void verify_one(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, const VHead& h,
+                    const uint32_t (&w)[kVerDw], uint4* set4, uint32_t l)
+{
+    if (h.skip) return;
+    if (h.fast) verify_fast(b, ws, k, h, w, set4, l);
+    else verify_slow(b, ws, k, set4, l);
+    __builtin_amdgcn_wave_barrier();
+}
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
+void rc_dec6_verify(rc_batch_dev b, rc_workspace_dev ws)
+{
+    __shared__ uint4 bits[kVerifyWaves][512];
+    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
+    uint4* set4 = bits[wave];
+    const uint32_t stride = gridDim.x * kVerifyWaves;
+    uint32_t k = blockIdx.x * kVerifyWaves + wave;
+    if (k >= b.n) return;
+    // two register sets, A and B: a packet's dwords load while the other's count
+    uint32_t wa[kVerDw], wb[kVerDw];
+    uint32_t hva = vhead_load(b, ws, k, l);
+    VHead ha = vhead_get(b, k, hva), hb;
+    vdata_load(ha, l, wa);
+    uint32_t hvb = vhead_load(b, ws, k + stride, l);
+    for (;;) {
+        // A holds packet k; B's header (packet k + stride) is in flight
+        hb = vhead_get(b, k + stride, hvb);
+        vdata_load(hb, l, wb);
+        hva = vhead_load(b, ws, k + 2 * stride, l);
+        verify_one(b, ws, k, ha, wa, set4, l);
+        k += stride;
+        if (k >= b.n) break;
+        ha = vhead_get(b, k + stride, hva);
+        vdata_load(ha, l, wa);
+        hvb = vhead_load(b, ws, k + 2 * stride, l);
+        verify_one(b, ws, k, hb, wb, set4, l);
+        k += stride;
+        if (k >= b.n) break;
     }
 }
 
@@ -671,7 +799,10 @@ extern "C" int rc_hip_dec6_verify_launch(const rc_batch_dev* b, const rc_workspa
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint32_t vb = (b->n + kVerifyWaves - 1) / kVerifyWaves;
-    hipLaunchKernelGGL(rc_dec6_verify, dim3(vb < 4096 ? vb : 4096), dim3(256), 0, st, *b, *ws);
+    // resident workgroups only: each wave then walks several packets, the
+    // next one's loads in flight
+    const uint32_t cap = (ws->cus ? ws->cus : 256u) * kVerifyBlocksPerCu;
+    hipLaunchKernelGGL(rc_dec6_verify, dim3(vb < cap ? vb : cap), dim3(256), 0, st, *b, *ws);
     return static_cast<int>(hipGetLastError());
 }
 
