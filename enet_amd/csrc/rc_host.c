@@ -216,8 +216,9 @@ void *enet_range_coder_create(void)
     memset(c, 0, sizeof *c);
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) goto fail;
-    if (hipMalloc((void **) &c->ws.counters, 32) != hipSuccess) goto fail;
-    if (hipMalloc((void **) &c->ws.bins, (RC_LEN_BINS + 1) * sizeof(uint32_t)) != hipSuccess) goto fail;
+    /* counters[8] and the length bins in one block: one fill clears both per call */
+    if (hipMalloc((void **) &c->ws.counters, RC_CTL_WORDS * sizeof(uint32_t)) != hipSuccess) goto fail;
+    c->ws.bins = c->ws.counters + 8;
     c->ws.exact_slots = EXACT_SLOTS;
     if (hipMalloc(&c->ws.exact_pool, (size_t) EXACT_SLOTS * RC_EXACT_POOL_BYTES) != hipSuccess) goto fail;
     if (ws_reserve(c, 1024) != 0) goto fail;
@@ -292,7 +293,6 @@ void enet_range_coder_destroy(void *context)
     if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
     if (c->ws.enc2_wlist) hipFree(c->ws.enc2_wlist);
     if (c->ws.enc2_wide) hipFree(c->ws.enc2_wide);
-    if (c->ws.bins) hipFree(c->ws.bins);
     if (c->ws.exact_pool) hipFree(c->ws.exact_pool);
     if (c->ws.lane_pool) hipFree(c->ws.lane_pool);
     if (c->crc_tables) hipFree(c->crc_tables);

@@ -1143,7 +1143,8 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (b->n == 0) return 0;
     if (b->n > ws->n_cap) return static_cast<int>(hipErrorInvalidValue);
-    hipError_t err = hipMemsetAsync(ws->counters, 0, 8 * sizeof(uint32_t), st);
+    // the counters and the length bins (one block, rc_host.c): one fill
+    hipError_t err = hipMemsetAsync(ws->counters, 0, RC_CTL_WORDS * sizeof(uint32_t), st);
     if (err != hipSuccess) return static_cast<int>(err);
     const uint32_t max_len = b->max_len ? b->max_len : 4096;
     uint32_t lds_w;

@@ -43,9 +43,14 @@ __device__ __forceinline__ uint32_t bin_rank(uint32_t* hist, uint32_t bin, bool 
     return rank;
 }
 
-extern "C" __global__ __launch_bounds__(256) void rc_len_hist(const uint32_t* len, uint32_t n, uint32_t* bins)
+// The histogram, then -- in the workgroup that finishes last (its ticket in
+// bins[RC_LEN_TICKET], cleared with the counters by launch()) -- the exclusive
+// prefix over the bins; bins[RC_LEN_BINS] = 1 when every packet falls in one
+// bin (uniform lengths: the lane kernels then keep batch order).
+extern "C" __global__ __launch_bounds__(RC_LEN_BINS) void rc_len_hist(const uint32_t* len, uint32_t n, uint32_t* bins)
 {
     __shared__ uint32_t h[RC_LEN_BINS];
+    __shared__ uint32_t last;
     h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * kBinChunk;
@@ -55,24 +60,23 @@ extern "C" __global__ __launch_bounds__(256) void rc_len_hist(const uint32_t* le
     }
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
-}
-
-// Exclusive prefix over the bins; bins[RC_LEN_BINS] = 1 when every packet
-// falls in one bin (uniform lengths: the lane kernels then keep batch order).
-extern "C" __global__ __launch_bounds__(RC_LEN_BINS) void rc_len_scan(uint32_t* bins)
-{
-    __shared__ uint32_t s[RC_LEN_BINS];
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&bins[RC_LEN_TICKET], 1u) == gridDim.x - 1 ? 1u : 0u;
+    __syncthreads();
+    if (!last) return;
+    // every workgroup's counts are in: the scan (atomic reads: device-coherent)
     const uint32_t t = threadIdx.x;
-    const uint32_t mine = bins[t];
-    s[t] = mine;
+    const uint32_t mine = atomicAdd(&bins[t], 0u);
+    h[t] = mine;
     const int used = __syncthreads_count(mine != 0);
     for (uint32_t d = 1; d < RC_LEN_BINS; d <<= 1) {
-        const uint32_t x = t >= d ? s[t - d] : 0u;
+        const uint32_t x = t >= d ? h[t - d] : 0u;
         __syncthreads();
-        s[t] += x;
+        h[t] += x;
         __syncthreads();
     }
-    bins[t] = s[t] - mine;               // exclusive prefix = first slot of the bin
+    bins[t] = h[t] - mine;               // exclusive prefix = first slot of the bin
     if (t == 0) bins[RC_LEN_BINS] = used <= 1 ? 1u : 0u;
 }
 
@@ -119,11 +123,9 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
     rc_workspace_dev w = *ws;
     w.order = nullptr;
     if (b->n >= 1024 && ws->order && ws->bins) {        // bin packets by length (ragged batches)
-        hipError_t e = hipMemsetAsync(ws->bins, 0, (RC_LEN_BINS + 1) * sizeof(uint32_t), st);
-        if (e != hipSuccess) return static_cast<int>(e);
+        // (the bins were cleared with the counters by launch(), rc_kernels.hip)
         const uint32_t g = (b->n + kBinChunk - 1) / kBinChunk;
-        hipLaunchKernelGGL(rc_len_hist, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins);
-        hipLaunchKernelGGL(rc_len_scan, dim3(1), dim3(RC_LEN_BINS), 0, st, ws->bins);
+        hipLaunchKernelGGL(rc_len_hist, dim3(g), dim3(RC_LEN_BINS), 0, st, b->in_len, b->n, ws->bins);
         hipLaunchKernelGGL(rc_len_scatter, dim3(g), dim3(256), 0, st, b->in_len, b->n, ws->bins, ws->order);
         w.order = ws->order;
     }
