@@ -387,6 +387,34 @@ def test_corrupted_streams_vs_oracle(coder):
     assert not bad, bad[:10]
 
 
+def test_check_on_unaligned_outputs_vs_oracle(coder):
+    """The decoder's check (rc_dec6_verify) reads each output as aligned dwords
+    from the one holding its first byte: outputs at every offset mod 4 (caps
+    n + 0..3, 5, 7), packets of 1 to 1500 bytes, valid streams (none left to
+    the lane kernels on the default variants) and bit-flipped ones, against
+    the oracle."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(0x5646)
+    pk = [rng.integers(0, 256, size=int(rng.integers(1, 1501)), dtype=np.uint8).tobytes() for _ in range(600)]
+    comp = [port.compress(p, 2 * len(p) + 64)[1] for p in pk]
+    caps = [len(p) + int(rng.choice([0, 1, 2, 3, 5, 7])) for p in pk]
+    back = _run(coder, True, comp, caps)
+    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+        assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
+    assert all(b == (len(p), p) for b, p in zip(back, pk))
+    flipped = []
+    for c in comp[:300]:
+        b = bytearray(c)
+        j = int(rng.integers(len(b) // 4, len(b))) if len(b) > 4 else len(b) - 1
+        b[j] ^= 1 << int(rng.integers(0, 8))
+        flipped.append(bytes(b))
+    res = _run(coder, True, flipped, caps[:300])
+    bad = [i for i, (g, c, r) in enumerate(zip(flipped, caps, res))
+           if (lambda e: r[0] != e[0] or (e[0] and r[1] != e[1]))(port.decompress(g, c))]
+    assert not bad, bad[:10]
+
+
 @pytest.fixture(scope="module")
 def wave_coder():
     """The one-packet-per-wavefront kernels (ENET_RC_KERNEL=wave), kept as an
