@@ -60,7 +60,30 @@ typedef struct {
     size_t d_pack_cap;
     uint64_t *d_bsum;
     size_t d_bsum_cap;
+    /* host batches in two halves (run_host_split): the second context on the
+       device, and the hand-off of the first half's input DMA */
+    void *twin;
+    struct h2d_sync *sync_sig, *sync_wait;
+    int last_split;
 } rc_ctx;
+
+/* The first half records ev on its stream once its input DMA is enqueued
+ * (ready 1; -1: it ended before that), the second half's stream waits for it
+ * before its own. */
+struct h2d_sync {
+    pthread_mutex_t m;
+    pthread_cond_t cv;
+    int ready;
+    hipEvent_t ev;
+};
+
+static void h2d_sync_set(struct h2d_sync *y, int v)
+{
+    pthread_mutex_lock(&y->m);
+    if (!y->ready) y->ready = v;
+    pthread_cond_broadcast(&y->cv);
+    pthread_mutex_unlock(&y->m);
+}
 
 static void *ctx_alloc(size_t n) { return enet_malloc ? enet_malloc(n) : malloc(n); }
 static void ctx_release(void *p) { if (enet_free) enet_free(p); else free(p); }
@@ -303,6 +326,7 @@ void enet_range_coder_destroy(void *context)
     if (c->d_stage) hipFree(c->d_stage);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
+    if (c->twin) enet_range_coder_destroy(c->twin);
     ctx_release(c);
 }
 
@@ -312,6 +336,7 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
                       void *stream)
 {
     if (!c) return (int) hipErrorInvalidValue;
+    c->last_split = 0;
     if (n == 0) return 0;
     if (n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
@@ -743,6 +768,14 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     memcpy(h + a_ilen, in_len, n * 4);
     memcpy(h + a_ooff, out_off, n * 8);
     memcpy(h + a_ocap, out_cap, n * 4);
+    if (c->sync_wait) {             /* the second half: its DMA after the first half's */
+        struct h2d_sync *y = c->sync_wait;
+        pthread_mutex_lock(&y->m);
+        while (!y->ready) pthread_cond_wait(&y->cv, &y->m);
+        const int r = y->ready;
+        pthread_mutex_unlock(&y->m);
+        if (r > 0) (void) hipStreamWaitEvent(c->stream, y->ev, 0);
+    }
     hipError_t err = hipMemcpyAsync(d + a_ioff, h + a_ioff, a_olen - a_ioff, hipMemcpyHostToDevice, c->stream);
     if (err != hipSuccess) { host_unpin(in + zc_lo, zc_pin); return (int) err; }
     /* the payload: straight from the caller's memory when it is one range and
@@ -781,6 +814,9 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         else par_scatter(h + a_in, hio, in, in_off, in_len, lo, hi, b1 - b0);
         if (b1 > b0) err = hipMemcpyAsync(d + a_in + b0, h + a_in + b0, b1 - b0, hipMemcpyHostToDevice, c->stream);
         if (err != hipSuccess) return (int) err;
+    }
+    if (c->sync_sig) {              /* the first half: its input DMA is enqueued */
+        h2d_sync_set(c->sync_sig, hipEventRecord(c->sync_sig->ev, c->stream) == hipSuccess ? 1 : -1);
     }
     if (prof) { tp[1] = now_ms(); hipStreamSynchronize(c->stream); tp[2] = now_ms(); }
     int rc = run_device(c, decompress, d + a_in, (const uint64_t *) (d + a_ioff),
@@ -915,18 +951,111 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     return err == hipSuccess ? 0 : (int) err;
 }
 
+/* ---- a large host batch in two halves, on this context and a second one
+ * on the same device (its own stream and workspace): the second half's input
+ * DMA follows the first half's, so its kernels overlap the first half's on
+ * the other CUs, and the first half's results cross PCIe while the second
+ * half computes.  The lane kernels take as long for half a batch as for the
+ * whole (a packet per lane), so the halves run side by side,
+ * never one after the other.  The caller's input and output ranges are
+ * page-locked once here for both halves (adjacent halves share boundary
+ * pages: see host_pin).  ENET_RC_HOST_SPLIT=0: off. */
+typedef struct {
+    rc_ctx *c;
+    int decompress;
+    const uint8_t *in; const uint64_t *in_off; const uint32_t *in_len; size_t n;
+    uint8_t *out; const uint64_t *out_off; const uint32_t *out_cap; uint32_t *out_len;
+    int rc;
+} half_job;
+
+static void *half_worker(void *p)
+{
+    half_job *j = (half_job *) p;
+    j->rc = run_host(j->c, j->decompress, j->in, j->in_off, j->in_len, j->n, j->out, j->out_off, j->out_cap,
+                     j->out_len, 1, NULL, NULL);
+    return NULL;
+}
+
+#define SPLIT_MIN_PACKETS 32768u
+#define SPLIT_MIN_BYTES (32ull << 20)
+
+static int run_host_split(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
+                          const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
+                          const uint32_t *out_cap, uint32_t *out_len)
+{
+    static int off = -1;
+    if (off < 0) { const char *e = getenv("ENET_RC_HOST_SPLIT"); off = e && strcmp(e, "0") == 0; }
+    if (!c) return (int) hipErrorInvalidValue;
+    c->last_split = 0;
+    uint64_t bytes = 0, ilo = UINT64_MAX, ihi = 0, olo = UINT64_MAX, ohi = 0;
+    if (!off && n >= SPLIT_MIN_PACKETS && c->ws.kernel != RC_KERNEL_WAVE) {
+        for (size_t i = 0; i < n; ++i) {
+            bytes += in_len[i];
+            if (in_len[i]) {
+                if (in_off[i] < ilo) ilo = in_off[i];
+                if (in_off[i] + in_len[i] > ihi) ihi = in_off[i] + in_len[i];
+            }
+            if (out_off[i] < olo) olo = out_off[i];
+            if (out_off[i] + out_cap[i] > ohi) ohi = out_off[i] + out_cap[i];
+        }
+    }
+    if (off || n < SPLIT_MIN_PACKETS || c->ws.kernel == RC_KERNEL_WAVE || bytes < SPLIT_MIN_BYTES || ihi <= ilo ||
+        ohi <= olo)
+        return run_host(c, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
+    if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
+    if (!c->twin) c->twin = enet_range_coder_create();
+    const int pi = c->twin ? host_pin(in + ilo, ihi - ilo) : 0;
+    const int po = pi ? host_pin(out + olo, ohi - olo) : 0;
+    struct h2d_sync y;
+    int ev_ok = 0;
+    if (po) {
+        pthread_mutex_init(&y.m, NULL);
+        pthread_cond_init(&y.cv, NULL);
+        y.ready = 0;
+        ev_ok = hipEventCreateWithFlags(&y.ev, hipEventDisableTiming) == hipSuccess;
+    }
+    if (!ev_ok) {                   /* (no second context, pinning or event: one piece) */
+        if (po) { pthread_cond_destroy(&y.cv); pthread_mutex_destroy(&y.m); }
+        host_unpin(out + olo, po);
+        host_unpin(in + ilo, pi);
+        return run_host(c, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
+    }
+    rc_ctx *t = (rc_ctx *) c->twin;
+    const size_t m = n / 2;
+    half_job hb = {t, decompress, in, in_off + m, in_len + m, n - m, out, out_off + m, out_cap + m, out_len + m, 0};
+    c->sync_sig = &y;
+    t->sync_wait = &y;
+    pthread_t th;
+    const int threaded = pthread_create(&th, NULL, half_worker, &hb) == 0;
+    if (!threaded) h2d_sync_set(&y, -1);
+    const int ra = run_host(c, decompress, in, in_off, in_len, m, out, out_off, out_cap, out_len, 1, NULL, NULL);
+    h2d_sync_set(&y, -1);           /* (the first half ended before its input DMA: no wait) */
+    if (threaded) pthread_join(th, NULL);
+    else half_worker(&hb);
+    c->sync_sig = NULL;
+    t->sync_wait = NULL;
+    hipEventDestroy(y.ev);
+    pthread_cond_destroy(&y.cv);
+    pthread_mutex_destroy(&y.m);
+    host_unpin(out + olo, po);
+    host_unpin(in + ilo, pi);
+    c->last_split = 1;
+    c->last_exact += t->last_exact;
+    return ra ? ra : hb.rc;
+}
+
 int enet_rc_compress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
                                 const uint32_t *in_len, size_t n, uint8_t *out,
                                 const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return run_host((rc_ctx *) context, 0, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
+    return run_host_split((rc_ctx *) context, 0, in, in_off, in_len, n, out, out_off, out_cap, out_len);
 }
 
 int enet_rc_decompress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
                                   const uint32_t *in_len, size_t n, uint8_t *out,
                                   const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return run_host((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
+    return run_host_split((rc_ctx *) context, 1, in, in_off, in_len, n, out, out_off, out_cap, out_len);
 }
 
 /* compress.c:246-342 over a batch of gather lists: packet i is
@@ -1230,20 +1359,24 @@ uint32_t enet_rc_last_lane_count(void *context)
 {
     rc_ctx *c = (rc_ctx *) context;
     if (!c) return 0;
-    uint32_t v = 0;
+    uint32_t v = 0, w = 0;
     hipDeviceSynchronize();
     if (hipMemcpy(&v, c->ws.counters + 3, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    return v;
+    if (c->last_split && c->twin &&
+        hipMemcpy(&w, ((rc_ctx *) c->twin)->ws.counters + 3, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return v + w;
 }
 
 uint32_t enet_rc_last_exact_count(void *context)
 {
     rc_ctx *c = (rc_ctx *) context;
     if (!c) return 0;
-    uint32_t v = 0;
+    uint32_t v = 0, w = 0;
     hipDeviceSynchronize();
     if (hipMemcpy(&v, c->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    return v;
+    if (c->last_split && c->twin &&
+        hipMemcpy(&w, ((rc_ctx *) c->twin)->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return v + w;
 }
 
 /* ------------------------------------------------------ for rc_multi.c */

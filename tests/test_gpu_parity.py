@@ -486,6 +486,59 @@ def test_host_pointer_batches_large(coder):
     assert np.array_equal(dout[: d.size], d)
 
 
+def test_host_pointer_batches_split(coder):
+    """A host batch of >= 32768 packets and >= 32 MB runs in two halves on two
+    contexts of the device (rc_host.c run_host_split: the second half's input
+    DMA after the first's, the halves' kernels side by side): bit-exact
+    against the oracle both ways, gapped compressed slots, and the hand-off
+    counts of both halves reported together."""
+    import ctypes as C
+    from oracle.pyoracle import compress_batch as ocompress, fnv_digest
+    d, o, l = synth.mixed_batch(50000, seed=17)          # ~36 MB: split
+    assert d.size >= 32 << 20
+    lib = coder.lib
+    n = len(l)
+    ln = l.astype(np.uint32)
+    cap = (2 * ln.astype(np.int64) + 64).astype(np.uint32)
+    coff = np.zeros(n, np.uint64)
+    coff[1:] = np.cumsum(cap[:-1].astype(np.uint64) + 5)
+    cout = np.zeros(int(coff[-1] + cap[-1]) + 16, np.uint8)
+    clen = np.zeros(n, np.uint32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    assert lib.enet_rc_compress_batch_host(coder.ctx, p(d), p(o), p(ln), n, p(cout), p(coff), p(cap), p(clen)) == 0
+    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+        assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
+    want, wo, wcap, wl = ocompress(d, o, l, "port")
+    assert np.array_equal(clen, wl)
+    assert fnv_digest(cout, coff, clen) == fnv_digest(want, wo, wl)
+    dout = np.zeros(int(o[-1]) + int(l[-1]) + 16, np.uint8)
+    dlen = np.zeros(n, np.uint32)
+    assert lib.enet_rc_decompress_batch_host(coder.ctx, p(cout), p(coff), p(clen), n, p(dout), p(o), p(ln),
+                                             p(dlen)) == 0
+    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+        assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
+    assert np.array_equal(dlen, ln)
+    assert np.array_equal(dout[: d.size], d)
+    # game state: the fast decoder hands every packet of both halves on
+    g, go, gl = synth.gamestate_batch(40000, 1200)
+    gn = len(gl)
+    gln = gl.astype(np.uint32)
+    gcap = (2 * gln.astype(np.int64) + 64).astype(np.uint32)
+    gcoff = np.zeros(gn, np.uint64)
+    gcoff[1:] = np.cumsum(gcap[:-1].astype(np.uint64))
+    gout = np.zeros(int(gcoff[-1] + gcap[-1]) + 16, np.uint8)
+    glen = np.zeros(gn, np.uint32)
+    assert lib.enet_rc_compress_batch_host(coder.ctx, p(g), p(go), p(gln), gn, p(gout), p(gcoff), p(gcap),
+                                           p(glen)) == 0
+    gback = np.zeros(g.size + 16, np.uint8)
+    gblen = np.zeros(gn, np.uint32)
+    assert lib.enet_rc_decompress_batch_host(coder.ctx, p(gout), p(gcoff), p(glen), gn, p(gback), p(go), p(gln),
+                                             p(gblen)) == 0
+    assert np.array_equal(gblen, gln) and np.array_equal(gback[: g.size], g)
+    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+        assert coder.last_lane_count() == gn
+
+
 def test_host_pointer_batches_uniform_slots(coder):
     """Host batches whose compressed packets sit in slots at a uniform, odd
     pitch from an odd base (rc_host.c run_host: the strided H2D of max_len
