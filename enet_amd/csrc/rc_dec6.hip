@@ -493,9 +493,14 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             else src_adv(in);
             PROF(3)
         }
-        // (nothing of the rare phase left in flight: a record load pending on some
-        // path would make the common step wait for vmcnt(0) before reusing its registers)
+        // (no wait for the phase's stores here: the rare steps consume their record
+        // loads themselves, so the common steps hold no load the compiler would
+        // wait for, and the next phase's record loads wait behind the stores in
+        // any case (vmcnt retires in order).  -DDEC6_END_WAIT: s_waitcnt(0) here,
+        // 0.3-0.8 % slower, profiles/r4e_dec6_end_wait.txt)
+#ifdef DEC6_END_WAIT
         __builtin_amdgcn_s_waitcnt(0);
+#endif
 #ifdef DEC6_STATS_PREFETCH
         stn = stats[p];
         {
