@@ -76,6 +76,9 @@ namespace {
 #ifndef DEC6_BLOCK
 #define DEC6_BLOCK 16
 #endif
+#ifndef DEC6_HELP_SLEEP
+#define DEC6_HELP_SLEEP 4          // the helper wavefront's pause when no lane wants a chunk (x 64 clocks; 2-16 within 0.5 %)
+#endif
 #ifndef DEC6_RARE_ITERS
 #define DEC6_RARE_ITERS 2
 #endif
@@ -583,7 +586,7 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
             bool fin = false;
             const bool busy = slot_help_iter(b, mctl, hctl, slotp, h, fin);
             if (fin) break;
-            if (!busy) __builtin_amdgcn_s_sleep(2);
+            if (!busy) __builtin_amdgcn_s_sleep(DEC6_HELP_SLEEP);
         }
         return;
     }
