@@ -76,6 +76,9 @@ namespace {
 #ifndef DEC6_BLOCK
 #define DEC6_BLOCK 16
 #endif
+#ifndef DEC6_PRIO
+#define DEC6_PRIO 3
+#endif
 #ifndef DEC6_HELP_SLEEP
 #define DEC6_HELP_SLEEP 4          // the helper wavefront's pause when no lane wants a chunk (x 64 clocks; 2-16 within 0.5 %)
 #endif
@@ -594,6 +597,9 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
     uint8_t* tab2 = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(ws.lane_slots) * kTab1 +
                     static_cast<size_t>(slot) * kTab2;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
+    // the decoding wavefront ahead of its helper when both can issue (-0.5 %,
+    // profiles/r4e_dec6_prio.txt; -DDEC6_PRIO=0: equal)
+    __builtin_amdgcn_s_setprio(DEC6_PRIO);
     SlotSrc in;
     in.gen = 0; in.mctl = mctl; in.hctl = hctl; in.slot = slotp;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * kLanes6s) {
