@@ -93,6 +93,31 @@ DEV void raw_load(const uint8_t* reg, uint32_t off, Raw& w)
     w.q0 = p[0]; w.q1 = p[1]; w.q2 = p[2]; w.q3 = p[3];
 }
 
+// A dense order-1 context keeps its block's C (16 cumulative group counts,
+// 32 B) in its record, where an inline one keeps its symbols (w4..w11: val,
+// cnt, oa[0..1]).  The record load a step issues ahead then brings C along,
+// and the decoder's dense search waits for one dependent load (the symbol's
+// group) instead of two.  The copy follows every change of the block's C:
+// densify, dense_add, dense_rescale.
+template <uint32_t NV, bool O2>
+DEV void rec_c_get(const Ctx<NV, O2>& c, uint4& c0, uint4& c1)
+{
+    if constexpr (O2 && NV == 3) {
+        c0 = make_uint4(c.val[0], c.val[1], c.val[2], c.cnt[0]);
+        c1 = make_uint4(c.cnt[1], c.cnt[2], c.oa[0], c.oa[1]);
+    }
+}
+
+template <uint32_t NV, bool O2>
+DEV void rec_c_set(Ctx<NV, O2>& c, const uint4& c0, const uint4& c1, bool en)
+{
+    if constexpr (O2 && NV == 3) {
+        c.val[0] = en ? c0.x : c.val[0]; c.val[1] = en ? c0.y : c.val[1]; c.val[2] = en ? c0.z : c.val[2];
+        c.cnt[0] = en ? c0.w : c.cnt[0]; c.cnt[1] = en ? c1.x : c.cnt[1]; c.cnt[2] = en ? c1.y : c.cnt[2];
+        c.oa[0] = en ? c1.z : c.oa[0]; c.oa[1] = en ? c1.w : c.oa[1];
+    }
+}
+
 template <uint32_t NV, bool O2>
 DEV void ctx_clear(Ctx<NV, O2>& c)
 {
@@ -188,6 +213,10 @@ DEV bool ctx_dense_search(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV,
                           uint32_t& v, uint32_t& u, uint32_t& n)
 {
     if (!O2 && c.dense == 2) return dense_search(ldsb, code, O2, z, v, u, n);
+    if (O2) {                                   // (C from the record)
+        rec_c_get(c, z.c0, z.c1);
+        return dense_search(reg + c.ext, code, O2, z, v, u, n, true);
+    }
     return dense_search(reg + c.ext, code, O2, z, v, u, n);
 }
 
@@ -356,6 +385,10 @@ DEV bool densify(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c, ui
 #pragma unroll
     for (uint32_t d = 0; d < (O2 ? NV : 1); ++d) { c.oa[d] = 0u; c.ob[d] = 0u; }
     c.dense = lds ? 2u : 1u;
+    if (O2) {                                   // the block's C into the record (as dense_fill wrote it)
+        const uint4* q = reinterpret_cast<const uint4*>(reg + c.ext);
+        rec_c_set(c, q[0], q[1], true);
+    }
     return true;
 }
 
@@ -375,6 +408,10 @@ DEV void ctx_rescale(uint8_t* reg, uint8_t* ldsb, Ctx<NV, O2>& c, bool en)
         if (en && c.dense != 0) {
             if (!O2 && c.dense == 2) sum = dense_rescale(ldsb);
             else sum = dense_rescale(reg + c.ext);
+            if (O2) {                           // (the halving above hit the record's copy of C: the new C)
+                const uint4* q = reinterpret_cast<const uint4*>(reg + c.ext);
+                rec_c_set(c, q[0], q[1], true);
+            }
         }
     }
     c.esc -= en ? (c.esc >> 1) : 0u;
@@ -404,6 +441,7 @@ DEV void ctx_update(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c,
         if (en && c.dense != 0 && !ovf) {                                   // (new: o2 info is 0)
             if (!O2 && c.dense == 2) dense_add(ldsb, v, kSubDelta, h.z);
             else dense_add(reg + c.ext, v, kSubDelta, h.z);
+            rec_c_set(c, h.z.c0, h.z.c1, true);
         }
     }
     if (ins && c.dense == 0) {

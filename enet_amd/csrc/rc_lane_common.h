@@ -306,11 +306,13 @@ DEV void dense_add(uint8_t* blk, uint32_t v, uint32_t d, Dense& z)
 }
 
 // decoder: symbol whose interval [C(<v), C(<=v)) holds code (minimum 0)
+// (have_c: z.c0 / z.c1 already hold the block's C -- rc_lane3.hip keeps an
+// order-1 context's C in its record)
 DEV bool dense_search(const uint8_t* blk, uint32_t code, bool links, Dense& z, uint32_t& v, uint32_t& under,
-                      uint32_t& cnt)
+                      uint32_t& cnt, bool have_c = false)
 {
     const uint4* p = reinterpret_cast<const uint4*>(blk);
-    z.c0 = p[0]; z.c1 = p[1];
+    if (!have_c) { z.c0 = p[0]; z.c1 = p[1]; }
     uint32_t g = 0, prev = 0;
 #pragma unroll
     for (uint32_t t = 0; t < 16; ++t) {
