@@ -590,12 +590,9 @@ def dominant_kernel(decompress, handed_off=0, n=1):
     if os.environ.get("ENET_RC_KERNEL", "lane3") == "wave":
         return "rc_decompress_wave" if decompress else "rc_compress_wave"
     if decompress:
-        dk = os.environ.get("ENET_RC_DEC", "8")
-        if os.environ.get("ENET_RC_LANES", "64") != "64" and dk == "8":
-            dk = "6"
-        fast = os.environ.get("ENET_RC_DEC4", "1") != "0" and dk != "0"
-        name = {"4": "rc_decompress_dec4", "6": "rc_decompress_dec6", "7": "rc_decompress_dec7"}.get(dk, "rc_decompress_dec6s")
-        return name if fast and 2 * handed_off < n else "rc_decompress_lane3"
+        fast = (os.environ.get("ENET_RC_DEC4", "1") != "0" and os.environ.get("ENET_RC_DEC", "1") != "0"
+                and os.environ.get("ENET_RC_LANES", "64") == "64")
+        return "rc_decompress_dec6s" if fast and 2 * handed_off < n else "rc_decompress_lane3"
     if os.environ.get("ENET_RC_ENC2", "1") == "0" or 2 * handed_off >= n:
         return "rc_compress_lane3"
     one = os.environ.get("ENET_RC_ENC2_CODE1") == "1" or os.environ.get("ENET_RC_ENC2_LANES") == "32"

@@ -303,12 +303,17 @@ class MultiCoder:
         if rc != 0:
             raise RuntimeError(f"enet_rc_multi host batch failed: HIP error {rc}")
 
-    def batch_device(self, decompress: bool, inp, in_off, in_len, out, out_off, out_cap, out_len, max_len=0):
-        """torch tensors on the first listed device (the batch's dtypes as RangeCoder.compress_batch)."""
-        fn = self.lib.enet_rc_multi_decompress_batch_device if decompress else \
-            self.lib.enet_rc_multi_compress_batch_device
+    def batch_device(self, decompress: bool, inp, in_off, in_len, out, out_off, out_cap, out_len, max_len=0,
+                     stream=None):
+        """torch tensors on the first listed device (the batch's dtypes as RangeCoder.compress_batch).
+        The inputs are taken in the order of `stream` (default: torch's current stream on that
+        device), which the root device's work waits for on the GPU."""
+        import torch
+        fn = self.lib.enet_rc_multi_decompress_batch_device_stream if decompress else \
+            self.lib.enet_rc_multi_compress_batch_device_stream
+        st = stream if stream is not None else torch.cuda.current_stream(inp.device)
         rc = fn(self.ctx, inp.data_ptr(), in_off.data_ptr(), in_len.data_ptr(), in_len.numel(), int(max_len),
-                out.data_ptr(), out_off.data_ptr(), out_cap.data_ptr(), out_len.data_ptr())
+                out.data_ptr(), out_off.data_ptr(), out_cap.data_ptr(), out_len.data_ptr(), st.cuda_stream)
         if rc != 0:
             raise RuntimeError(f"enet_rc_multi device batch failed: HIP error {rc}")
 

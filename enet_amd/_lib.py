@@ -87,7 +87,9 @@ def _load() -> C.CDLL:
     for name, args in (("enet_rc_multi_compress_batch_host", batch_host),
                        ("enet_rc_multi_decompress_batch_host", batch_host),
                        ("enet_rc_multi_compress_batch_device", batch_dev[:-1]),
-                       ("enet_rc_multi_decompress_batch_device", batch_dev[:-1])):
+                       ("enet_rc_multi_decompress_batch_device", batch_dev[:-1]),
+                       ("enet_rc_multi_compress_batch_device_stream", batch_dev),
+                       ("enet_rc_multi_decompress_batch_device_stream", batch_dev)):
         f = getattr(lib, name)
         f.restype = C.c_int
         f.argtypes = args
@@ -97,6 +99,10 @@ def _load() -> C.CDLL:
     lib.enet_rc_last_exact_count.argtypes = [vp]
     lib.enet_rc_last_lane_count.restype = u32
     lib.enet_rc_last_lane_count.argtypes = [vp]
+    lib.enet_rc_config_flags.restype = u32
+    lib.enet_rc_config_flags.argtypes = [vp]
+    lib.enet_rc_last_split.restype = u32
+    lib.enet_rc_last_split.argtypes = [vp]
     lib.enet_rc_version.restype = C.c_char_p
     lib.enet_rc_version.argtypes = []
     lib.rc_hip_lds_bytes.restype = u32

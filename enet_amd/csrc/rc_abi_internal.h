@@ -60,14 +60,11 @@ typedef struct {
     void     *enc2_wide;
     uint64_t  enc2_wide_cap;  /* bytes */
     uint32_t *enc2_wlist;     /* [n_cap] */
-    /* the fast decoder in front of the v3 lane decoder: 8 = record-light with its input through
-       LDS slots a helper wavefront refills (rc_dec6.hip rc_decompress_dec6s, default with
-       lane_active == 64), 6 = the same loading its own input (rc_decompress_dec6; ENET_RC_DEC=6,
-       or lane_active != 64), 7 = record-light with serving wavefronts (rc_dec7.hip;
-       ENET_RC_DEC=7), 4 = bucket-history (rc_dec4.hip; ENET_RC_DEC=4), 0 = none (ENET_RC_DEC4=0
-       or ENET_RC_DEC=0);
+    /* the fast decoder in front of the v3 lane decoder: 1 = the record-light decoder with its
+       input through LDS slots a helper wavefront refills (rc_dec6.hip rc_decompress_dec6s; the
+       default, lane_active == 64), 0 = none (ENET_RC_DEC=0, or lane_active != 64);
        the packets it leaves go to enc2_list / counters[3] */
-    uint32_t  dec4;
+    uint32_t  fast_dec;
     /* rc_dec6.hip: per packet, the positions the decoder took to start a new bigram (its
        check, rc_dec6_verify), 0xFFFFFFFF for a packet left to the lane kernels */
     uint32_t *claims;       /* [n_cap] */
@@ -108,20 +105,12 @@ uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len);
 uint64_t rc_hip_enc2_wide_slot_bytes(uint32_t max_len);
 int rc_hip_enc2_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
 
-/* Bucket-history decoder (rc_dec4.hip): one packet per lane over the lane
- * regions; packets off its fast path are listed in ws->enc2_list, count in
- * ws->counters[3]. */
-int rc_hip_dec4_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
-
 /* Record-light decoder (rc_dec6.hip) and its check: one packet per lane, model in LDS;
  * packets off its fast path or failing the check are listed in ws->enc2_list, count in
  * ws->counters[3]. */
 int rc_hip_dec6_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
-/* rc_dec6.hip's check alone (after rc_decompress_dec6 or rc_decompress_dec7). */
+/* rc_dec6.hip's check alone (after rc_decompress_dec6s). */
 int rc_hip_dec6_verify_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, void *stream);
-/* Record-light decoder with a helper wavefront per SIMD (rc_dec7.hip), then the check;
- * needs lane_active == 64.  Same lists as rc_hip_dec6_launch. */
-int rc_hip_dec7_launch(const rc_batch_dev *b, const rc_workspace_dev *ws, uint32_t blocks, void *stream);
 
 /* Per-lane region size the lane kernels need for packets up to max_len bytes. */
 uint32_t rc_hip_lane3_region_bytes(uint32_t max_len);

@@ -1,14 +1,13 @@
 // rc_dec6.hip -- record-light range decoder (compress.c:498-627), bit-exact.
 //
-// One packet per lane, like the bucket-history decoder (rc_dec4.hip), whose
-// algebra it shares: position j's order-1 context is x[j-1], its order-2
-// context (x[j-2], x[j-1]); both hold only the positions of bucket x[j-1], and
-// every sub-context statistic is a function of those elements (a = x[j-2],
-// v = x[j], decoded at order 2 or not).  What differs is where the model
-// lives.  dec4 reads and writes a 64-B bucket record in HBM for every byte --
-// one random read-modify-write per byte over a 1-GB table, which is the
-// decoder's bound.  Here the common step touches no model in
-// memory at all:
+// One packet per lane.  The bucket algebra: position j's order-1 context is
+// x[j-1], its order-2 context (x[j-2], x[j-1]); both hold only the positions
+// of bucket x[j-1], and every sub-context statistic is a function of those
+// elements (a = x[j-2], v = x[j], decoded at order 2 or not).  A decoder that
+// keeps each bucket as a 64-B record in HBM reads and writes one for every
+// byte -- one random read-modify-write per byte over a 1-GB table, which bound
+// the round-2 decoder (rc_dec4.hip, retired in round 5).  Here the
+// common step touches no model in memory at all:
 //
 //   * per bucket, one LDS byte: t1 (positions that visited order 1) and
 //     r1 = t1 - d1 (those that found their symbol there): the order-1
@@ -30,7 +29,7 @@
 // order-2 context exists (the step after a hit) -- stalls its lane.  Every
 // kBlock6 steps the wavefront runs the rare phase for its stalled lanes
 // together: each loads its bucket's records and decodes its step exactly, with
-// dec4's algebra over the unsorted elements (order-2 hits, which leave order
+// the bucket algebra over the unsorted elements (order-2 hits, which leave order
 // 1 alone, are kept in registers).  An earlier version rebuilt the bucket by
 // scanning the packet's decoded output instead: ~40 dependent 16-B loads per
 // rare phase, 7.3 ms for C2 against 1.06 ms for the common steps alone.
@@ -67,7 +66,6 @@
 #include "rc_udiv.h"
 #include "rc_lane_common.h"
 #include "rc_root3.h"
-#include "rc_bucket4.h"
 #include "rc_dec6_rare.h"
 #include "rc_slot.h"
 
@@ -189,9 +187,9 @@ DEV void sink1_finish(ByteSink1& o)
     sink_bytes(o.waddr, make_uint4(q[0], q[1], q[2], q[3]), 0ull, 4 * ws + o.nb, o.lo);
 }
 
-// Src: ByteSrc (the stream's chunks loaded by the lane, rc_decompress_dec6) or
-// SlotSrc (through the LDS slot a helper wavefront refills, rc_slot.h,
-// rc_decompress_dec6s).
+// Src: SlotSrc (through the LDS slot a helper wavefront refills, rc_slot.h,
+// rc_decompress_dec6s) or ByteSrc (the stream's chunks loaded by the lane
+// itself: the host build of tests/proto/lane_host.cpp, variant v6).
 template <class Src>
 DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* root,
                          uint8_t* stats, uint8_t* tab, uint8_t* tab2, const uint8_t* itab, Src& in)
@@ -249,8 +247,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             uint32_t shc = 0;                                  // (SlotSrc: h_ctl and the slot, used at the end)
             uint4 ssl = make_uint4(0u, 0u, 0u, 0u);
             if constexpr (kSlot) {
-                shc = *in.hctl;
-                ssl = *reinterpret_cast<const uint4*>(in.slot);
+                slot_read(in, shc, ssl);
             } else {
                 src_fill(in, true);
             }
@@ -372,8 +369,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             uint32_t shc = 0;
             uint4 ssl = make_uint4(0u, 0u, 0u, 0u);
             if constexpr (kSlot) {
-                shc = *in.hctl;
-                ssl = *reinterpret_cast<const uint4*>(in.slot);
+                slot_read(in, shc, ssl);
             } else {
                 src_fill(in, true);
             }
@@ -533,34 +529,7 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
 }  // namespace
 
 #ifndef RC_LANE_HOST_TEST
-// one wave per SIMD by design (a packet per lane, 65536 lanes fill the chip)
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void rc_decompress_dec6(rc_batch_dev b, rc_workspace_dev ws)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t act = ws.lane_active;
-    const uint32_t wave = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const uint32_t local = wave * act + l;
-    uint8_t* root = smem + local * kLds6;
-    uint8_t* stats = root + kStats6;
-    uint8_t* itab = smem + 4 * act * kLds6;          // root3_inc_init's table, 16 x 32 B
-    if (threadIdx.x < 16) root3_inc_init(itab, threadIdx.x);
-    __syncthreads();
-    const uint32_t per_block = 4 * act;
-    const uint32_t slot = blockIdx.x * per_block + local;
-    uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * kTab1;
-    uint8_t* tab2 = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(ws.lane_slots) * kTab1 +
-                    static_cast<size_t>(slot) * kTab2;
-    const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
-    if (l >= act) return;
-    ByteSrc in;
-    for (uint32_t i = slot; i < b.n; i += gridDim.x * per_block) {
-        const uint32_t pkt = order ? order[i] : i;
-        decompress_one6(b, ws, pkt, root, stats, tab, tab2, itab, in);
-    }
-}
-
-// The same with the lanes' input through LDS (rc_slot.h): waves 0-3 decode,
+// The decoder, with the lanes' input through LDS (rc_slot.h): waves 0-3 decode,
 // wave w + 4 (on wave w's SIMD) keeps their slots filled.  LDS per lane:
 // root | slot (the root's pad) | bucket bytes, then m_ctl / m_pkt, h_ctl;
 // then root3_inc_init's table (16 x 32 B).
@@ -609,7 +578,7 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
     mctl[1] = kFinS;
 }
 
-// Counts the distinct bigrams of each packet rc_decompress_dec6 decoded and
+// Counts the distinct bigrams of each packet rc_decompress_dec6s decoded and
 // lists the packets whose count differs from the decoder's (see the header).
 // A wavefront per packet: a 65536-bit set in LDS, cleared per packet; a lane
 // sets the bits of its positions' bigrams with LDS atomics and counts the
@@ -823,16 +792,10 @@ extern "C" int rc_hip_dec6_verify_launch(const rc_batch_dev* b, const rc_workspa
 extern "C" int rc_hip_dec6_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t blocks, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (ws->dec4 == 8 && ws->lane_active == 64) {
-        // (the slot variant: 12 B more per lane for the control words)
-        const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12) + 512;
-        hipLaunchKernelGGL(rc_decompress_dec6s, dim3(blocks), dim3(512), lds, st, *b, *ws);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return static_cast<int>(e);
-        return rc_hip_dec6_verify_launch(b, ws, stream);
-    }
-    const size_t lds = static_cast<size_t>(4 * ws->lane_active) * kLds6 + 512;
-    hipLaunchKernelGGL(rc_decompress_dec6, dim3(blocks), dim3(256), lds, st, *b, *ws);
+    if (ws->lane_active != 64) return static_cast<int>(hipErrorInvalidValue);
+    // (12 B more per lane than the model for the slot control words)
+    const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12) + 512;
+    hipLaunchKernelGGL(rc_decompress_dec6s, dim3(blocks), dim3(512), lds, st, *b, *ws);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
     return rc_hip_dec6_verify_launch(b, ws, stream);

@@ -1,11 +1,32 @@
-// rc_dec6_rare.h -- the record-light decoders' exact step over a bucket's
-// elements (rc_dec6.hip's rare phase, rc_dec7.hip's helper wavefront):
-// compress.c:536-568 in the order-2 and order-1 contexts of position j, both
-// rebuilt from the elements of bucket x[j-1] (dec4's algebra, rc_dec4.hip).
-// Include after rc_lane_common.h and rc_bucket4.h.
+// rc_dec6_rare.h -- the record-light decoder's exact step over a bucket's
+// elements (rc_dec6.hip's rare phase): compress.c:536-568 in the order-2 and
+// order-1 contexts of position j, both rebuilt from the elements of bucket
+// x[j-1] (the bucket algebra of rc_dec6.hip's header; tests/proto/histdec.py
+// restates it).  Include after rc_lane_common.h.
 #pragma once
 
 namespace {
+
+// 0x01 in each byte where x and y agree
+DEV uint32_t eq01(uint32_t x, uint32_t y)
+{
+    const uint32_t z = x ^ y;
+    const uint32_t t = ((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z;
+    return (~t >> 7) & 0x01010101u;
+}
+
+// the 0x01 bytes of e as four bits
+DEV uint32_t gather4(uint32_t e) { return (e | (e >> 7) | (e >> 14) | (e >> 21)) & 0xFu; }
+
+DEV uint32_t popc(uint32_t x) { return static_cast<uint32_t>(__builtin_popcount(x)); }
+DEV uint32_t low_bits(uint32_t n) { return n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u); }
+
+// a packet left for the lane kernels (their sub-list, counters[3])
+DEV void bail(const rc_workspace_dev& ws, uint32_t pkt)
+{
+    const uint32_t slot = atomicAdd(&ws.counters[3], 1u);
+    ws.enc2_list[slot] = pkt;
+}
 
 // A lane's records: its first table (16-B records, 4 KB) in a dense array of
 // first tables, its second table (48-B records) and dummy slots apart, so

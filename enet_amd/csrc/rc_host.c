@@ -188,8 +188,15 @@ static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
         hipDeviceSynchronize();
         if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
         c->ws.enc2_stream = NULL; c->ws.enc2_cap = 0;
-        /* + 1 MB past the stream: the code pass's dummy store targets (rc_enc2.hip) */
-        if (hipMalloc(&c->ws.enc2_stream, want + (1u << 20)) != hipSuccess) return -1;
+        /* + 1 MB past the stream: the code pass's dummy store targets (rc_enc2.hip).
+         * A device short of memory gets a smaller stream (the batch then runs in
+         * more chunks), down to one packet's slot. */
+        while (hipMalloc(&c->ws.enc2_stream, want + (1u << 20)) != hipSuccess) {
+            c->ws.enc2_stream = NULL;
+            (void) hipGetLastError();
+            if (want <= slot) return -1;
+            want = want / 2 > slot ? (want / 2) / slot * slot : slot;
+        }
         c->ws.enc2_cap = want;
     }
     if (c->enc2_wide_on) {
@@ -276,17 +283,13 @@ void *enet_range_coder_create(void)
         c->enc2_wide_on = !(ew && strcmp(ew, "0") == 0);
         c->enc2_stream_max = env_mb_cap("ENET_RC_ENC2_STREAM_MB", ENC2_STREAM_MAX);
         c->enc2_wide_max = env_mb_cap("ENET_RC_ENC2_WIDE_MB", ENC2_WIDE_MAX);
-        /* the fast decoder: rc_dec6.hip with its input through LDS slots (8,
-           rc_decompress_dec6s; 64 packets per wavefront) unless ENET_RC_DEC=6
-           (its own chunk loads, rc_decompress_dec6), 7 (rc_dec7.hip) or 4
-           (rc_dec4.hip); none with ENET_RC_DEC=0 or ENET_RC_DEC4=0 */
+        /* the fast decoder: rc_dec6.hip's rc_decompress_dec6s (64 packets per
+           wavefront); none with ENET_RC_DEC=0 (ENET_RC_DEC4=0, the older name,
+           too) or with 32 / 16 packets per wavefront */
         const char *d4 = getenv("ENET_RC_DEC4");
         const char *dk = getenv("ENET_RC_DEC");
-        c->ws.dec4 = c->ws.lane_active == 64 ? 8 : 6;
-        if (dk && strcmp(dk, "6") == 0) c->ws.dec4 = 6;
-        if (dk && strcmp(dk, "7") == 0 && c->ws.lane_active == 64) c->ws.dec4 = 7;
-        if (dk && strcmp(dk, "4") == 0) c->ws.dec4 = 4;
-        if ((dk && strcmp(dk, "0") == 0) || (d4 && strcmp(d4, "0") == 0)) c->ws.dec4 = 0;
+        c->ws.fast_dec = c->ws.lane_active == 64;
+        if ((dk && strcmp(dk, "0") == 0) || (d4 && strcmp(d4, "0") == 0)) c->ws.fast_dec = 0;
         const char *dd = getenv("ENET_RC_DEC6_DEBUG");
         c->ws.dec6_debug = dd ? (uint32_t) atoi(dd) : 0u;
         const char *es = getenv("ENET_RC_ENC2_SLOW");
@@ -300,6 +303,26 @@ void *enet_range_coder_create(void)
 fail:
     enet_range_coder_destroy(c);
     return NULL;
+}
+
+/* The settings enet_range_coder_create reads from the environment, copied
+ * from a context to another on the same device (run_host_split's second
+ * half runs with its parent's configuration, whatever the environment says
+ * by then). */
+static void ctx_copy_config(rc_ctx *dst, const rc_ctx *src)
+{
+    dst->ws.kernel = src->ws.kernel;
+    dst->ws.lane_active = src->ws.lane_active;
+    dst->ws.small_max = src->ws.small_max;
+    dst->ws.cus = src->ws.cus;
+    dst->ws.fast_dec = src->ws.fast_dec;
+    dst->ws.dec6_debug = src->ws.dec6_debug;
+    dst->ws.enc2_slow = src->ws.enc2_slow;
+    dst->enc2_on = src->enc2_on;
+    dst->enc2_wide_on = src->enc2_wide_on;
+    dst->enc2_stream_max = src->enc2_stream_max;
+    dst->enc2_wide_max = src->enc2_wide_max;
+    dst->max_slots = src->max_slots;
 }
 
 void enet_range_coder_destroy(void *context)
@@ -1003,7 +1026,10 @@ static int run_host_split(rc_ctx *c, int decompress, const uint8_t *in, const ui
         ohi <= olo)
         return run_host(c, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
-    if (!c->twin) c->twin = enet_range_coder_create();
+    if (!c->twin) {
+        c->twin = enet_range_coder_create();
+        if (c->twin) ctx_copy_config((rc_ctx *) c->twin, c);
+    }
     const int pi = c->twin ? host_pin(in + ilo, ihi - ilo) : 0;
     const int po = pi ? host_pin(out + olo, ohi - olo) : 0;
     struct h2d_sync y;
@@ -1378,6 +1404,30 @@ uint32_t enet_rc_last_exact_count(void *context)
         hipMemcpy(&w, ((rc_ctx *) c->twin)->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
     return v + w;
 }
+
+/* The context's kernel configuration as flag bits (the settings
+ * enet_range_coder_create read from the environment); bit 31: the context
+ * that runs the second half of its split host batches (run_host_split) has a
+ * different one. */
+static uint32_t config_flags(const rc_ctx *c)
+{
+    return (c->ws.kernel == RC_KERNEL_WAVE ? 1u : 0u) | (c->enc2_on ? 2u : 0u) | (c->enc2_wide_on ? 4u : 0u) |
+           (c->ws.fast_dec ? 8u : 0u) | (c->ws.enc2_slow ? 16u : 0u) | ((c->ws.lane_active & 0x7Fu) << 8);
+}
+
+uint32_t enet_rc_config_flags(void *context)
+{
+    const rc_ctx *c = (const rc_ctx *) context;
+    if (!c) return 0;
+    const uint32_t f = config_flags(c);
+    const rc_ctx *t = (const rc_ctx *) c->twin;
+    return f | ((t && (config_flags(t) != f || t->enc2_stream_max != c->enc2_stream_max ||
+                       t->enc2_wide_max != c->enc2_wide_max || t->max_slots != c->max_slots ||
+                       t->ws.small_max != c->ws.small_max || t->ws.dec6_debug != c->ws.dec6_debug))
+                    ? 0x80000000u : 0u);
+}
+
+uint32_t enet_rc_last_split(void *context) { return context && ((rc_ctx *) context)->last_split ? 1u : 0u; }
 
 /* ------------------------------------------------------ for rc_multi.c */
 

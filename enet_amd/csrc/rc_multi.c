@@ -16,11 +16,17 @@
  *                    (rc_multi_plan.hip; the host reads back 5 words per
  *                    device, nothing per packet); every other device's range
  *                    is copied to it over the peer link (hipMemcpyPeerAsync:
- *                    xGMI between MI355X), its offsets rebased there,
- *                    coded there, packed back to back (rc_pack.hip) and
- *                    copied back, then unpacked into the root's output slots
- *                    -- only the produced bytes cross the link, and nothing
- *                    outside [out_off[i], out_off[i] + out_len[i]) is written.
+ *                    xGMI between MI355X), its offsets rebased there and
+ *                    coded there; the root's stream waits for that device's
+ *                    event and a copy kernel on the root reads each packet's
+ *                    produced bytes straight out of the device's slots over
+ *                    the link (peer access) into the root's slots -- only the
+ *                    produced bytes cross the link, nothing outside
+ *                    [out_off[i], out_off[i] + out_len[i]) is written, and the
+ *                    host waits for nothing between the plan's read-back and
+ *                    the end.  Without peer access (no xGMI path) the slot
+ *                    range comes over in one runtime-staged copy into a root
+ *                    buffer sized from the plan, then the same copy kernel.
  * The split is enet_rc_multi_split (also exported, for tests and callers
  * that place packets themselves).
  */
@@ -40,21 +46,21 @@
 typedef struct {
     void *ctx;                      /* coder context bound to the device */
     int device;
+    int peer;                       /* the root reads this device's memory directly (same device, or peer access) */
     uint8_t *buf;                   /* device version, non-root: this device's copy of its range */
     size_t buf_cap;
-    hipEvent_t done;                /* its packed results are on the root */
+    hipEvent_t done;                /* its results are ready for the root to read */
 } rc_dev;
 
 typedef struct {
     size_t n;
     rc_dev d[RC_MULTI_MAX];
-    uint8_t *stage;                 /* root: the other devices' packed results */
+    uint8_t *stage;                 /* root: slot ranges of devices without peer access */
     size_t stage_cap;
     uint64_t *d_plan;               /* root: the split's plan and scan words (rc_multi_plan.hip) */
     size_t plan_cap;
-    uint64_t *h_plan;               /* pinned: the plan as read back; then each device's packed bytes */
-    uint64_t *h_packed;
-    hipEvent_t ready;               /* root: the caller's inputs (its null stream) */
+    uint64_t *h_plan;               /* pinned: the plan as read back */
+    hipEvent_t ready;               /* root: the caller's inputs */
 } rc_multi;
 
 int enet_rc_multi_split(const uint32_t *in_len, size_t n, size_t parts, uint64_t *first)
@@ -115,20 +121,21 @@ void *enet_rc_multi_create(const int *devices, size_t n_devices)
     }
     hipSetDevice(devices[0]);
     if (hipEventCreateWithFlags(&m->ready, hipEventDisableTiming) != hipSuccess) goto fail;
-    if (hipHostMalloc((void **) &m->h_plan, (5 * RC_MULTI_MAX + 1 + RC_MULTI_MAX) * 8, 0) != hipSuccess) {
+    if (hipHostMalloc((void **) &m->h_plan, (5 * RC_MULTI_MAX + 1) * 8, 0) != hipSuccess) {
         m->h_plan = NULL;
         goto fail;
     }
-    m->h_packed = m->h_plan + 5 * RC_MULTI_MAX + 1;
     /* direct peer access between the root and every other device (xGMI);
-     * where it is unavailable (same device, no link) copies are staged by the
-     * runtime, which is slower but correct */
+     * where it is unavailable (no link) the input copies are staged by the
+     * runtime and the results come back through the root's stage buffer */
+    m->d[0].peer = 1;
     for (size_t k = 1; k < n_devices; ++k) {
-        if (devices[k] == devices[0]) continue;
+        if (devices[k] == devices[0]) { m->d[k].peer = 1; continue; }
         int can = 0;
         if (hipDeviceCanAccessPeer(&can, devices[0], devices[k]) == hipSuccess && can) {
             hipSetDevice(devices[0]);
-            hipDeviceEnablePeerAccess(devices[k], 0);
+            const hipError_t e = hipDeviceEnablePeerAccess(devices[k], 0);
+            m->d[k].peer = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
             hipSetDevice(devices[k]);
             hipDeviceEnablePeerAccess(devices[0], 0);
         }
@@ -287,12 +294,26 @@ typedef struct {
     size_t lo, cnt;                 /* packet range */
     uint64_t lo_in, pay;            /* input bytes [lo_in, lo_in + pay) of the root's in */
     uint64_t lo_out, slots;         /* output slot bytes [lo_out, lo_out + slots) */
-    size_t a_ioff, a_ilen, a_out, a_ooff, a_ocap, a_olen, a_pack, total;
+    size_t a_ioff, a_ilen, a_out, a_ooff, a_ocap, a_olen, total;
 } share;
+
+/* root stage bytes for the devices the root cannot read directly: each one's
+ * whole slot range, sized from the plan (no read-back of produced sizes) */
+static int stage_reserve_multi(rc_multi *m, uint64_t need, void *rst)
+{
+    if (need <= m->stage_cap) return 0;
+    hipStreamSynchronize((hipStream_t) rst);
+    if (m->stage) hipFree(m->stage);
+    m->stage = NULL; m->stage_cap = 0;
+    if (hipMalloc((void **) &m->stage, need) != hipSuccess) return (int) hipErrorOutOfMemory;
+    m->stage_cap = need;
+    return 0;
+}
 
 static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const uint64_t *in_off,
                         const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
-                        const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
+                        const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len, void *stream,
+                        int have_stream)
 {
     if (!m) return (int) hipErrorInvalidValue;
     if (n == 0) return 0;
@@ -302,11 +323,18 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
     const int root = m->d[0].device;
     void *rst = rc_ctx_stream(m->d[0].ctx);
     hipError_t err = hipSetDevice(root);
-    /* the caller's inputs are complete on the root's null stream (which waits
-     * for every blocking stream): the root's stream waits for that, the host
-     * does not */
-    if (err == hipSuccess) err = hipEventRecord(m->ready, 0);
-    if (err == hipSuccess) err = hipStreamWaitEvent((hipStream_t) rst, m->ready, 0);
+    /* the caller's inputs: complete on the caller's stream (the root's stream
+     * waits for an event recorded there; the host does not), or -- no stream
+     * given -- on the whole root device (a device-wide wait: streams created
+     * non-blocking, as PyTorch's are, do not order with the null stream) */
+    if (err == hipSuccess) {
+        if (have_stream) {
+            err = hipEventRecord(m->ready, (hipStream_t) stream);
+            if (err == hipSuccess) err = hipStreamWaitEvent((hipStream_t) rst, m->ready, 0);
+        } else {
+            err = hipDeviceSynchronize();
+        }
+    }
     if (err != hipSuccess) { hipSetDevice(prev); return (int) err; }
     int rc = 0;
     if (m->n == 1) {                /* one device: the plain batch */
@@ -320,7 +348,15 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
     const uint64_t *first = m->h_plan, *ext = m->h_plan + m->n + 1;
     share sh[RC_MULTI_MAX];
     memset(sh, 0, sizeof sh);
-    /* phase 1: scatter, code, pack -- every device enqueued before any wait */
+    /* the stage for devices without peer access, sized from the plan */
+    uint64_t stage_need = 0, stage_at[RC_MULTI_MAX];
+    for (size_t k = 1; k < m->n && !rc; ++k) {
+        const uint64_t *e = ext + 4 * k;
+        stage_at[k] = stage_need;
+        if (!m->d[k].peer && first[k + 1] > first[k]) stage_need += al16(e[3] - e[2]);
+    }
+    if (!rc && stage_need) rc = stage_reserve_multi(m, stage_need, rst);
+    /* phase 1: scatter and code -- every device enqueued, nothing waited for */
     for (size_t k = 0; k < m->n && !rc; ++k) {
         rc_dev *d = &m->d[k];
         share *s = &sh[k];
@@ -345,8 +381,7 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
         s->a_ooff = al16(s->a_out + s->slots);
         s->a_ocap = s->a_ooff + s->cnt * 8;
         s->a_olen = al16(s->a_ocap + s->cnt * 4);
-        s->a_pack = al16(s->a_olen + s->cnt * 4);
-        s->total = s->a_pack + s->slots + 16;
+        s->total = s->a_olen + s->cnt * 4 + 16;
         if ((err = hipSetDevice(d->device)) != hipSuccess) { rc = (int) err; break; }
         if (s->total > d->buf_cap) {
             hipStreamSynchronize((hipStream_t) st);
@@ -356,8 +391,6 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
             d->buf_cap = s->total;
         }
         uint8_t *b = d->buf;
-        uint64_t *bsum = rc_ctx_bsum(d->ctx, s->cnt);
-        if (!bsum) { rc = (int) hipErrorOutOfMemory; break; }
         /* the range's bytes and metadata over the peer link; offsets rebased there */
         hipStream_t hs = (hipStream_t) st;
         err = hipMemcpyPeerAsync(b, d->device, in + s->lo_in, root, s->pay, hs);
@@ -374,51 +407,26 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
                                (const uint64_t *) (b + s->a_ooff), (const uint32_t *) (b + s->a_ocap),
                                (uint32_t *) (b + s->a_olen), st);
         if (rc) break;
-        rc = rc_hip_pack(b + s->a_out, (const uint64_t *) (b + s->a_ooff), (const uint32_t *) (b + s->a_olen),
-                         (uint32_t) s->cnt, bsum, b + s->a_pack, st);
-        if (rc) break;
-        /* the lengths to the root now; the packed bytes once their total is known */
+        /* the lengths to the root; without peer access the whole slot range too */
         err = hipMemcpyPeerAsync(out_len + s->lo, root, b + s->a_olen, d->device, s->cnt * 4, hs);
-        if (err == hipSuccess)
-            err = hipMemcpyAsync(&m->h_packed[k], bsum + (s->cnt + 1023) / 1024, 8, hipMemcpyDeviceToHost, hs);
+        if (err == hipSuccess && !d->peer)
+            err = hipMemcpyPeerAsync(m->stage + stage_at[k], root, b + s->a_out, d->device, s->slots, hs);
+        if (err == hipSuccess) err = hipEventRecord(d->done, hs);
         if (err != hipSuccess) { rc = (int) err; break; }
     }
-    /* phase 2: gather -- each device's packed bytes to the root's staging,
-     * unpacked into the output slots on the root's stream behind an event */
-    uint64_t stage_need = 0, stage_at[RC_MULTI_MAX];
+    /* phase 2: gather -- the root's stream waits for each device's event, then
+     * one copy kernel per device moves each packet's produced bytes into the
+     * root's slots, reading the device's slots over the link (or the stage) */
+    if (!rc) hipSetDevice(root);
     for (size_t k = 1; k < m->n && !rc; ++k) {
-        if (sh[k].cnt == 0) continue;
-        if ((err = hipSetDevice(m->d[k].device)) != hipSuccess ||
-            (err = hipStreamSynchronize((hipStream_t) rc_ctx_stream(m->d[k].ctx))) != hipSuccess) { rc = (int) err; break; }
-        if (m->h_packed[k] > sh[k].slots) { rc = (int) hipErrorUnknown; break; }
-        stage_at[k] = stage_need;
-        stage_need += al16(m->h_packed[k]);
-    }
-    if (!rc && stage_need) {
-        hipSetDevice(root);
-        if (stage_need > m->stage_cap) {
-            hipStreamSynchronize((hipStream_t) rst);
-            if (m->stage) hipFree(m->stage);
-            m->stage = NULL; m->stage_cap = 0;
-            if (hipMalloc((void **) &m->stage, stage_need) != hipSuccess) rc = (int) hipErrorOutOfMemory;
-            else m->stage_cap = stage_need;
-        }
-        uint64_t *rbsum = rc ? NULL : rc_ctx_bsum(m->d[0].ctx, n);
-        if (!rc && !rbsum) rc = (int) hipErrorOutOfMemory;
-        for (size_t k = 1; k < m->n && !rc; ++k) {
-            share *s = &sh[k];
-            if (s->cnt == 0) continue;
-            hipSetDevice(m->d[k].device);
-            void *st = rc_ctx_stream(m->d[k].ctx);
-            const uint64_t packed = m->h_packed[k];
-            err = packed ? hipMemcpyPeerAsync(m->stage + stage_at[k], root, m->d[k].buf + s->a_pack, m->d[k].device,
-                                              packed, (hipStream_t) st) : hipSuccess;
-            if (err == hipSuccess) err = hipEventRecord(m->d[k].done, (hipStream_t) st);
-            if (err == hipSuccess) { hipSetDevice(root); err = hipStreamWaitEvent((hipStream_t) rst, m->d[k].done, 0); }
-            if (err != hipSuccess) { rc = (int) err; break; }
-            rc = rc_hip_unpack(m->stage + stage_at[k], out, out_off + s->lo, out_len + s->lo, (uint32_t) s->cnt,
-                               rbsum, rst);
-        }
+        share *s = &sh[k];
+        if (s->cnt == 0) continue;
+        err = hipStreamWaitEvent((hipStream_t) rst, m->d[k].done, 0);
+        if (err != hipSuccess) { rc = (int) err; break; }
+        /* src + out_off[i] is packet i's slot on the device: its slots sit at
+         * a_out + (out_off[i] - lo_out) */
+        const uint8_t *src = (m->d[k].peer ? m->d[k].buf + s->a_out : m->stage + stage_at[k]) - s->lo_out;
+        rc = rc_hip_slot_copy(src, out_off + s->lo, out_len + s->lo, (uint32_t) s->cnt, out, rst);
     }
     /* everything done before returning (the device batch calls of one
      * context return with work enqueued; this one returns with results) */
@@ -450,14 +458,30 @@ int enet_rc_multi_compress_batch_device(void *multi, const uint8_t *in, const ui
                                         const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
                                         const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return multi_device((rc_multi *) multi, 0, in, in_off, in_len, n, max_len, out, out_off, out_cap, out_len);
+    return multi_device((rc_multi *) multi, 0, in, in_off, in_len, n, max_len, out, out_off, out_cap, out_len, NULL, 0);
 }
 
 int enet_rc_multi_decompress_batch_device(void *multi, const uint8_t *in, const uint64_t *in_off,
                                           const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
                                           const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len)
 {
-    return multi_device((rc_multi *) multi, 1, in, in_off, in_len, n, max_len, out, out_off, out_cap, out_len);
+    return multi_device((rc_multi *) multi, 1, in, in_off, in_len, n, max_len, out, out_off, out_cap, out_len, NULL, 0);
+}
+
+int enet_rc_multi_compress_batch_device_stream(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                               const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                                               const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+                                               void *stream)
+{
+    return multi_device((rc_multi *) multi, 0, in, in_off, in_len, n, max_len, out, out_off, out_cap, out_len, stream, 1);
+}
+
+int enet_rc_multi_decompress_batch_device_stream(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                                 const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                                                 const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+                                                 void *stream)
+{
+    return multi_device((rc_multi *) multi, 1, in, in_off, in_len, n, max_len, out, out_off, out_cap, out_len, stream, 1);
 }
 
 size_t enet_rc_multi_devices(void *multi) { return multi ? ((rc_multi *) multi)->n : 0; }

@@ -1,6 +1,6 @@
 // rc_route.hip -- the lane-path launcher: length binning of ragged batches,
 // then the fast kernels (two-pass encoder rc_enc2.hip, record-light decoder
-// rc_dec7.hip / rc_dec6.hip or bucket-history decoder rc_dec4.hip) and the v3 lane kernels (rc_lane3.hip) for what they leave.
+// rc_dec6.hip) and the v3 lane kernels (rc_lane3.hip) for what they leave.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -137,12 +137,10 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
         w.sub_list = ws->enc2_list;
         w.sub_count = ws->counters + 3;
     }
-    if (decompress && ws->dec4) {
-        // the fast decoder takes what it can (rc_dec6.hip, or rc_dec4.hip);
-        // the lanes decode only the packets it lists
-        const int rc = ws->dec4 == 7 ? rc_hip_dec7_launch(b, &w, blocks, stream)
-                     : (ws->dec4 == 6 || ws->dec4 == 8) ? rc_hip_dec6_launch(b, &w, blocks, stream)
-                                     : rc_hip_dec4_launch(b, &w, blocks, stream);
+    if (decompress && ws->fast_dec && act == 64) {
+        // the fast decoder takes what it can (rc_dec6.hip); the lanes decode
+        // only the packets it lists
+        const int rc = rc_hip_dec6_launch(b, &w, blocks, stream);
         if (rc != 0) return rc;
         w.sub_list = ws->enc2_list;
         w.sub_count = ws->counters + 3;

@@ -12,11 +12,24 @@
 // decoding wavefront issues no global load for its input at all.
 //
 // Words (each written by one side only):
-//   m_ctl = wanted chunk (12 bits) << 16 | packet generation (4 bits) << 28,
+//   m_ctl = wanted chunk (12 bits) << 16 | packet generation (16 bits),
 //   m_pkt = the packet (kNoPktS before the first, kFinS when the lane is done),
-//   h_ctl = the slot's chunk << 16 | its generation << 28.
+//   h_ctl = the slot's chunk << 16 | its generation.
 // The decoding side waits only for the helper, the helper only for its own
 // loads: no deadlock.
+//
+// Ordering.  The helper stores the slot, then h_ctl with a workgroup-scope
+// release (the slot's LDS write has completed before h_ctl is written).  The
+// decoder reads h_ctl, then the slot, with a compiler barrier between the two
+// reads (slot_read), so they issue in that order; a wavefront's LDS operations
+// are performed in issue order, so a slot read that follows an h_ctl read
+// which saw chunk j sees chunk j (or a later one, which the chunk index in
+// h_ctl then does not announce yet: the decoder only takes a slot whose
+// announced chunk is the one it wants).  No wait is put on the decoder's step
+// (an acquire load would add an LDS round trip to every step).
+// A 16-bit generation per lane -- wrapping only after 65535 packets on one lane
+// -- and the packet index (m_pkt) both mark a new packet for the helper, which
+// then forgets the chunk it holds.
 #pragma once
 
 namespace {
@@ -41,7 +54,19 @@ struct SlotSrc {
     const uint8_t* slot;
 };
 
-DEV void slot_publish(const SlotSrc& s) { s.mctl[0] = ((s.want & 0xFFFu) << 16) | (s.gen << 28); }
+DEV void slot_publish(const SlotSrc& s) { s.mctl[0] = ((s.want & 0xFFFu) << 16) | s.gen; }
+
+// h_ctl, then the slot, in that order (see the header)
+DEV void slot_read(const SlotSrc& s, uint32_t& hc, uint4& sl)
+{
+#ifndef RC_LANE_HOST_TEST
+    hc = __hip_atomic_load(s.hctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+#else
+    hc = *s.hctl;
+#endif
+    sl = *reinterpret_cast<const uint4*>(s.slot);
+}
 
 DEV void slot_shift(SlotSrc& s, bool en)
 {
@@ -63,7 +88,7 @@ DEV void slot_fill(SlotSrc& s, bool en)
 // c used up: the slot's chunk if it is chunk j + 1 (hc: h_ctl as read, sl: the slot)
 DEV void slot_take(SlotSrc& s, const uint4& sl, uint32_t hc, bool en)
 {
-    const bool ready = ((hc >> 16) & 0xFFFu) == ((s.j + 1) & 0xFFFu) && (hc >> 28) == s.gen;
+    const bool ready = ((hc >> 16) & 0xFFFu) == ((s.j + 1) & 0xFFFu) && (hc & 0xFFFFu) == s.gen;
     const bool t = en && s.q == 4 && ready;
     s.c.x = t ? sl.x : s.c.x; s.c.y = t ? sl.y : s.c.y; s.c.z = t ? sl.z : s.c.z; s.c.w = t ? sl.w : s.c.w;
     s.q = t ? 0u : s.q;
@@ -91,8 +116,9 @@ DEV void slot_need1(SlotSrc& s, bool en)
 {
     bool w = en && s.na == 0 && s.q == 4;
     while (rare_lane(w)) {
-        const uint32_t hc = *s.hctl;
-        const uint4 sl = *reinterpret_cast<const uint4*>(s.slot);
+        uint32_t hc;
+        uint4 sl;
+        slot_read(s, hc, sl);
         slot_take(s, sl, hc, w);
         slot_publish(s);
         w = w && s.q == 4;
@@ -181,9 +207,9 @@ DEV uint32_t slot_init(SlotSrc& s, const uint8_t* p, uint32_t len, uint32_t pkt)
     slot_adv0(s, c1);
     slot_fill(s, true);
     slot_adv0(s, c1);
-    s.gen = s.gen % 15u + 1u;
+    s.gen = s.gen % 0xFFFFu + 1u;
     s.want = s.j + 1;
-    *reinterpret_cast<uint2*>(s.mctl) = make_uint2(((s.want & 0xFFFu) << 16) | (s.gen << 28), pkt);
+    *reinterpret_cast<uint2*>(s.mctl) = make_uint2(((s.want & 0xFFFu) << 16) | s.gen, pkt);
     // (settled here: a load pending at the step loop's header makes the compiler
     // wait for vmcnt(0) at every step)
     __builtin_amdgcn_s_waitcnt(0);
@@ -192,11 +218,14 @@ DEV uint32_t slot_init(SlotSrc& s, const uint8_t* p, uint32_t len, uint32_t pkt)
 
 // ------------------------------------------------------------------ helper
 struct SlotHelp {
-    uint32_t have, hgen, cgen, pub, len;
+    uint32_t have, hgen, cgen, pub, len, pkt;
     uintptr_t ib;
 };
 
-DEV void slot_help_init(SlotHelp& h) { h.have = 0; h.hgen = 0; h.cgen = 0; h.pub = 0; h.len = 0; h.ib = 0; }
+DEV void slot_help_init(SlotHelp& h)
+{
+    h.have = 0; h.hgen = 0; h.cgen = 0; h.pub = 0; h.len = 0; h.ib = 0; h.pkt = kNoPktS;
+}
 
 // One pass over the helper's lanes: a new packet's input range, the wanted
 // chunk into the slot, h_ctl.  Returns whether it loaded anything; fin_all:
@@ -206,13 +235,17 @@ DEV bool slot_help_iter(const rc_batch_dev& bt, const uint32_t* mctl, uint32_t* 
 {
     const uint2 m = *reinterpret_cast<const uint2*>(mctl);
     const bool fin = m.y == kFinS;
-    const uint32_t want = (m.x >> 16) & 0xFFFu, mgen = m.x >> 28;
-    const bool np = !fin && m.y != kNoPktS && mgen != h.cgen;
+    const uint32_t want = (m.x >> 16) & 0xFFFu, mgen = m.x & 0xFFFFu;
+    // a new packet: a new generation, or (should the generation have wrapped
+    // round unseen) a new packet index; the chunk held is then forgotten
+    const bool np = !fin && m.y != kNoPktS && (mgen != h.cgen || m.y != h.pkt);
     if (any_lane(np)) {
         if (np) {
             h.len = bt.in_len[m.y];
             h.ib = reinterpret_cast<uintptr_t>(bt.in + bt.in_off[m.y]);
             h.cgen = mgen;
+            h.pkt = m.y;
+            h.hgen = 0;             // (generation 0: no decoder's, slot_init counts from 1)
         }
     }
     const bool inq = !fin && h.cgen != 0 && mgen == h.cgen && (want != h.have || h.hgen != h.cgen);
@@ -225,10 +258,15 @@ DEV bool slot_help_iter(const rc_batch_dev& bt, const uint32_t* mctl, uint32_t* 
         h.have = inq ? want : h.have;
         h.hgen = inq ? h.cgen : h.hgen;
     }
-    const uint32_t hc = (h.have << 16) | (h.hgen << 28);
+    const uint32_t hc = (h.have << 16) | h.hgen;
     if (hc != h.pub) {
-        __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the slot written before the word that announces it
+        // the slot written before the word that announces it (release: the
+        // slot's LDS write completes first, and no store moves past this one)
+#ifndef RC_LANE_HOST_TEST
+        __hip_atomic_store(hctl, hc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
         *hctl = hc;
+#endif
         h.pub = hc;
     }
     fin_all = !any_lane(!fin);

@@ -37,6 +37,39 @@ def shard_ranges(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
+def split_on_device(lengths, offsets, world: int):
+    """shard_ranges computed where the batch lives (the GPU, on the GPU path),
+    with the byte range of each part: ([(a, b)] * world, [(lo, hi)] * world).
+    Only 3 world + 1 integers come back to the host -- not the lengths and
+    offsets arrays.  The same split as enet_rc_multi_split / rc_multi_plan.hip:
+    part k starts at the first packet whose exclusive prefix sum of lengths,
+    times world, reaches total * k."""
+    import torch
+    n = lengths.numel()
+    dev = lengths.device
+    if world <= 1 or n == 0:
+        hi = int((offsets[-1].to(torch.int64) + lengths[-1].to(torch.int64)).item()) if n else 0
+        lo = int(offsets[0].item()) if n else 0
+        return [(0, n)] + [(n, n)] * max(0, world - 1), [(lo, hi)] + [(0, 0)] * max(0, world - 1)
+    ln = lengths.to(torch.int64)
+    excl = torch.cumsum(ln, 0) - ln
+    total = ln.sum()
+    ks = torch.arange(1, world, dtype=torch.int64, device=dev)
+    mid = torch.searchsorted(excl * world, total * ks)            # first index with excl * world >= total * k
+    first = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), mid,
+                       torch.full((1,), n, dtype=torch.int64, device=dev)])
+    a, b = first[:-1], first[1:]
+    last = torch.clamp(b - 1, min=0)
+    off = offsets.to(torch.int64)
+    lo = off[torch.clamp(a, max=n - 1)]
+    hi = off[last] + ln[last]
+    got = torch.cat([first, lo, hi]).cpu().tolist()               # the one read-back
+    f, los, his = got[:world + 1], got[world + 1:2 * world + 1], got[2 * world + 1:]
+    ranges = [(int(f[r]), int(f[r + 1])) for r in range(world)]
+    spans = [(int(los[r]), int(his[r])) if f[r + 1] > f[r] else (0, 0) for r in range(world)]
+    return ranges, spans
+
+
 def _offsets(lengths):
     import torch
     off = torch.zeros_like(lengths, dtype=torch.int64)
@@ -63,15 +96,10 @@ def scatter_batch(dist, data, offsets, lengths, root: int = 0, device=None):
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = device if device is not None else (data.device if data is not None else torch.device("cpu"))
     if rank == root:
-        ln_cpu = lengths.to("cpu")
-        ranges = shard_ranges(ln_cpu.numpy(), world)
-        off_cpu = offsets.to("cpu")
+        ranges, spans = split_on_device(lengths, offsets, world)
         hdrs, parts, keep = [], [], None
         for r, (a, b) in enumerate(ranges):
-            if a < b:
-                lo = int(off_cpu[a]); hi = int(off_cpu[b - 1] + ln_cpu[b - 1])
-            else:
-                lo = hi = 0
+            lo, hi = spans[r]
             ln_r = lengths[a:b].to(device=dev, dtype=torch.int32).contiguous()
             pay = data[lo:hi].to(dev).contiguous()
             if r == root:

@@ -242,16 +242,28 @@ int enet_rc_multi_decompress_batch_host(void *multi, const uint8_t *in, const ui
                                         const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
 /* DEVICE pointers on devices[0]: the split is computed there; every other
  * device's range is copied to it over the peer link (hipMemcpyPeerAsync,
- * xGMI), coded there, packed back to back and copied back, then unpacked into
- * the root's slots (only bytes [out_off[i], +out_len[i]) are written).  The
- * inputs must be complete on the root's null stream (HIP's default stream,
- * which waits for every blocking stream); returns with the results in place. */
+ * xGMI) and coded there, and a copy kernel on the root reads each packet's
+ * produced bytes back into the root's slots over the link (only bytes
+ * [out_off[i], +out_len[i]) are written).  The _stream calls take the
+ * caller's stream on the root (hipStream_t, NULL = the null stream): the
+ * inputs must be complete in its order, and the root's work waits for it
+ * there, not on the host.  The calls without a stream wait for the whole root
+ * device first (any stream's work on the inputs).  Both return with the
+ * results in place. */
 int enet_rc_multi_compress_batch_device(void *multi, const uint8_t *in, const uint64_t *in_off,
                                         const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
                                         const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
 int enet_rc_multi_decompress_batch_device(void *multi, const uint8_t *in, const uint64_t *in_off,
                                           const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
                                           const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len);
+int enet_rc_multi_compress_batch_device_stream(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                               const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                                               const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+                                               void *stream);
+int enet_rc_multi_decompress_batch_device_stream(void *multi, const uint8_t *in, const uint64_t *in_off,
+                                                 const uint32_t *in_len, size_t n, uint32_t max_len, uint8_t *out,
+                                                 const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
+                                                 void *stream);
 
 /* Packs out_len[i] bytes of each packet (at out_off[i]) back to back into
  * packed, on the device (the gather of a batch's results before a copy);
@@ -265,6 +277,15 @@ uint32_t enet_rc_last_exact_count(void *context);
 /* Number of packets of the last batch that the first pass (the two-pass
  * encoder, or the record-light decoder and its check) left to the lane kernels. */
 uint32_t enet_rc_last_lane_count(void *context);
+/* The context's kernel configuration, fixed when it was created (bits: 1 wave
+ * kernel, 2 two-pass encoder, 4 its wide mode, 8 fast decoder, 16 the
+ * encoder's slow paths forced, 8-14 packets per lane-kernel wavefront); bit 31
+ * set if the context that runs the second half of its split host batches was
+ * configured differently (never, by construction). */
+uint32_t enet_rc_config_flags(void *context);
+/* 1 if the last host-pointer batch ran in two halves on two contexts of the
+ * device (large batches: input copies of one half under the other's kernels). */
+uint32_t enet_rc_last_split(void *context);
 /* Library version string. */
 const char *enet_rc_version(void);
 

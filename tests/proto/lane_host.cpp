@@ -1,12 +1,9 @@
 // TEST ONLY: host build of the lane kernels' per-lane compress/decompress
-// (rc_lane3.hip) and, with -DDEC4 / -DDEC6 / -DDEC7, the fast decoder in front of them.
+// (rc_lane3.hip) and, with -DDEC6, the fast decoder in front of them.
 #define RC_LANE_HOST_TEST 1
 #include <stdlib.h>
 #include <string.h>
 #include "../../enet_amd/csrc/rc_lane3.hip"
-#ifdef DEC4
-#include "../../enet_amd/csrc/rc_dec4.hip"
-#endif
 #ifdef DEC6
 #include "../../enet_amd/csrc/rc_dec6.hip"
 static uint8_t g_lds6[528] __attribute__((aligned(16)));   // root + bucket bytes
@@ -52,43 +49,6 @@ static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n, uint32_t rst = 0)
 }
 #endif
 
-#ifdef DEC7
-#ifndef DEC6
-static uint32_t distinct_bigrams(const uint8_t* x, uint32_t n)
-{
-    static uint8_t seen[65536];
-    memset(seen, 0, sizeof seen);
-    uint32_t c = 0;
-    for (uint32_t j = 1; j < n; ++j) {
-        const uint32_t b = (x[j - 1] << 8) | x[j];
-        c += seen[b] ? 0u : 1u;
-        seen[b] = 1;
-    }
-    return c;
-}
-#endif
-#include "../../enet_amd/csrc/rc_dec7.hip"
-// the decoder's two sides for one lane: the main lane runs the packet, and the
-// helper runs one pass after every main step and whenever the main lane waits
-static uint8_t g_lds7[lds7_bytes(1)] __attribute__((aligned(16)));
-static Help7 g_h7;
-static Lds7 g_x7;
-static const rc_batch_dev* g_b7 = nullptr;
-static uint32_t g_kicks7 = 0, g_period7 = 1, g_rng7 = 12345;
-// period p > 1: the helper runs at about one in p of its chances (pseudo-random),
-// so answers, input chunks and ring space arrive late, as on the GPU
-extern "C" void lane_host_dec7_period(uint32_t p) { g_period7 = p ? p : 1; }
-namespace {
-static void dec7_host_kick()
-{
-    ++g_kicks7;
-    bool fin = false;
-    g_rng7 = g_rng7 * 1103515245u + 12345u;
-    if (g_period7 <= 1 || (g_rng7 >> 16) % g_period7 == 0) help7_iter(*g_b7, g_x7, g_h7, fin);
-}
-}  // namespace
-#endif
-
 #define REGION_BYTES rc_hip_lane3_region_bytes
 #define COMPRESS_ONE compress_one3
 #define DECOMPRESS_ONE decompress_one3
@@ -121,14 +81,6 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     ws.claims = claims;
     ws.dec6_resets = resets;
     *out_len = 0xFFFFFFFFu;
-#ifdef DEC4
-    // the bucket-history decoder first; a packet it leaves goes to the lanes (as on the GPU)
-    if (decompress) {
-        uint32_t wbail = 0;
-        decompress_one4(b, ws, 0, region, g_root, &wbail);
-        if (!counters[3]) return 0;
-    }
-#endif
 #ifdef DEC6
     // the record-light decoder and its check; a packet it leaves or that fails the check goes to the lanes
     if (decompress) {
@@ -152,25 +104,7 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
     }
 #endif
 
-#ifdef DEC7
-    // the record-light decoder with its helper, and the check, as on the GPU
-    if (decompress) {
-        g_b7 = &b;
-        g_x7 = lds7(g_lds7, 0, 1);
-        *reinterpret_cast<uint2*>(g_x7.mctl) = make_uint2(0u, kNoPkt7);
-        g_x7.hctl[0] = 0u;
-        help7_init(g_h7);
-        Main7 m = {0u, 0u, 0u};
-        main7_packet(b, ws, 0, g_x7, m);
-        if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len)) {
-            counters[3] = 1; g_dec6_unverified++;
-        }
-        if (!counters[3] && (claims[0] >> 31)) *out_len = 0;
-        if (!counters[3]) return 0;
-    }
-#endif
-
     if (decompress) DECOMPRESS_ONE(b, ws, 0, region, g_root, g_ldsb, g_lc);
     else COMPRESS_ONE(b, ws, 0, region, g_root COMPRESS_ARGS);
-    return counters[0] ? 1 : (counters[3] ? 2 : 0);   // 1 = routed to the exact path, 2 = left by dec4
+    return counters[0] ? 1 : (counters[3] ? 2 : 0);   // 1 = routed to the exact path, 2 = left by the fast decoder
 }

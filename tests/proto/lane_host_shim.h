@@ -1,5 +1,5 @@
 /* TEST ONLY: lets tests/proto/lane_host.cpp compile the per-lane logic of
- * enet_amd/csrc/rc_lane3.hip, rc_dec4.hip, rc_dec6.hip and rc_dec7.hip for the
+ * enet_amd/csrc/rc_lane3.hip and rc_dec6.hip for the
  * host, to check it against the golden fixtures without a GPU.  Never part of
  * the product library. */
 #pragma once

@@ -22,12 +22,6 @@ VARIANTS = {
     # check, its input through LDS slots (rc_dec6.hip rc_decompress_dec6s, rc_slot.h),
     # in front of the v3 lane kernels (rc_lane3.hip)
     "lane3": {"ENET_RC_KERNEL": "lane3"},
-    # rc_dec6.hip loading its own input
-    "dec6": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "6"},
-    # the record-light decoder with helper wavefronts (rc_dec7.hip) instead
-    "dec7": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "7"},
-    # the bucket-history decoder (rc_dec4.hip) in front of the lane kernels instead
-    "dec4": {"ENET_RC_KERNEL": "lane3", "ENET_RC_DEC": "4"},
     # the two-pass encoder's slow paths forced (every position exceptional,
     # every bucket sorted and re-walked: what a device without lane-ordered
     # LDS atomics would take)
@@ -301,7 +295,7 @@ def test_mtu_packets_model_reset_on_fast_decoder(coder):
     pk = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in sizes]
     comp = [port.compress(p, 2 * len(p) + 64)[1] for p in pk]
     back = _run(coder, True, comp, [4096] * len(comp), max_len=max(len(c) for c in comp))
-    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+    if getattr(coder, "variant", "") == "lane3":
         assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
     assert all(b == (len(p), p) for b, p in zip(back, pk))
     # output limits inside the second segment
@@ -327,7 +321,7 @@ def test_mtu_packets_model_reset_on_fast_encoder(coder):
     pk += [rng.integers(0, 40, size=4096, dtype=np.uint8).tobytes() for _ in range(8)]
     caps = [2 * len(p) + 64 for p in pk]
     res = _run(coder, False, pk[:narrow], caps[:narrow])
-    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+    if getattr(coder, "variant", "") == "lane3":
         assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
     res += _run(coder, False, pk[narrow:], caps[narrow:])
     for p, c, r in zip(pk, caps, res):
@@ -400,7 +394,7 @@ def test_check_on_unaligned_outputs_vs_oracle(coder):
     comp = [port.compress(p, 2 * len(p) + 64)[1] for p in pk]
     caps = [len(p) + int(rng.choice([0, 1, 2, 3, 5, 7])) for p in pk]
     back = _run(coder, True, comp, caps)
-    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+    if getattr(coder, "variant", "") == "lane3":
         assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
     assert all(b == (len(p), p) for b, p in zip(back, pk))
     flipped = []
@@ -506,7 +500,13 @@ def test_host_pointer_batches_split(coder):
     clen = np.zeros(n, np.uint32)
     p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
     assert lib.enet_rc_compress_batch_host(coder.ctx, p(d), p(o), p(ln), n, p(cout), p(coff), p(cap), p(clen)) == 0
-    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+    # the batch ran in two halves, the second on a context configured like this one
+    assert lib.enet_rc_last_split(coder.ctx) == 1
+    flags = lib.enet_rc_config_flags(coder.ctx)
+    assert flags & 0x80000000 == 0, hex(flags)
+    assert bool(flags & 2) == (coder.variant != "lane3-only") and bool(flags & 8) == (coder.variant != "lane3-only")
+    assert bool(flags & 16) == (coder.variant == "enc2-slow")
+    if getattr(coder, "variant", "") == "lane3":
         assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
     want, wo, wcap, wl = ocompress(d, o, l, "port")
     assert np.array_equal(clen, wl)
@@ -515,7 +515,8 @@ def test_host_pointer_batches_split(coder):
     dlen = np.zeros(n, np.uint32)
     assert lib.enet_rc_decompress_batch_host(coder.ctx, p(cout), p(coff), p(clen), n, p(dout), p(o), p(ln),
                                              p(dlen)) == 0
-    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+    assert lib.enet_rc_last_split(coder.ctx) == 1
+    if getattr(coder, "variant", "") == "lane3":
         assert coder.last_lane_count() == 0 and coder.last_exact_count() == 0
     assert np.array_equal(dlen, ln)
     assert np.array_equal(dout[: d.size], d)
@@ -535,7 +536,7 @@ def test_host_pointer_batches_split(coder):
     assert lib.enet_rc_decompress_batch_host(coder.ctx, p(gout), p(gcoff), p(glen), gn, p(gback), p(go), p(gln),
                                              p(gblen)) == 0
     assert np.array_equal(gblen, gln) and np.array_equal(gback[: g.size], g)
-    if getattr(coder, "variant", "") in ("lane3", "dec6"):
+    if getattr(coder, "variant", "") == "lane3":
         assert coder.last_lane_count() == gn
 
 

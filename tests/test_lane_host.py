@@ -1,5 +1,5 @@
 """Host (CPU) build of the lane kernels' per-lane logic (enet_amd/csrc/rc_lane3.hip,
-and the bucket-history decoder rc_dec4.hip in front of it, compiled with
+and the record-light decoder rc_dec6.hip in front of it, compiled with
 tests/proto/lane_host_shim.h) against the reference fixtures.
 
 The lane kernel is scalar code per lane, so its model and coder logic can be
@@ -17,23 +17,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "tests", "proto", "liblanehost.so")
 
 
-# v3: the lane kernels alone; v4: the bucket-history decoder (rc_dec4.hip) in front of them;
-# v6: the record-light decoder (rc_dec6.hip) and its check in front of them, as on the GPU;
-# v7: rc_dec7.hip's main side and a scalar restatement of its serving side (run after every
-# main step, or at random late) and the check
-# v6s: rc_dec6.hip with its input through the LDS slot (rc_slot.h; the helper run after every step)
-@pytest.fixture(scope="module", params=["v3", "v4", "v6", "v6s", "v7"])
+# v3: the lane kernels alone;
+# v6: the record-light decoder (rc_dec6.hip) and its check in front of them, loading its own input;
+# v6s: rc_dec6.hip with its input through the LDS slot (rc_slot.h; the helper run after every
+# step), as on the GPU
+@pytest.fixture(scope="module", params=["v3", "v6", "v6s"])
 def lane(request):
     so = SO.replace("liblanehost", "liblanehost" + request.param[1:])
     csrc = os.path.join(ROOT, "enet_amd", "csrc")
     src = [os.path.join(ROOT, "tests", "proto", "lane_host.cpp")] + \
-        [os.path.join(csrc, f) for f in ("rc_lane3.hip", "rc_dec4.hip", "rc_dec6.hip", "rc_dec7.hip", "rc_dec6_rare.h",
-                                         "rc_slot.h", "rc_bucket4.h",
-                                         "rc_lane_common.h", "rc_root3.h")]
+        [os.path.join(csrc, f) for f in ("rc_lane3.hip", "rc_dec6.hip", "rc_dec6_rare.h",
+                                         "rc_slot.h", "rc_lane_common.h", "rc_root3.h")]
     if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in src):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared"] +
-                              {"v3": [], "v4": ["-DDEC4"], "v6": ["-DDEC6"], "v6s": ["-DDEC6", "-DDEC6S"],
-                               "v7": ["-DDEC7"]}[request.param] +
+                              {"v3": [], "v6": ["-DDEC6"], "v6s": ["-DDEC6", "-DDEC6S"]}[request.param] +
                               ["-I", csrc, "-I", os.path.join(ROOT, "tests", "proto"), "-o", so, src[0]])
     lib = C.CDLL(so)
     lib.lane_host_run.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
@@ -82,16 +79,16 @@ def test_lane_logic_decompress_fixtures(lane):
         if c["ret"]:
             assert r[1] == c["expect"]
     assert 0 < exact < 2000
-    if lane.version in ("v4", "v6", "v6s", "v7"):     # most fixtures are garbage or low-entropy: those are left to the lanes
+    if lane.version in ("v6", "v6s"):     # most fixtures are garbage or low-entropy: those are left to the lanes
         assert 0 < lane.left < len(cases) - 1000, (lane.left, len(cases))
 
 
-def test_dec4_takes_random_packets(lane):
-    """The bucket-history decoder (and the record-light one) decodes random
-    packets up to MTU size itself (no bucket reaches its limits) and matches
-    the oracle at every output limit edge."""
+def test_dec6_takes_random_packets(lane):
+    """The record-light decoder decodes random packets up to MTU size itself
+    (no bucket reaches its limits) and matches the oracle at every output
+    limit edge."""
     if lane.version == "v3":
-        pytest.skip("dec4 / dec6 only")
+        pytest.skip("dec6 only")
     from oracle.pyoracle import Coder
     port = Coder("port")
     rng = np.random.default_rng(11)
@@ -187,39 +184,3 @@ def test_lane_logic_dense_order2_contexts(lane):
         ref = port.compress(p, out_limit=cap)
         assert lane(0, p, cap, max_len=len(p)) == ref
         assert lane(1, ref[1], len(p), max_len=len(p)) == (len(p), p)
-
-
-@pytest.mark.parametrize("period", [2, 7])
-def test_dec7_late_helper(lane, period):
-    """rc_dec7.hip with its helper running at one in `period` of its chances:
-    answers, input chunks and ring space come late (lanes keep waiting, the
-    ring fills up), and the decode must not change.  Random, low-entropy and
-    corrupt streams against the oracle."""
-    if lane.version != "v7":
-        pytest.skip("dec7 only")
-    from enet_amd import synth
-    from oracle.pyoracle import Coder
-    port = Coder("port")
-    lib = lane.lib
-    lib.lane_host_dec7_period(period)
-    try:
-        rng = np.random.default_rng(40 + period)
-        pk = [rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 1393, size=30)]
-        pk += [rng.integers(0, 6, size=900, dtype=np.uint8).tobytes(), bytes(1000)]
-        d, o, l = synth.gamestate_batch(3, 1200)
-        pk += [d[int(o[i]): int(o[i]) + 1200].tobytes() for i in range(3)]
-        valid_left = 0
-        for p in pk:
-            r, c = port.compress(p, 2 * len(p) + 64)
-            lane.left = 0
-            for lim in (len(p), 4096):
-                assert lane(1, c, lim) == port.decompress(c, lim), (len(p), lim)
-            valid_left += lane.left
-            bad = bytearray(c)
-            bad[len(bad) // 2] ^= 0x5A
-            got = lane(1, bytes(bad), 4096)
-            if got[0] != "exact":    # (the exact path, not built here, takes root codes past symbol 255)
-                assert got == port.decompress(bytes(bad), 4096)
-        assert valid_left <= 2 * 5, valid_left     # (only the low-entropy packets may leave)
-    finally:
-        lib.lane_host_dec7_period(1)

@@ -1,9 +1,11 @@
 """One process, several GPUs through the C ABI (enet_rc_multi_*, rc_multi.c;
 SURVEY.md §8e).  CPU: the split against enet_amd/shard.py's ranges.  GPU:
-bit-exact results against the oracle with the device lists [0] (one device)
-and [0, 0, 0] (three contexts on the one GPU of the test box: the non-root
-ranges take the whole scatter / code / pack / gather / unpack path of a
-multi-GPU node, over a same-device "peer" copy)."""
+bit-exact results against the oracle with the device lists [0] (one device),
+[0, 0, 0] (three contexts on the one GPU of the test box: the non-root ranges
+take the whole scatter / code / gather path of a multi-GPU node, over a
+same-device "peer" copy and the root's direct read of the device's slots) and
+[0, 0] with a batch whose second range is empty.  Multi-GPU scaling itself is
+unmeasured here (one GPU per test box)."""
 import numpy as np
 import pytest
 
@@ -63,6 +65,28 @@ def test_plan_host_mirror(n, parts):
     z = np.zeros(n, np.uint32)           # no payload: every split point 0
     got = multi_plan(z, ioff, ooff, cap, parts)
     assert [int(x) for x in got[:parts]] == [0] * parts and int(got[parts]) == n
+
+
+@pytest.mark.parametrize("n,parts", [(0, 2), (1, 1), (1, 5), (7, 8), (1000, 3), (5000, 64), (70000, 8)])
+def test_shard_split_on_device_mirror(n, parts):
+    """shard.split_on_device (the split shard.scatter_batch computes where the
+    batch lives, CPU tensors here) against shard_ranges and the C split, with
+    unequal lengths, zero-length packets, and parts left empty"""
+    torch = pytest.importorskip("torch")
+    ln, ioff, ooff, cap = _plan_case(n, n * 5 + parts)
+    for lens in (ln, np.zeros(n, np.uint32), np.where(np.arange(n) == n - 1, 1000, 0).astype(np.uint32)):
+        off = np.zeros(n, np.int64)
+        if n > 1:
+            off[1:] = np.cumsum(lens[:-1].astype(np.int64))
+        ranges, spans = shard.split_on_device(torch.from_numpy(lens.astype(np.int32)), torch.from_numpy(off), parts)
+        assert ranges == shard.shard_ranges(lens, parts)
+        if n:
+            assert [a for a, _ in ranges] + [n] == [int(x) for x in multi_split(lens, parts)]
+        for (a, b), (lo, hi) in zip(ranges, spans):
+            if a < b:
+                assert (lo, hi) == (int(off[a]), int(off[b - 1] + lens[b - 1]))
+            else:
+                assert (lo, hi) == (0, 0)
 
 
 @pytest.mark.gpu
@@ -150,4 +174,43 @@ def test_multi_device_batches_vs_oracle(devices):
     m.batch_device(True, cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
     assert torch.equal(dl, dlen)
     assert torch.equal(dout, din)
+    m.close()
+
+
+@pytest.mark.gpu
+def test_multi_device_empty_range_and_stream():
+    """[0, 0] with every payload byte in the last packet: the second device's
+    range is empty (the plan's split puts all packets on the root).  Then a
+    batch whose inputs are written on a side stream: the root waits for that
+    stream (the _stream entry), not for the null stream."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from enet_amd import MultiCoder
+    from oracle.pyoracle import compress_batch as ocompress, fnv_digest
+    n = 3000
+    rng = np.random.default_rng(77)
+    ln = np.zeros(n, np.uint32)
+    ln[-1] = 1200
+    d = rng.integers(0, 256, size=1200, dtype=np.uint8)
+    o = np.full(n, 0, np.uint64)
+    first = multi_split(ln, 2)
+    assert int(first[1]) == n - 1 or int(first[1]) == n          # one part holds every packet with payload
+    dev = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
+    m = MultiCoder([0, 0])
+    for side in (False, True):
+        s = torch.cuda.Stream() if side else torch.cuda.current_stream()
+        with torch.cuda.stream(s):
+            din, doff, dlen = dev(d, torch.uint8), dev(o, torch.int64), dev(ln, torch.int32)
+            cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+            coff = torch.zeros(n, dtype=torch.int64, device="cuda")
+            coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+            cout = torch.zeros(int(coff[-1] + cap[-1]), dtype=torch.uint8, device="cuda")
+            clen = torch.full((n,), 77, dtype=torch.int32, device="cuda")
+            m.batch_device(False, din, doff, dlen, cout, coff, cap, clen, max_len=1200)
+        torch.cuda.synchronize()
+        want, wo, wcap, wl = ocompress(d, o, ln, "port")
+        cl = clen.cpu().numpy().astype(np.uint32)
+        assert np.array_equal(cl, wl)
+        assert fnv_digest(cout.cpu().numpy(), coff.cpu().numpy().astype(np.uint64), cl) == fnv_digest(want, wo, wl)
     m.close()
