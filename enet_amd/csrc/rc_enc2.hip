@@ -639,8 +639,7 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
         const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
         const uint32_t mx = max(max(c4.x, c4.y), max(c4.z, c4.w));
         if (any_lane(mx > kE2Bucket)) {
-            if (len > kE2MaxLen) fb_add(s, e, slot, pkt, t);     // (the wide kernels do not reset)
-            else big_add(s, e, slot, pkt, idx, t);
+            big_add(s, e, slot, pkt, idx, t);            // (the wide kernels reset as this scan does)
             if (!fetched) pf = scan_prefetch(b, e, idx + gridDim.x);
             break;
         }
@@ -1410,17 +1409,31 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
 
 constexpr uint32_t kWideDense = 32;             // runs longer than this take a dense walk
 
+// Wide element word: pos (0-11) | v (12-19) | a | 256 (20-28, 0 for position 1).
+// (12 bits of position: model segments of up to 4096 positions, rc_enc2_wscan_l.)
+constexpr uint32_t kWPos = 4095u, kWV = 12, kWA = 20, kWHas = 256u << kWA;
+DEV uint32_t wv_of(uint32_t w) { return (w >> kWV) & 255; }
+DEV uint32_t wa_of(uint32_t w) { return (w >> kWA) & 255; }
+// wide record, w word (half B): totalB | B coded << 16 | root codes << 17 |
+// model reset before this position << 18 (compress.c:148-157, the first position
+// of a segment after the first) | packet left to the lane kernels << 19 (position 0)
+constexpr uint32_t kWRst = 1u << 18, kWLeft = 1u << 19;
+constexpr uint32_t kWideLong = 4096;           // rc_enc2_wscan_l: segments of up to this many positions
+
 // L: the longest packet of the launch (its positions); two sizes are built,
 // 2048 and 1216 -- the smaller one leaves room for 9 wavefronts per CU
 // instead of 6 (the scan is latency-bound: LDS and ballots)
 template <uint32_t L>
 struct WScanLdsT {
-    uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i]; then a big bucket's run sizes / starts
+    // the window's bytes at x[16 + mis + i]; then a big bucket's run sizes / starts (2 KB)
+    uint8_t  x[L <= 2048 ? 16 + 2048 + 16 : 16 + L + 16];
     uint32_t cnt[256];                // bucket sizes, then fill pointers
     uint32_t start[256];              // bucket starts (4-aligned)
-    uint32_t e[L + 768];              // elements in bucket order (element word as in pass 1)
+    uint32_t e[L + 768];              // elements in bucket order (wide element words)
     uint32_t sw[L];                   // a big bucket's element words by a, then its order-1 visits
-    uint32_t f2bits[64];              // positions found at order 2 (big buckets)
+    uint32_t f2bits[L / 32];          // positions found at order 2 (big buckets; every bucket in a
+                                      // packet that can reach the model reset)
+    uint32_t rootbits[L / 32];        // ... positions coded at the root (a packet that can reset)
     uint32_t tab[64];                 // dense walk: a round's updated counts (256 bytes); rank counts
     uint32_t runs[64];                // a big bucket's long runs (a keys)
     uint32_t nruns;
@@ -1524,7 +1537,7 @@ DEV uint2 closed_code(uint32_t t, uint32_t dist, uint32_t same, uint32_t less)
     return make_uint2(kNoCodeLo, kNoCodeTot);
 }
 
-DEV uint32_t akey_of(uint32_t w) { return (w & (256u << 19)) ? (w >> 19) & 511 : 1024u; }   // 1024: none (position 1)
+DEV uint32_t akey_of(uint32_t w) { return (w & kWHas) ? (w >> kWA) & 511 : 1024u; }   // 1024: none (position 1)
 
 // Buckets of <= kE2Bucket elements, whole buckets per round: a window of 64
 // element slots starting at a bucket start takes every bucket that ends inside
@@ -1538,7 +1551,7 @@ DEV uint32_t akey_of(uint32_t w) { return (w & (256u << 19)) ? (w >> 19) & 511 :
 // found2 of every lane is known at once (an earlier lane with the same a and
 // v), so nothing runs lane after lane.
 template <class S>
-DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
+DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec, bool track)
 {
     const uint32_t t = lane_id();
     const uint64_t below = below_mask();
@@ -1556,7 +1569,7 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
         const bool pad = w == kPadWord;
         uint32_t bs = 0, be = 0, p = 0;
         if (!pad) {
-            p = s.x[q0 + (w & 2047) - 1];
+            p = s.x[q0 + (w & kWPos) - 1];
             bs = s.start[p];
             be = s.cnt[p];
         }
@@ -1574,8 +1587,8 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
         }
         const uint64_t am = __builtin_amdgcn_ballot_w64(act);
         if (am) {
-            const uint32_t v = (w >> 11) & 255, a = (w >> 19) & 255;
-            const bool has = (w & (256u << 19)) != 0;
+            const uint32_t v = wv_of(w), a = wa_of(w);
+            const bool has = (w & kWHas) != 0;
             const KeyBits kv = key_bits(v);
             // my bucket: its elements are lanes [bs - W, be - W) of the window
             // (buckets are contiguous in e[], and an active one lies inside it)
@@ -1603,8 +1616,13 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec)
             const uint32_t less1 = popc64(ltv & vis1 & below);
             const bool f1 = act && !f2 && (same1m & below) != 0;
             const uint64_t F1 = __builtin_amdgcn_ballot_w64(f1);
+            if (track && act) {                       // (the model reset's node count: wreset_after)
+                const uint32_t pos = w & kWPos;
+                if (f2) atomicOr(&s.f2bits[pos >> 5], 1u << (pos & 31));
+                if (!f2 && !f1) atomicOr(&s.rootbits[pos >> 5], 1u << (pos & 31));
+            }
             if (act) {
-                const uint32_t pos = w & 2047;
+                const uint32_t pos = w & kWPos;
                 const uint2 ca = closed_code(t2, dist2, same2, less2);
                 wrec[2 * pos] = make_uint2(ca.x, ca.y | v << 16);
                 if (f2) {
@@ -1635,7 +1653,7 @@ DEV void wide_short_runs(S& s, uint32_t ks, const uint32_t* hist, const uint32_t
         const uint32_t j = W + t;
         const bool in = j < ks;
         const uint32_t w = s.sw[in ? j : ks - 1];
-        const uint32_t a = (w >> 19) & 255, v = (w >> 11) & 255;
+        const uint32_t a = wa_of(w), v = wv_of(w);
         const uint32_t re = rend[a], rs = re - hist[a];
         const bool act = in && re <= W + 64;
         const uint64_t nt = __builtin_amdgcn_ballot_w64(in && !act);
@@ -1649,7 +1667,7 @@ DEV void wide_short_runs(S& s, uint32_t ks, const uint32_t* hist, const uint32_t
         const bool f2 = act && (samem & below) != 0;
         const uint64_t F2 = __builtin_amdgcn_ballot_w64(f2);
         if (act) {
-            const uint32_t pos = w & 2047;
+            const uint32_t pos = w & kWPos;
             const uint2 c = closed_code(popc64(ctx & below), popc64(ctx & below & ~F2), popc64(samem & below), less);
             wrec[2 * pos] = make_uint2(c.x, c.y | v << 16);
             if (f2) {
@@ -1677,7 +1695,7 @@ DEV uint32_t nonzero_bytes(uint32_t x)
 // position's order-2 hit bit and closes half B; else half B with the root
 // flag.
 template <class S>
-DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, uint2* wrec)
+DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, uint2* wrec, bool track = false)
 {
     const uint32_t t = lane_id();
     uint8_t* sc = reinterpret_cast<uint8_t*>(s.tab);   // a round's final counts of its symbols (0: untouched)
@@ -1690,7 +1708,7 @@ DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, ui
         const uint32_t j = base + t;
         const bool act = j < m;
         const uint32_t w = list[act ? j : m - 1];
-        const uint32_t pos = w & 2047, v = (w >> 11) & 255;
+        const uint32_t pos = w & kWPos, v = wv_of(w);
         const uint32_t dw = __shfl(tabr, static_cast<int>(v >> 2), 64);
         const uint32_t pd = __shfl(pre, static_cast<int>(v >> 2), 64);
         const uint32_t sh = 8 * (v & 3);
@@ -1726,6 +1744,7 @@ DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, ui
             } else {
                 const bool coded = hit || esc_l != 0;
                 wrec[2 * pos + 1] = make_uint2(code.x, code.y | (coded ? 1u << 16 : 0u) | (hit ? 0u : 1u << 17));
+                if (track && !hit) atomicOr(&s.rootbits[pos >> 5], 1u << (pos & 31));
             }
         }
         // the table: the last committed visit of each symbol posts its count,
@@ -1762,7 +1781,7 @@ DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, ui
 // a big bucket of a wide packet (> kE2Bucket elements, [bs, bs + k) in
 // position order), the whole wavefront
 template <class S>
-DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp, bool ordered)
+DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp, bool ordered, bool track)
 {
     const uint32_t t = lane_id();
     uint32_t* hist = reinterpret_cast<uint32_t*>(s.x);          // [256] run sizes by a
@@ -1775,9 +1794,9 @@ DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp,
     for (uint32_t q = 0; q < k; q += 64) {
         const bool ok0 = q + t < k;
         const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
-        const bool has = (w & (256u << 19)) != 0;
-        if (ok0 && has) atomicAdd(&hist[(w >> 19) & 255], 1u);
-        if (ok0 && !has) wrec[2 * (w & 2047)] = make_uint2(kNoCodeLo, kNoCodeTot | ((w >> 11) & 255) << 16);
+        const bool has = (w & kWHas) != 0;
+        if (ok0 && has) atomicAdd(&hist[wa_of(w)], 1u);
+        if (ok0 && !has) wrec[2 * (w & kWPos)] = make_uint2(kNoCodeLo, kNoCodeTot | (wv_of(w)) << 16);
     }
     wave_sync();
     uint32_t ks;
@@ -1803,12 +1822,12 @@ DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp,
     for (uint32_t q = 0; q < k; q += 64) {
         const bool ok0 = q + t < k;
         const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
-        const bool has = ok0 && (w & (256u << 19)) != 0;
+        const bool has = ok0 && (w & kWHas) != 0;
         uint32_t rk = 0;
         if (ordered) {
-            if (has) rk = atomicAdd(&rst[(w >> 19) & 255], 1u);     // (lane order: see wscan_main)
+            if (has) rk = atomicAdd(&rst[wa_of(w)], 1u);     // (lane order: see wscan_main)
         } else {
-            rk = group_add<true>(rst, (w >> 19) & 255, has);
+            rk = group_add<true>(rst, wa_of(w), has);
         }
         if (has) s.sw[rk] = w;
     }
@@ -1838,7 +1857,7 @@ DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp,
     for (uint32_t q = 0; q < k; q += 64) {
         const bool ok0 = q + t < k;
         const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
-        const uint32_t pos = w & 2047;
+        const uint32_t pos = w & kWPos;
         const bool vis = ok0 && !bit_at(s.f2bits, pos);
         const uint64_t vm = __builtin_amdgcn_ballot_w64(vis);
         if (vis) s.sw[m1 + popc64(vm & below_mask())] = w;
@@ -1846,7 +1865,7 @@ DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp,
     }
     wave_sync();
     W2P(8)
-    wide_dense_walk(s, s.sw, m1, false, wrec);
+    wide_dense_walk(s, s.sw, m1, false, wrec, track);
     wave_sync();
     W2P(9)
 }
@@ -1880,6 +1899,73 @@ DEV WPf wide_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t q, uint
     return f;
 }
 
+// The nodes compress.c creates at each position of a wide window scanned as
+// a model segment (as reset_after for the narrow scan, compress.c:68-88 via
+// :286-337): position 0 the root's; a position coded at the root creates the
+// root's node at its byte's first root visit, its order-1 node (position >= 1)
+// and its order-2 node (>= 2); an order-1 hit its order-2 node (>= 2); an
+// order-2 hit none.  The walks' f2bits / rootbits say which.  Returns the
+// window position after whose byte the count reaches 4094 (compress.c:148-157),
+// or n.  After the walks; s.sw and s.cnt are reused.
+template <uint32_t L, class S>
+DEV uint32_t wreset_after(S& s, uint32_t n, uint32_t total, uint32_t x0, uint32_t t)
+{
+    uint8_t* inc = reinterpret_cast<uint8_t*>(s.sw);     // per position: nodes | 0x80 = root visit
+    uint32_t* first = s.cnt;                             // the first root visit per byte value
+    *reinterpret_cast<uint4*>(&first[4 * t]) = make_uint4(~0u, ~0u, ~0u, ~0u);
+    wave_sync();
+    if (t == 0) { first[x0] = 0u; inc[0] = 1; }
+#pragma unroll 1
+    for (uint32_t k = t; k < total; k += kScanThreads) {
+        const uint32_t w = s.e[k];
+        if (w == kPadWord) continue;
+        const uint32_t pos = w & kWPos;
+        const bool rv = bit_at(s.rootbits, pos), f2 = bit_at(s.f2bits, pos);
+        const uint32_t c = rv ? (pos >= 1 ? 1u : 0u) + (pos >= 2 ? 1u : 0u) : (f2 ? 0u : (pos >= 2 ? 1u : 0u));
+        inc[pos] = static_cast<uint8_t>(c | (rv ? 0x80u : 0u));
+        if (rv) atomicMin(&first[wv_of(w)], pos);
+    }
+    wave_sync();
+#pragma unroll 1
+    for (uint32_t k = t; k < total; k += kScanThreads) {
+        const uint32_t w = s.e[k];
+        if (w == kPadWord) continue;
+        const uint32_t pos = w & kWPos;
+        if (bit_at(s.rootbits, pos) && first[wv_of(w)] == pos) inc[pos] = static_cast<uint8_t>(inc[pos] + 1);
+    }
+    wave_sync();
+    // positions C t .. C t + C - 1: their sum, the prefix over the lanes, the first crossing
+    constexpr uint32_t C = (L + kScanThreads - 1) / kScanThreads;
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t q = 0; q < C; ++q) {
+        const uint32_t pos = C * t + q;
+        sum += pos < n ? (inc[pos] & 0x7Fu) : 0u;
+    }
+    uint32_t acc = 1 + wave_incl_scan(sum) - sum;        // nodes before position C t (the root: 1)
+    uint32_t hit = n;
+    if (acc + sum >= kMaxNodesE2) {
+#pragma unroll 1
+        for (uint32_t q = 0; q < C; ++q) {
+            const uint32_t pos = C * t + q;
+            if (pos >= n) break;
+            acc += inc[pos] & 0x7Fu;
+            if (acc >= kMaxNodesE2) { hit = pos; break; }
+        }
+    }
+    const uint64_t m = __builtin_amdgcn_ballot_w64(hit < n);
+    const uint32_t r = m ? __builtin_amdgcn_readlane(hit, static_cast<uint32_t>(__builtin_ctzll(m))) : n;
+    wave_sync();
+    return r;
+}
+
+// A listed packet is taken in windows (as scan_main's): each window is a
+// model segment scanned as a packet of its own, up to L positions; when the
+// packet can reach compress.c's reset (> 1919 bytes) the nodes its positions
+// create give the byte after which the model resets, and the next window
+// starts after it, its position-0 record flagged kWRst (the code pass clears
+// its root there).  A segment longer than the LDS layout holds (L positions)
+// leaves the packet to the lane kernels (kWLeft in its first record).
 template <uint32_t L>
 DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
 {
@@ -1899,12 +1985,34 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
     WPf pf = wide_prefetch(b, e, blockIdx.x, nw);
     for (uint32_t q = blockIdx.x; q < nw; q += gridDim.x) {
         const WPf cur = pf;
-        const uint32_t n = cur.n, mis = cur.mis;      // (1 <= n <= slot_len: rc_enc2_scan)
-        uint2* wrec = reinterpret_cast<uint2*>(e.wide + static_cast<size_t>(q) * e.wslot_bytes);
+        const uint32_t len = cur.n;                   // (1 <= len <= slot_len: rc_enc2_scan)
+        uint2* wrec0 = reinterpret_cast<uint2*>(e.wide + static_cast<size_t>(q) * e.wslot_bytes);
+        const bool track = len > kE2MaxLen;           // (wave-uniform) the model can reset
+        uint32_t s0 = 0, mis = cur.mis;
+        uintptr_t src0 = 0;
+        if (len + mis > 2048 || track) {
+            const uint32_t idx = const_load(e.wlist, q);
+            src0 = reinterpret_cast<uintptr_t>(b.in + const_load(b.in_off, packet_of(e, idx)));
+        }
+        bool fetched = false;
+#pragma unroll 1
+        for (;;) {
+        const uint32_t n = min(len - s0, L);         // the window: positions s0 .. s0 + n - 1
+        uint2* wrec = wrec0 + 2 * s0;
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
-        if (t < 16) *reinterpret_cast<uint4*>(&s.f2bits[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = cur.r0;
-        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = cur.r1;
+        for (uint32_t k = t; k < L / 32; k += kScanThreads) { s.f2bits[k] = 0u; s.rootbits[k] = 0u; }
+        if (s0 == 0) {
+            *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = cur.r0;
+            *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = cur.r1;
+        }
+        if (s0 > 0 || n + mis > 2048) {
+            // the window's bytes past the prefetched 2 KB (or a later window's): aligned 16-B chunks
+            const uintptr_t a16 = (src0 + s0) & ~static_cast<uintptr_t>(15);
+            const uint32_t last = (mis + n - 1) >> 4;
+#pragma unroll 1
+            for (uint32_t c = (s0 > 0 ? 0u : 2u * kScanThreads) + t; c <= last; c += kScanThreads)
+                *reinterpret_cast<uint4*>(s.x + 16 + 16 * c) = gload16(a16 + 16 * c);
+        }
         wave_sync();
         W2P(0)
         const uint32_t q0 = 16 + mis;
@@ -1947,7 +2055,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
                 const uint32_t b3 = bytes3(s.x, q0 + max(ii, 2u));   // (position 1: its a byte unused)
                 p[h] = s.x[q0 + ii - 1];
                 const uint32_t v = s.x[q0 + ii];
-                w[h] = ii | v << 11 | (ii >= 2 ? ((b3 & 255) | 256u) << 19 : 0u);
+                w[h] = ii | v << kWV | (ii >= 2 ? ((b3 & 255) | 256u) << kWA : 0u);
             }
 #pragma unroll
             for (uint32_t h = 0; h < 2; ++h) {
@@ -1962,10 +2070,11 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         }
         const uint32_t x0 = s.x[q0];
         wave_sync();
-        pf = wide_prefetch(b, e, q + gridDim.x, nw);  // (the next packet, while this one is walked)
+        if (!fetched) pf = wide_prefetch(b, e, q + gridDim.x, nw);  // (the next packet, while this one is walked)
+        fetched = true;
         W2P(3)
         // buckets of <= kE2Bucket elements, whole buckets per round
-        wide_small_buckets(s, q0, total, wrec);
+        wide_small_buckets(s, q0, total, wrec, track);
         wave_sync();
         W2P(4)
         // big ones: the wavefront, one at a time
@@ -1980,16 +2089,33 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
             for (uint32_t r = 0; r < 4; ++r) {
                 if (!((bm >> r) & 1u)) continue;
                 const uint32_t bk = 4 * ld + r;
-                wide_big_bucket(s, s.start[bk], s.cnt[bk] - s.start[bk], wrec, wp, ordered);
+                wide_big_bucket(s, s.start[bk], s.cnt[bk] - s.start[bk], wrec, wp, ordered, track);
             }
             bl &= bl - 1;
         }
-        if (t == 0) {                                 // position 0: root only
+        if (t == 0) {                                 // position 0: root only (after a reset: the root cleared)
             wrec[0] = make_uint2(kNoCodeLo, kNoCodeTot | x0 << 16);
-            wrec[1] = make_uint2(kNoCodeLo, kNoCodeTot | 1u << 17);
+            wrec[1] = make_uint2(kNoCodeLo, kNoCodeTot | 1u << 17 | (s0 ? kWRst : 0u));
         }
         wave_sync();
         W2P(10)
+        if (!track) break;                            // (no reset: <= 2 * 1918 + 256 nodes, compress.c:150)
+        const uint32_t r = wreset_after<L>(s, n, total, x0, t);
+        if (r >= n) {                                 // no reset in the window
+            if (s0 + n < len) {
+                // a model segment longer than the window: the lane kernels take the packet
+                if (t == 0) {
+                    wrec0[1] = make_uint2(kNoCodeLo, kNoCodeTot | 1u << 17 | kWLeft);
+                    e.list[atomicAdd(e.count, 1u)] = packet_of(e, const_load(e.wlist, q));
+                }
+            }
+            break;
+        }
+        s0 += r + 1;
+        if (s0 >= len) break;                         // (the reset after the last byte changes nothing)
+        mis = static_cast<uint32_t>((src0 + s0) & 15);
+        wave_sync();
+        }
     }
     W2P_FLUSH
 }
@@ -2009,6 +2135,15 @@ void rc_enc2_wscan_s(rc_batch_dev b, E2Params e)
     wscan_main<kWideSmallL>(b, e, s);
 }
 
+// ... and for launches with packets over 2048 bytes: model segments of up to
+// kWideLong positions (43 KB of LDS: 3 wavefronts per CU)
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_wscan_l(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) WScanLdsT<kWideLong> s;
+    wscan_main<kWideLong>(b, e, s);
+}
+
 // ---- wide code pass: rc_enc2_code over explicit records
 DEV Pre prep_wide(const uint4& r, bool en)
 {
@@ -2022,13 +2157,25 @@ DEV Pre prep_wide(const uint4& r, bool en)
     p.u2 = p.e2 ? r.z & 0xFFFF : 0u;
     p.c2 = p.e2 ? r.z >> 16 : 1u;
     p.r2 = rcp64(p.e2 ? r.w & 0xFFFF : 1u);
+    p.rst = en && (r.w & kWRst) != 0;
     return p;
 }
 
-// code_step with the next position's wide record
+// code_step with the next position's wide record.  RST: the batch has packets
+// that can reach the model reset (compress.c:148-157): a position flagged
+// kWRst starts a new segment, its root cleared first.
+template <bool RST>
 DEV void wcode_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, const uint8_t* itab, Pre& p,
                     const uint4& nx, bool enn, uintptr_t dummy)
 {
+    if (RST && any_lane(p.rst)) {
+        if (p.rst) {
+            Root R;
+            root3_clear<true>(root, R);
+            k.rtot = 1 + 256;
+            k.rrt = rcp64(k.rtot);
+        }
+    }
     const uint32_t n0 = o.n;
     uint32_t under0, cnt0;
     root3_lookup(root, mtab, p.v, under0, cnt0);
@@ -2054,8 +2201,8 @@ DEV void wcode_step(CodeState& k, Ring& o, uint8_t* root, const uint8_t* mtab, c
     p = q;
 }
 
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
-void rc_enc2_wcode(rc_batch_dev b, E2Params e)
+template <bool RST>
+DEV void wcode_main(const rc_batch_dev& b, const E2Params& e)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint8_t* mtab = smem + kCodeMtab;
@@ -2068,7 +2215,7 @@ void rc_enc2_wcode(rc_batch_dev b, E2Params e)
     if (blockIdx.x * 256 >= nw) return;               // (wave-uniform for whole blocks)
     const bool live = q < nw;
     const uint32_t pkt = live ? packet_of(e, e.wlist[q]) : 0u;
-    const uint32_t len = live ? b.in_len[pkt] : 0u;
+    const uint32_t len0 = live ? b.in_len[pkt] : 0u;
     const uintptr_t base = reinterpret_cast<uintptr_t>(e.wide) + static_cast<size_t>(live ? q : 0u) * e.wslot_bytes;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(e.dummy) + ((blockIdx.x * 256u + threadIdx.x) & 65535u) * 16u;
     uint8_t* root = smem + threadIdx.x * kCodeLds;
@@ -2090,22 +2237,25 @@ void rc_enc2_wcode(rc_batch_dev b, E2Params e)
     // positions ahead) right after its position is prepared
     uint4 c0 = gload16(base), c1 = gload16(base + 16), c2 = gload16(base + 32), c3 = gload16(base + 48);
     __builtin_amdgcn_s_waitcnt(0);
+    // a packet the wide scan left to the lane kernels (a model segment past its LDS): nothing here
+    const bool left = RST && live && (c0.w & kWLeft) != 0;
+    const uint32_t len = left ? 0u : len0;
     Pre p = prep_wide(c0, 0 < len);
     c0 = gload16(base + 64);
     uintptr_t a = base + 80;
     for (uint32_t i = 0; any_lane(i < len && o.n <= o.cap); i += 4, a += 64) {
-        wcode_step(k, o, root, mtab, itab, p, c1, i + 1 < len, dummy);
+        wcode_step<RST>(k, o, root, mtab, itab, p, c1, i + 1 < len, dummy);
         c1 = gload16(a);
-        wcode_step(k, o, root, mtab, itab, p, c2, i + 2 < len, dummy);
+        wcode_step<RST>(k, o, root, mtab, itab, p, c2, i + 2 < len, dummy);
         c2 = gload16(a + 16);
-        wcode_step(k, o, root, mtab, itab, p, c3, i + 3 < len, dummy);
+        wcode_step<RST>(k, o, root, mtab, itab, p, c3, i + 3 < len, dummy);
         c3 = gload16(a + 32);
-        wcode_step(k, o, root, mtab, itab, p, c0, i + 4 < len, dummy);
+        wcode_step<RST>(k, o, root, mtab, itab, p, c0, i + 4 < len, dummy);
         c0 = gload16(a + 48);
     }
     ring_store(o);
     ring_chunk(o, o.n, dummy);
-    bool ok = live && o.n <= o.cap;
+    bool ok = live && !left && o.n <= o.cap;
     uint32_t low = k.low;
     while (any_lane(ok && low != 0)) {
         const bool more = ok && low != 0;
@@ -2118,8 +2268,15 @@ void rc_enc2_wcode(rc_batch_dev b, E2Params e)
         ring_store(o);
     }
     ring_finish(o, ok);
-    if (live) b.out_len[pkt] = ok ? o.n : 0u;
+    if (live && !left) b.out_len[pkt] = ok ? o.n : 0u;
 }
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void rc_enc2_wcode(rc_batch_dev b, E2Params e) { wcode_main<false>(b, e); }
+
+// launches with packets over 1919 bytes: model resets (kWRst) and left packets (kWLeft)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void rc_enc2_wcode_r(rc_batch_dev b, E2Params e) { wcode_main<true>(b, e); }
 
 }  // namespace
 
@@ -2146,7 +2303,7 @@ extern "C" uint64_t rc_hip_enc2_slot_bytes(uint32_t max_len)
 // bytes of one wide-mode slot (16-B records, rc_enc2_wcode reads 4 ahead)
 extern "C" uint64_t rc_hip_enc2_wide_slot_bytes(uint32_t max_len)
 {
-    const uint64_t l = max_len < kE2MaxLen ? max_len : kE2MaxLen;
+    const uint64_t l = max_len < kE2SlotMax ? max_len : kE2SlotMax;
     return 16 * l + 256;
 }
 
@@ -2206,13 +2363,17 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         else
             hipLaunchKernelGGL(rc_enc2_code2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
         if (e.wide) {
+            const dim3 g(cnt < scan_blocks_max ? cnt : scan_blocks_max);
             if (e.slot_len <= kWideSmallL)
-                hipLaunchKernelGGL(rc_enc2_wscan_s, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max),
-                                   dim3(kScanThreads), 0, st, *b, e);
+                hipLaunchKernelGGL(rc_enc2_wscan_s, g, dim3(kScanThreads), 0, st, *b, e);
+            else if (e.slot_len <= 2048)
+                hipLaunchKernelGGL(rc_enc2_wscan, g, dim3(kScanThreads), 0, st, *b, e);
             else
-                hipLaunchKernelGGL(rc_enc2_wscan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max),
-                                   dim3(kScanThreads), 0, st, *b, e);
-            hipLaunchKernelGGL(rc_enc2_wcode, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
+                hipLaunchKernelGGL(rc_enc2_wscan_l, g, dim3(kScanThreads), 0, st, *b, e);
+            if (e.slot_len <= kE2MaxLen)
+                hipLaunchKernelGGL(rc_enc2_wcode, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
+            else
+                hipLaunchKernelGGL(rc_enc2_wcode_r, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
         }
     }
     return static_cast<int>(hipGetLastError());

@@ -167,7 +167,7 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
  * a chunk smaller than that leaves the code pass's lanes partly idle for a
  * whole packet's time) */
 #define ENC2_STREAM_MAX (3ull << 30)
-#define ENC2_WIDE_MAX (3ull << 30)
+#define ENC2_WIDE_MAX (5ull << 30)      /* (65536 wide 4096-B packets: 4.3 GB, one chunk) */
 
 static uint64_t env_mb_cap(const char *name, uint64_t cap)
 {

@@ -149,3 +149,71 @@ def test_wide_off_takes_lanes():
     _check(c, pk, lambda n: 2 * n + 64)
     assert c.last_lane_count() == 2048
     c.close()
+
+
+def _long_wide_packets(n, seed):
+    """Wide packets of 1920-4096 bytes (a bucket over 64 positions): low-entropy
+    ones that never reach compress.c's model reset within 4096 bytes (game
+    state, mostly-zero), and skewed random ones that reset once or twice
+    (compress.c:148-157 at 4094 nodes: zeros with random bytes between them
+    make ~2 nodes per random byte)."""
+    rng = np.random.default_rng(seed)
+    d, o, l = synth.gamestate_batch(max(1, n // 4), 4096)
+    out = [d[int(o[i]): int(o[i]) + int(l[i])].tobytes()[: int(rng.integers(1920, 4097))] for i in range(len(l))]
+    while len(out) < n:
+        ln = int(rng.integers(1920, 4097))
+        z = rng.uniform(0.25, 0.6) if len(out) % 2 else rng.uniform(0.6, 0.95)
+        out.append(np.where(rng.random(ln) < z, 0, rng.integers(0, 256, ln)).astype(np.uint8).tobytes())
+    return out
+
+
+def test_wide_model_reset_vs_oracle():
+    """The wide mode through the model reset (compress.c:148-157): windows at
+    the reset byte, the code pass clearing its root there; every packet stays
+    on the wide path, bit-exact, both outLimit modes."""
+    from tests.proto.twopass import scan_wide
+    c = _coder()
+    pk = _long_wide_packets(1200, 21)
+    # (the generator does reach the reset: the model restated in tests/proto/twopass.py)
+    assert sum(1 for p in pk[301:341] for rec in scan_wide(p, max_len=4096) if rec[3]) > 0
+    _check(c, pk, lambda n: 2 * n + 64)
+    assert c.last_lane_count() == 0
+    _check(c, pk, lambda n: n)
+    c.close()
+
+
+def test_wide_4096_gamestate_full_batch():
+    """65536 game-state packets of 4096 bytes: every packet on the wide path
+    (last_lane_count 0), bit-exact against the oracle on a sample and the round
+    trip on all."""
+    from oracle.pyoracle import compress_batch as ocompress
+    c = _coder()
+    d, o, l = synth.gamestate_batch(65536, 4096)
+    n = len(l)
+    din = torch.from_numpy(d).cuda()
+    doff = torch.from_numpy(o.astype(np.int64)).cuda()
+    dlen = torch.from_numpy(l.astype(np.int32)).cuda()
+    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+    coff = torch.zeros(n, dtype=torch.int64, device="cuda")
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+    cout = torch.zeros(int(coff[-1] + cap[-1]), dtype=torch.uint8, device="cuda")
+    clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    c.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=4096)
+    torch.cuda.synchronize()
+    assert c.last_lane_count() == 0 and c.last_exact_count() == 0
+    cl = clen.cpu().numpy().astype(np.uint32)
+    co = coff.cpu().numpy()
+    cb = cout.cpu().numpy()
+    sel = np.arange(0, n, 97)
+    ref, roff, rcap, rlen = ocompress(np.concatenate([d[int(o[i]): int(o[i]) + 4096] for i in sel]),
+                                      (np.arange(len(sel)) * 4096).astype(np.uint64),
+                                      np.full(len(sel), 4096, np.uint32), "port")
+    for k, i in enumerate(sel):
+        assert int(cl[i]) == int(rlen[k]), i
+        assert np.array_equal(cb[int(co[i]): int(co[i]) + int(cl[i])], ref[int(roff[k]): int(roff[k]) + int(rlen[k])]), i
+    back = torch.zeros_like(din)
+    bl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    c.decompress_batch(cout, coff, clen, back, doff, dlen, bl, max_len=int(cl.max()))
+    torch.cuda.synchronize()
+    assert torch.equal(bl, dlen) and torch.equal(back, din)
+    c.close()
