@@ -169,7 +169,7 @@ int rc_hip_gather16(const uint8_t *src, const uint64_t *soff, uint8_t *dst, cons
 /* out_len bytes of each packet from src + off[i] to dst + off[i], one
  * wavefront per packet; dst may be mapped host memory (rc_pack.hip) */
 int rc_hip_slot_copy(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint8_t *dst,
-                     void *stream);
+                     uint32_t max_wgs, void *stream);
 /* The reverse of rc_hip_pack: packed (back to back) -> out[out_off[i] .. +out_len[i]). */
 int rc_hip_unpack(const uint8_t *packed, uint8_t *out, const uint64_t *out_off, const uint32_t *out_len,
                   uint32_t n, uint64_t *bsum, void *stream);

@@ -32,6 +32,8 @@ extern void *enet_malloc(size_t) __attribute__((weak));
 extern void enet_free(void *) __attribute__((weak));
 extern void enet_host_compress(ENetHost *, const ENetCompressor *) __attribute__((weak));
 
+#define SPLIT_MAX 4                 /* pieces of a large host batch (run_host_split) */
+#define SPLIT_DEFAULT 3
 #define EXACT_SLOTS 256u            /* concurrent exact-path packets (64 KiB pool each) */
 
 typedef struct {
@@ -60,16 +62,17 @@ typedef struct {
     size_t d_pack_cap;
     uint64_t *d_bsum;
     size_t d_bsum_cap;
-    /* host batches in two halves (run_host_split): the second context on the
-       device, and the hand-off of the first half's input DMA */
-    void *twin;
+    /* host batches in pieces (run_host_split): the further contexts on the
+       device, and the hand-off of each piece's input DMA to the next piece */
+    void *twin[SPLIT_MAX - 1];
     struct h2d_sync *sync_sig, *sync_wait;
-    int last_split;
+    int last_split;                 /* pieces of the last host batch (0: one piece) */
+    int split_k;                    /* pieces of a large host batch (ENET_RC_HOST_SPLIT) */
 } rc_ctx;
 
-/* The first half records ev on its stream once its input DMA is enqueued
- * (ready 1; -1: it ended before that), the second half's stream waits for it
- * before its own. */
+/* A piece records ev on its stream once its input DMA is enqueued (ready 1;
+ * -1: it ended before that), the next piece's stream waits for it before its
+ * own. */
 struct h2d_sync {
     pthread_mutex_t m;
     pthread_cond_t cv;
@@ -283,6 +286,18 @@ void *enet_range_coder_create(void)
         c->enc2_wide_on = !(ew && strcmp(ew, "0") == 0);
         c->enc2_stream_max = env_mb_cap("ENET_RC_ENC2_STREAM_MB", ENC2_STREAM_MAX);
         c->enc2_wide_max = env_mb_cap("ENET_RC_ENC2_WIDE_MB", ENC2_WIDE_MAX);
+        /* large host batches in pieces (run_host_split): ENET_RC_HOST_SPLIT=k
+           pieces, 2..SPLIT_MAX (0 or 1: off) */
+        const char *hs = getenv("ENET_RC_HOST_SPLIT");
+        c->split_k = hs ? atoi(hs) : SPLIT_DEFAULT;
+        if (c->split_k < 1) c->split_k = 1;
+        if (c->split_k > SPLIT_MAX) c->split_k = SPLIT_MAX;
+        /* each piece's stream needs a hardware queue of its own (streams
+           sharing one run one after the other), and the process's default
+           stream holds one of the runtime's GPU_MAX_HW_QUEUES (default 4) */
+        const char *hq = getenv("GPU_MAX_HW_QUEUES");
+        const int queues = hq && atoi(hq) > 0 ? atoi(hq) : 4;
+        if (c->split_k > queues - 1) c->split_k = queues > 2 ? queues - 1 : 1;
         /* the fast decoder: rc_dec6.hip's rc_decompress_dec6s (64 packets per
            wavefront); none with ENET_RC_DEC=0 (ENET_RC_DEC4=0, the older name,
            too) or with 32 / 16 packets per wavefront */
@@ -323,6 +338,7 @@ static void ctx_copy_config(rc_ctx *dst, const rc_ctx *src)
     dst->enc2_stream_max = src->enc2_stream_max;
     dst->enc2_wide_max = src->enc2_wide_max;
     dst->max_slots = src->max_slots;
+    dst->split_k = 1;
 }
 
 void enet_range_coder_destroy(void *context)
@@ -349,7 +365,8 @@ void enet_range_coder_destroy(void *context)
     if (c->d_stage) hipFree(c->d_stage);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->stream) hipStreamDestroy(c->stream);
-    if (c->twin) enet_range_coder_destroy(c->twin);
+    for (int i = 0; i < SPLIT_MAX - 1; ++i)
+        if (c->twin[i]) enet_range_coder_destroy(c->twin[i]);
     ctx_release(c);
 }
 
@@ -676,6 +693,69 @@ static double now_ms(void)
     return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
 }
 
+/* A host-to-device copy from page-locked memory as 2D copies (rows of 1 MiB,
+ * or 64 KiB below 4 MiB; the tail as two overlapping rows): the runtime runs
+ * 2D copies on a DMA engine, a plain one of this size as a copy kernel, which
+ * takes CUs from the kernels of the pieces already running (run_host_split).
+ * ENET_RC_H2D_DMA=0: plain copies. */
+static hipError_t h2d_copy(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("ENET_RC_H2D_DMA");
+        on = e ? atoi(e) != 0 : 1;
+    }
+    const size_t w = bytes >= (4u << 20) ? (1u << 20) : (1u << 16), rows = bytes / w;
+    /* (past 48 MB the runtime ran some 2D copies as a row-by-row copy kernel
+     * at a tenth of the link's rate: C4's pieces, profiles/r5s_split) */
+    if (!on || rows < 2 || bytes > (48u << 20)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+    hipError_t err = hipMemcpy2DAsync(dst, w, src, w, w, rows, hipMemcpyHostToDevice, s);
+    const size_t t = bytes - rows * w;
+    if (err == hipSuccess && t) {
+        /* the last 2 * ceil(t / 2) bytes (re-copying at most one byte of the rows) */
+        const size_t h = (t + 1) / 2, at = bytes - 2 * h;
+        err = hipMemcpy2DAsync((uint8_t *) dst + at, h, (const uint8_t *) src + at, h, h, 2, hipMemcpyHostToDevice, s);
+    }
+    return err;
+}
+
+static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const uint64_t *out_off,
+                        const uint32_t *out_cap, uint32_t *out_len, int allow_pin, uint64_t out_bytes, size_t total,
+                        size_t a_olen, size_t a_out, size_t a_ooff, uint64_t in_bytes, int prof, double *tp);
+
+/* Workgroups of the slot copy of a piece of a split host batch
+ * (ENET_RC_PIECE_COPY_WGS, default 64; 0: 8 per CU) */
+static uint32_t piece_copy_wgs(void)
+{
+    static long w = -1;
+    if (w < 0) {
+        const char *e = getenv("ENET_RC_PIECE_COPY_WGS");
+        w = e ? atol(e) : 64;
+        if (w < 0) w = 0;
+    }
+    return (uint32_t) w;
+}
+
+/* A large device-to-host copy into page-locked memory; ENET_RC_D2H_DMA=1: as
+ * 2D copies (a DMA engine, not a copy kernel on the CUs), like h2d_copy */
+static hipError_t d2h_copy(void *dst, const void *src, size_t bytes, hipStream_t s)
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("ENET_RC_D2H_DMA");
+        on = e ? atoi(e) != 0 : 0;
+    }
+    const size_t w = bytes >= (4u << 20) ? (1u << 20) : (1u << 16), rows = bytes / w;
+    if (!on || rows < 2) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+    hipError_t err = hipMemcpy2DAsync(dst, w, src, w, w, rows, hipMemcpyDeviceToHost, s);
+    const size_t t = bytes - rows * w;
+    if (err == hipSuccess && t) {
+        const size_t h = (t + 1) / 2, at = bytes - 2 * h;
+        err = hipMemcpy2DAsync((uint8_t *) dst + at, h, (const uint8_t *) src + at, h, h, 2, hipMemcpyDeviceToHost, s);
+    }
+    return err;
+}
+
 static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
                     const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
                     const uint32_t *out_cap, uint32_t *out_len, int allow_pin,
@@ -791,7 +871,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     memcpy(h + a_ilen, in_len, n * 4);
     memcpy(h + a_ooff, out_off, n * 8);
     memcpy(h + a_ocap, out_cap, n * 4);
-    if (c->sync_wait) {             /* the second half: its DMA after the first half's */
+    if (c->sync_wait) {             /* a later piece: its DMA after the previous piece's */
         struct h2d_sync *y = c->sync_wait;
         pthread_mutex_lock(&y->m);
         while (!y->ready) pthread_cond_wait(&y->cv, &y->m);
@@ -799,13 +879,13 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         pthread_mutex_unlock(&y->m);
         if (r > 0) (void) hipStreamWaitEvent(c->stream, y->ev, 0);
     }
-    hipError_t err = hipMemcpyAsync(d + a_ioff, h + a_ioff, a_olen - a_ioff, hipMemcpyHostToDevice, c->stream);
+    hipError_t err = h2d_copy(d + a_ioff, h + a_ioff, a_olen - a_ioff, c->stream);
     if (err != hipSuccess) { host_unpin(in + zc_lo, zc_pin); return (int) err; }
     /* the payload: straight from the caller's memory when it is one range and
      * can be page-locked; else in four packet groups through pinned staging,
      * the staging copy of group k+1 overlapping the DMA of group k */
     const int pin_in = packed_in && allow_pin ? host_pin(in + in_lo, in_bytes) : 0;
-    if (pin_in) err = hipMemcpyAsync(d + a_in, in + in_lo, in_bytes, hipMemcpyHostToDevice, c->stream);
+    if (pin_in) err = h2d_copy(d + a_in, in + in_lo, in_bytes, c->stream);
     if (pitch) {
         err = hipMemcpy2DAsync(d + a_in, row, in + zc_lo, pitch, max_len, n - 1, hipMemcpyHostToDevice, c->stream);
         if (err == hipSuccess && in_len[n - 1])
@@ -838,7 +918,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         if (b1 > b0) err = hipMemcpyAsync(d + a_in + b0, h + a_in + b0, b1 - b0, hipMemcpyHostToDevice, c->stream);
         if (err != hipSuccess) return (int) err;
     }
-    if (c->sync_sig) {              /* the first half: its input DMA is enqueued */
+    if (c->sync_sig) {              /* its input DMA is enqueued: the next piece's may follow */
         h2d_sync_set(c->sync_sig, hipEventRecord(c->sync_sig->ev, c->stream) == hipSuccess ? 1 : -1);
     }
     if (prof) { tp[1] = now_ms(); hipStreamSynchronize(c->stream); tp[2] = now_ms(); }
@@ -846,12 +926,26 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
                         (const uint32_t *) (d + a_ilen), n, max_len, max_cap, d + a_out,
                         (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_ocap),
                         (uint32_t *) (d + a_olen), (void *) c->stream);
-    if (pin_in || zc_pin) {     /* the input DMA / gather is behind the kernels on the stream */
+    if (rc == 0) rc = host_results(c, decompress, n, out, out_off, out_cap, out_len, allow_pin, out_bytes, total,
+                                   a_olen, a_out, a_ooff, in_bytes, prof, tp);
+    if (pin_in == 1 || zc_pin == 1) {   /* (registered for this call: the input DMA / gather is done by now) */
         hipStreamSynchronize(c->stream);
         host_unpin(in + in_lo, pin_in);
         host_unpin(in + zc_lo, zc_pin);
     }
-    if (rc != 0) return rc;
+    return rc;
+}
+
+/* The results of run_host's kernels into the caller's slots; returns after
+ * the stream has drained (on success). */
+static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const uint64_t *out_off,
+                        const uint32_t *out_cap, uint32_t *out_len, int allow_pin, uint64_t out_bytes, size_t total,
+                        size_t a_olen, size_t a_out, size_t a_ooff, uint64_t in_bytes, int prof, double *tp)
+{
+    uint8_t *h = c->h_stage, *d = c->d_stage;
+    const size_t blocks = (n + 1023) / 1024;
+    hipError_t err = hipSuccess;
+    int rc = 0;
     if (prof) { hipStreamSynchronize(c->stream); tp[3] = now_ms(); }
     if (out_bytes <= (1u << 20)) {
         /* small batches (the per-datagram drop-in calls): one D2H of the slots,
@@ -865,28 +959,33 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
             if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
         return 0;
     }
-    /* the results: straight into the caller's slots when they are back to
-     * back and every packet filled its slot exactly (a decompress batch with
-     * out_cap = the packet lengths) -- one DMA writes exactly the results;
-     * else packed on the device (rc_pack.hip), copied, scattered on the host */
-    int contig_out = 1;
+    /* a decompress batch whose slots are back to back (out_cap = the packet
+     * lengths): the whole span in one DMA straight behind the kernels (a slot
+     * a packet did not fill gets unspecified bytes past its out_len, as the
+     * reference's outLimit allows) */
+    /* (a piece of a split batch of packets of >= 512 B on average: its slot
+     * copy below with few workgroups, leaving the other pieces' kernels
+     * their CUs' issue slots; the copy's wavefronts each move a packet, so
+     * smaller packets need them all to keep PCIe busy) */
+    const uint32_t wgs = (c->sync_sig || c->sync_wait) && in_bytes >= 512 * (uint64_t) n ? piece_copy_wgs() : 0u;
+    int contig_out = decompress;
     for (size_t i = 1; i < n && contig_out; ++i) contig_out = out_off[i] == out_off[i - 1] + out_cap[i - 1];
-    err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
-    if (err == hipSuccess && contig_out) err = hipStreamSynchronize(c->stream);
-    if (err != hipSuccess) return (int) err;
     if (contig_out) {
-        const uint32_t *ol = (const uint32_t *) (h + a_olen);
-        int full = 1;
-        for (size_t i = 0; i < n && full; ++i) full = ol[i] == out_cap[i];
         const uint64_t span = out_off[n - 1] + out_cap[n - 1] - out_off[0];
-        const int pin_out = full && allow_pin ? host_pin(out + out_off[0], span) : 0;
+        /* (registering the caller's range while the kernels run made this
+         * copy 1.2 ms slower: register it once they are done) */
+        hipStreamSynchronize(c->stream);
+        const int pin_out = allow_pin ? host_pin(out + out_off[0], span) : 0;
         if (pin_out) {
-            err = hipMemcpyAsync(out + out_off[0], d + a_out + out_off[0], span, hipMemcpyDeviceToHost, c->stream);
-            if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+            err = d2h_copy(out + out_off[0], d + a_out + out_off[0], span, c->stream);
+            if (err == hipSuccess) err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
+            if (err == hipSuccess)
+                err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
+            const hipError_t e2 = hipStreamSynchronize(c->stream);
             host_unpin(out + out_off[0], pin_out);
+            if (err == hipSuccess) err = e2;
             if (err != hipSuccess) return (int) err;
-            memcpy(out_len, ol, n * 4);
+            memcpy(out_len, h + a_olen, n * 4);
             if (prof) {
                 tp[5] = now_ms();
                 fprintf(stderr, "enet_rc host %s n=%zu in=%.1f MB out=%.1f MB (direct): stage+H2D enqueue %.3f, "
@@ -912,7 +1011,10 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         if (op && hipHostGetDevicePointer(&dp, (void *) (out + lo), 0) == hipSuccess && dp) {
             err = (hipError_t) rc_hip_slot_copy(d + a_out, (const uint64_t *) (d + a_ooff),
                                                 (const uint32_t *) (d + a_olen), (uint32_t) n, (uint8_t *) dp - lo,
-                                                (void *) c->stream);
+                                                wgs, (void *) c->stream);
+            if (err == hipSuccess) err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
+            if (err == hipSuccess)
+                err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
             const hipError_t e2 = hipStreamSynchronize(c->stream);
             host_unpin(out + lo, op);
             if (err == hipSuccess) err = e2;
@@ -933,7 +1035,9 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
                      c->d_bsum, c->d_pack, (void *) c->stream);
     if (rc != 0) return rc;
     uint64_t packed = 0;
-    err = hipMemcpyAsync(&packed, c->d_bsum + blocks, 8, hipMemcpyDeviceToHost, c->stream);
+    err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(&packed, c->d_bsum + blocks, 8, hipMemcpyDeviceToHost, c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     if (err != hipSuccess) return (int) err;
     if (prof) tp[4] = now_ms();
@@ -974,44 +1078,46 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     return err == hipSuccess ? 0 : (int) err;
 }
 
-/* ---- a large host batch in two halves, on this context and a second one
- * on the same device (its own stream and workspace): the second half's input
- * DMA follows the first half's, so its kernels overlap the first half's on
- * the other CUs, and the first half's results cross PCIe while the second
- * half computes.  The lane kernels take as long for half a batch as for the
- * whole (a packet per lane), so the halves run side by side,
- * never one after the other.  The caller's input and output ranges are
- * page-locked once here for both halves (adjacent halves share boundary
- * pages: see host_pin).  ENET_RC_HOST_SPLIT=0: off. */
+/* ---- a large host batch in pieces, on this context and further contexts
+ * on the same device (each with its own stream and workspace): each piece's
+ * input DMA follows the previous piece's, so its kernels start while the
+ * later pieces' inputs still cross PCIe and run beside the earlier pieces'
+ * on the other CUs, and the earlier pieces' results cross PCIe while the later
+ * ones compute.  The lane kernels take as long for part of a batch as for the
+ * whole (a packet per lane), so the pieces run side by side,
+ * never one after the other.  Pieces hold equal input bytes.  The caller's
+ * input and output ranges are page-locked once here for all pieces (adjacent
+ * pieces share boundary pages: see host_pin).  ENET_RC_HOST_SPLIT=k: k pieces
+ * (2..SPLIT_MAX; 0 or 1: off). */
 typedef struct {
     rc_ctx *c;
     int decompress;
     const uint8_t *in; const uint64_t *in_off; const uint32_t *in_len; size_t n;
     uint8_t *out; const uint64_t *out_off; const uint32_t *out_cap; uint32_t *out_len;
     int rc;
-} half_job;
+} piece_job;
 
-static void *half_worker(void *p)
+static void *piece_worker(void *p)
 {
-    half_job *j = (half_job *) p;
+    piece_job *j = (piece_job *) p;
     j->rc = run_host(j->c, j->decompress, j->in, j->in_off, j->in_len, j->n, j->out, j->out_off, j->out_cap,
                      j->out_len, 1, NULL, NULL);
+    /* (a piece that ended before its input DMA: the next one waits for nothing) */
+    if (j->c->sync_sig) h2d_sync_set(j->c->sync_sig, -1);
     return NULL;
 }
 
-#define SPLIT_MIN_PACKETS 32768u
-#define SPLIT_MIN_BYTES (32ull << 20)
-
+#define SPLIT_MIN_PACKETS 8192u         /* per piece */
+#define SPLIT_MIN_BYTES (8ull << 20)    /* per piece */
 static int run_host_split(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
                           const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
                           const uint32_t *out_cap, uint32_t *out_len)
 {
-    static int off = -1;
-    if (off < 0) { const char *e = getenv("ENET_RC_HOST_SPLIT"); off = e && strcmp(e, "0") == 0; }
     if (!c) return (int) hipErrorInvalidValue;
     c->last_split = 0;
+    int k = c->split_k;
     uint64_t bytes = 0, ilo = UINT64_MAX, ihi = 0, olo = UINT64_MAX, ohi = 0;
-    if (!off && n >= SPLIT_MIN_PACKETS && c->ws.kernel != RC_KERNEL_WAVE) {
+    if (k > 1 && n >= 32768 && c->ws.kernel != RC_KERNEL_WAVE) {
         for (size_t i = 0; i < n; ++i) {
             bytes += in_len[i];
             if (in_len[i]) {
@@ -1022,52 +1128,92 @@ static int run_host_split(rc_ctx *c, int decompress, const uint8_t *in, const ui
             if (out_off[i] + out_cap[i] > ohi) ohi = out_off[i] + out_cap[i];
         }
     }
-    if (off || n < SPLIT_MIN_PACKETS || c->ws.kernel == RC_KERNEL_WAVE || bytes < SPLIT_MIN_BYTES || ihi <= ilo ||
-        ohi <= olo)
+    if (n < 32768 || bytes < (32ull << 20)) k = 1;   /* (smaller batches: one piece) */
+    while (k > 1 && (n < (size_t) k * SPLIT_MIN_PACKETS || bytes < (uint64_t) k * SPLIT_MIN_BYTES)) --k;
+    if (k < 2 || ihi <= ilo || ohi <= olo)
         return run_host(c, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
-    if (!c->twin) {
-        c->twin = enet_range_coder_create();
-        if (c->twin) ctx_copy_config((rc_ctx *) c->twin, c);
-    }
-    const int pi = c->twin ? host_pin(in + ilo, ihi - ilo) : 0;
+    for (int i = 0; i < k - 1; ++i)
+        if (!c->twin[i]) {
+            c->twin[i] = enet_range_coder_create();
+            if (c->twin[i]) ctx_copy_config((rc_ctx *) c->twin[i], c);
+            else { k = i + 1; break; }
+        }
+    const int pi = k > 1 ? host_pin(in + ilo, ihi - ilo) : 0;
     const int po = pi ? host_pin(out + olo, ohi - olo) : 0;
-    struct h2d_sync y;
-    int ev_ok = 0;
-    if (po) {
-        pthread_mutex_init(&y.m, NULL);
-        pthread_cond_init(&y.cv, NULL);
-        y.ready = 0;
-        ev_ok = hipEventCreateWithFlags(&y.ev, hipEventDisableTiming) == hipSuccess;
+    struct h2d_sync y[SPLIT_MAX - 1];
+    int ny = 0;
+    for (; po && ny < k - 1; ++ny) {
+        if (hipEventCreateWithFlags(&y[ny].ev, hipEventDisableTiming) != hipSuccess) break;
+        pthread_mutex_init(&y[ny].m, NULL);
+        pthread_cond_init(&y[ny].cv, NULL);
+        y[ny].ready = 0;
     }
-    if (!ev_ok) {                   /* (no second context, pinning or event: one piece) */
-        if (po) { pthread_cond_destroy(&y.cv); pthread_mutex_destroy(&y.m); }
+    if (ny < k - 1) {               /* (no further context, pinning or event: one piece) */
+        for (int i = 0; i < ny; ++i) {
+            hipEventDestroy(y[i].ev);
+            pthread_cond_destroy(&y[i].cv);
+            pthread_mutex_destroy(&y[i].m);
+        }
         host_unpin(out + olo, po);
         host_unpin(in + ilo, pi);
         return run_host(c, decompress, in, in_off, in_len, n, out, out_off, out_cap, out_len, 1, NULL, NULL);
     }
-    rc_ctx *t = (rc_ctx *) c->twin;
-    const size_t m = n / 2;
-    half_job hb = {t, decompress, in, in_off + m, in_len + m, n - m, out, out_off + m, out_cap + m, out_len + m, 0};
-    c->sync_sig = &y;
-    t->sync_wait = &y;
-    pthread_t th;
-    const int threaded = pthread_create(&th, NULL, half_worker, &hb) == 0;
-    if (!threaded) h2d_sync_set(&y, -1);
-    const int ra = run_host(c, decompress, in, in_off, in_len, m, out, out_off, out_cap, out_len, 1, NULL, NULL);
-    h2d_sync_set(&y, -1);           /* (the first half ended before its input DMA: no wait) */
-    if (threaded) pthread_join(th, NULL);
-    else half_worker(&hb);
-    c->sync_sig = NULL;
-    t->sync_wait = NULL;
-    hipEventDestroy(y.ev);
-    pthread_cond_destroy(&y.cv);
-    pthread_mutex_destroy(&y.m);
+    /* piece boundaries at equal shares of the input bytes */
+    size_t first[SPLIT_MAX + 1];
+    first[0] = 0;
+    first[k] = n;
+    {
+        uint64_t acc = 0;
+        size_t i = 0;
+        for (int p = 1; p < k; ++p) {
+            const uint64_t goal = bytes * (uint64_t) p / (uint64_t) k;
+            while (i < n && acc + in_len[i] <= goal) acc += in_len[i++];
+            /* whole 2048-packet groups: a piece's decoder and code-pass
+               workgroups (256 packets each) then spread evenly over the 8
+               XCDs, and the pieces' workgroups together fill each XCD's CUs
+               once (a piece one workgroup over lands it on a busy CU and
+               doubles that piece's time) */
+            size_t f = (i + 1024) & ~(size_t) 2047;
+            if (f <= first[p - 1]) f = first[p - 1] + 2048;
+            first[p] = f < n ? f : n;
+        }
+    }
+    piece_job job[SPLIT_MAX];
+    pthread_t th[SPLIT_MAX];
+    int threaded[SPLIT_MAX] = {0};
+    for (int p = 0; p < k; ++p) {
+        rc_ctx *x = p ? (rc_ctx *) c->twin[p - 1] : c;
+        const size_t a = first[p], m = first[p + 1] - a;
+        piece_job j = {x, decompress, in, in_off + a, in_len + a, m, out, out_off + a, out_cap + a, out_len + a, 0};
+        job[p] = j;
+        x->sync_wait = p ? &y[p - 1] : NULL;
+        x->sync_sig = p < k - 1 ? &y[p] : NULL;
+    }
+    for (int p = 1; p < k; ++p) threaded[p] = pthread_create(&th[p], NULL, piece_worker, &job[p]) == 0;
+    piece_worker(&job[0]);
+    for (int p = 1; p < k; ++p) {
+        if (threaded[p]) pthread_join(th[p], NULL);
+        else piece_worker(&job[p]);     /* (its predecessors have all signalled by now) */
+    }
+    int rc = 0;
+    uint32_t exact = 0;
+    for (int p = 0; p < k; ++p) {
+        rc_ctx *x = job[p].c;
+        x->sync_wait = x->sync_sig = NULL;
+        if (!rc) rc = job[p].rc;
+        exact += x->last_exact;
+    }
+    c->last_exact = exact;
+    for (int i = 0; i < k - 1; ++i) {
+        hipEventDestroy(y[i].ev);
+        pthread_cond_destroy(&y[i].cv);
+        pthread_mutex_destroy(&y[i].m);
+    }
     host_unpin(out + olo, po);
     host_unpin(in + ilo, pi);
-    c->last_split = 1;
-    c->last_exact += t->last_exact;
-    return ra ? ra : hb.rc;
+    c->last_split = k;
+    return rc;
 }
 
 int enet_rc_compress_batch_host(void *context, const uint8_t *in, const uint64_t *in_off,
@@ -1388,9 +1534,12 @@ uint32_t enet_rc_last_lane_count(void *context)
     uint32_t v = 0, w = 0;
     hipDeviceSynchronize();
     if (hipMemcpy(&v, c->ws.counters + 3, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    if (c->last_split && c->twin &&
-        hipMemcpy(&w, ((rc_ctx *) c->twin)->ws.counters + 3, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    return v + w;
+    for (int i = 0; i + 1 < c->last_split; ++i) {
+        if (!c->twin[i] ||
+            hipMemcpy(&w, ((rc_ctx *) c->twin[i])->ws.counters + 3, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+        v += w;
+    }
+    return v;
 }
 
 uint32_t enet_rc_last_exact_count(void *context)
@@ -1400,9 +1549,12 @@ uint32_t enet_rc_last_exact_count(void *context)
     uint32_t v = 0, w = 0;
     hipDeviceSynchronize();
     if (hipMemcpy(&v, c->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    if (c->last_split && c->twin &&
-        hipMemcpy(&w, ((rc_ctx *) c->twin)->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    return v + w;
+    for (int i = 0; i + 1 < c->last_split; ++i) {
+        if (!c->twin[i] || hipMemcpy(&w, ((rc_ctx *) c->twin[i])->ws.counters, 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return 0;
+        v += w;
+    }
+    return v;
 }
 
 /* The context's kernel configuration as flag bits (the settings
@@ -1420,14 +1572,17 @@ uint32_t enet_rc_config_flags(void *context)
     const rc_ctx *c = (const rc_ctx *) context;
     if (!c) return 0;
     const uint32_t f = config_flags(c);
-    const rc_ctx *t = (const rc_ctx *) c->twin;
-    return f | ((t && (config_flags(t) != f || t->enc2_stream_max != c->enc2_stream_max ||
-                       t->enc2_wide_max != c->enc2_wide_max || t->max_slots != c->max_slots ||
-                       t->ws.small_max != c->ws.small_max || t->ws.dec6_debug != c->ws.dec6_debug))
-                    ? 0x80000000u : 0u);
+    int differ = 0;
+    for (int i = 0; i < SPLIT_MAX - 1; ++i) {
+        const rc_ctx *t = (const rc_ctx *) c->twin[i];
+        differ |= t && (config_flags(t) != f || t->enc2_stream_max != c->enc2_stream_max ||
+                        t->enc2_wide_max != c->enc2_wide_max || t->max_slots != c->max_slots ||
+                        t->ws.small_max != c->ws.small_max || t->ws.dec6_debug != c->ws.dec6_debug);
+    }
+    return f | (differ ? 0x80000000u : 0u);
 }
 
-uint32_t enet_rc_last_split(void *context) { return context && ((rc_ctx *) context)->last_split ? 1u : 0u; }
+uint32_t enet_rc_last_split(void *context) { return context ? (uint32_t) ((rc_ctx *) context)->last_split : 0u; }
 
 /* ------------------------------------------------------ for rc_multi.c */
 

@@ -426,7 +426,7 @@ static int multi_device(rc_multi *m, int decompress, const uint8_t *in, const ui
         /* src + out_off[i] is packet i's slot on the device: its slots sit at
          * a_out + (out_off[i] - lo_out) */
         const uint8_t *src = (m->d[k].peer ? m->d[k].buf + s->a_out : m->stage + stage_at[k]) - s->lo_out;
-        rc = rc_hip_slot_copy(src, out_off + s->lo, out_len + s->lo, (uint32_t) s->cnt, out, rst);
+        rc = rc_hip_slot_copy(src, out_off + s->lo, out_len + s->lo, (uint32_t) s->cnt, out, 0, rst);
     }
     /* everything done before returning (the device batch calls of one
      * context return with work enqueued; this one returns with results) */

@@ -232,14 +232,17 @@ void rc_slot_copy(const uint8_t* src, const uint64_t* off, const uint32_t* len, 
 }
 
 extern "C" int rc_hip_slot_copy(const uint8_t* src, const uint64_t* off, const uint32_t* len, uint32_t n,
-                                uint8_t* dst, void* stream)
+                                uint8_t* dst, uint32_t max_wgs, void* stream)
 {
     if (n == 0) return 0;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
     uint32_t blocks = (n + kThreads / 64 - 1) / (kThreads / 64);
-    const uint32_t cap = static_cast<uint32_t>(cus) * 8;
+    // max_wgs: at most that many workgroups (0: 8 per CU) -- a copy beside
+    // other kernels (a piece of a split host batch, run_host_split) leaves
+    // their CUs' issue slots to them; PCIe, not the waves, bounds the copy
+    const uint32_t cap = max_wgs ? max_wgs : static_cast<uint32_t>(cus) * 8;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL(rc_slot_copy, dim3(blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream), src, off, len,
                        n, dst);
