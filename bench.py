@@ -63,6 +63,16 @@ def make_batch(kind, n, size, rank):
     return synth.mixed_batch(n, seed=(synth.SEED ^ 0x4D495845) + rank)
 
 
+def workload_name(kind, n=65536, size=1200):
+    """The workload label; a packet count or size other than the config's is
+    named as such (the C2/C3 shapes are 65536 x 1200 B)."""
+    name = WORKLOADS[kind]
+    if kind in ("c2", "c3") and (n, size) != (65536, 1200):
+        name = name.replace("C2 65536x1200B", f"C2-shaped {n}x{size}B").replace("C3 65536x1200B",
+                                                                               f"C3-shaped {n}x{size}B")
+    return name
+
+
 WORKLOADS = {"c2": "C2 65536x1200B uniform-random, compress+decompress round trip",
              "c3": "C3 65536x1200B game-state, compress+decompress round trip",
              "c4": "C4 1Mi mixed 64-1392B random, compress+decompress round trip"}
@@ -159,7 +169,7 @@ def run_workload(coder, dev, stream, kind, n, size, rank, steps, warmup, dist=No
         roofline["traffic_frac_of_peak"] = round(rate / HBM_PEAK_GBPS, 4)
         roofline["traffic_over_alg"] = round(traffic / alg, 2)
     summary = {
-        "workload": WORKLOADS[kind], "packets": n, "value": round(in_bytes * world * steps / elapsed / GIB, 4),
+        "workload": workload_name(kind, n, size), "packets": n, "value": round(in_bytes * world * steps / elapsed / GIB, 4),
         "unit": "GiB/s", "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": warmup,
         "bit_exact_roundtrip": ok, "compression_ratio": round(comp_bytes / in_bytes, 5),
         "compress_GiBps": round(in_bytes / t_comp / GIB, 4), "decompress_GiBps": round(in_bytes / t_dec / GIB, 4),
@@ -210,7 +220,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": WORKLOADS[args.workload],
+        "config": {"workload": workload_name(args.workload, args.packets, args.size),
                    "packets_per_gpu": n, "packet_bytes": args.size if args.workload != "c4" else "64-1392",
                    "parallelism": f"shard{world}", "out_cap": "2N+64"},
         "bit_exact_roundtrip": main_line["bit_exact_roundtrip"],

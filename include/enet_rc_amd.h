@@ -280,11 +280,12 @@ uint32_t enet_rc_last_lane_count(void *context);
 /* The context's kernel configuration, fixed when it was created (bits: 1 wave
  * kernel, 2 two-pass encoder, 4 its wide mode, 8 fast decoder, 16 the
  * encoder's slow paths forced, 8-14 packets per lane-kernel wavefront); bit 31
- * set if the context that runs the second half of its split host batches was
+ * set if a context that runs a piece of its split host batches was
  * configured differently (never, by construction). */
 uint32_t enet_rc_config_flags(void *context);
-/* 1 if the last host-pointer batch ran in two halves on two contexts of the
- * device (large batches: input copies of one half under the other's kernels). */
+/* The number of pieces the last host-pointer batch ran in, each on its own
+ * context of the device (large batches: a piece's input copy under the
+ * earlier pieces' kernels; ENET_RC_HOST_SPLIT), or 0 if it ran in one. */
 uint32_t enet_rc_last_split(void *context);
 /* Library version string. */
 const char *enet_rc_version(void);
