@@ -737,7 +737,10 @@ static uint32_t piece_copy_wgs(void)
 }
 
 /* A large device-to-host copy into page-locked memory; ENET_RC_D2H_DMA=1: as
- * 2D copies (a DMA engine, not a copy kernel on the CUs), like h2d_copy */
+ * 2D copies (a DMA engine, not a copy kernel on the CUs), like h2d_copy.  Off
+ * by default: for the results of a split batch's pieces the DMA engine ran at
+ * half the copy kernel's rate and one piece after the other
+ * (profiles/r5_split/ab_c2_d2h_dma.txt) */
 static hipError_t d2h_copy(void *dst, const void *src, size_t bytes, hipStream_t s)
 {
     static int on = -1;
@@ -746,7 +749,7 @@ static hipError_t d2h_copy(void *dst, const void *src, size_t bytes, hipStream_t
         on = e ? atoi(e) != 0 : 0;
     }
     const size_t w = bytes >= (4u << 20) ? (1u << 20) : (1u << 16), rows = bytes / w;
-    if (!on || rows < 2) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+    if (!on || rows < 2 || bytes > (48u << 20)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
     hipError_t err = hipMemcpy2DAsync(dst, w, src, w, w, rows, hipMemcpyDeviceToHost, s);
     const size_t t = bytes - rows * w;
     if (err == hipSuccess && t) {
@@ -973,8 +976,9 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
     if (contig_out) {
         const uint64_t span = out_off[n - 1] + out_cap[n - 1] - out_off[0];
         /* (registering the caller's range while the kernels run made this
-         * copy 1.2 ms slower: register it once they are done) */
-        hipStreamSynchronize(c->stream);
+         * copy 1.2 ms slower: register it once they are done; a piece of a
+         * split batch finds its range registered already) */
+        if (!c->sync_sig && !c->sync_wait) hipStreamSynchronize(c->stream);
         const int pin_out = allow_pin ? host_pin(out + out_off[0], span) : 0;
         if (pin_out) {
             err = d2h_copy(out + out_off[0], d + a_out + out_off[0], span, c->stream);

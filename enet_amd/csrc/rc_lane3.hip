@@ -865,6 +865,19 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             at = 0;
         }
         PROF(3)
+#ifdef RC_PROFILE
+        // event counts (lanes, summed per wave): steps in a dense order-1
+        // context, its lookups (search or the root step's find), order-2 hits
+        // whose next link misses the LDS cache, root steps
+        {
+            const bool dn = L.order >= 1 && L.cur.dense != 0;
+            const bool lcv0 = dn && L.cext != 0 && L.cur.ext == L.cext && v < kLinkCache;
+            prof_acc[7] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(dn));
+            prof_acc[8] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(dn && at <= 1));
+            prof_acc[10] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(dn && at == 2 && !lcv0));
+            prof_acc[11] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(at == 0));
+        }
+#endif
         lane_prefetch(L, reg, v);
         // the step's last code and the root's update: only the next step
         // needs them, so they run after the record load is issued (as in

@@ -69,7 +69,16 @@ def main():
         lib.rc_lane_prof_read(buf.ctypes.data, 1)
         names = DEC3 if V3 else DEC
         dec = {names[k]: round(float(buf[16 + k]) / steps, 1) for k in range(12) if names[k]}
-        dec["TOTAL"] = round(float(buf[16:28].sum()) / steps, 1)
+        dec["TOTAL"] = round(float(buf[16:28].sum() - (buf[23] + buf[24] + buf[26] + buf[27] if V3 else 0)) / steps, 1)
+        if V3:      # event counts (rc_lane3.hip), per lane-step
+            ls = steps * 64.0
+            for k in (7, 8, 10, 11):
+                dec.pop(names[k], None)
+            res["decompress_events_per_lane_step"] = {
+                "in a dense order-1 context": round(float(buf[23]) / ls, 4),
+                "dense order-1 lookups (order 1 or root steps)": round(float(buf[24]) / ls, 4),
+                "order-2 hits whose link misses the LDS cache": round(float(buf[26]) / ls, 4),
+                "root steps": round(float(buf[27]) / ls, 4)}
         res["decompress_cycles_per_wave_step"] = dec
         res["roundtrip_ok"] = bool(torch.equal(back, din))
     res["workload"] = wl
