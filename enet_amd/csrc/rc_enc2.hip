@@ -123,7 +123,6 @@ struct E2Params {
     uint32_t*       wlist;      // listed packets (batch indices), count *wcount, at most wcap slots
     uint32_t*       wcount;
     uint32_t        wcap;
-    uint32_t        prio;       // pass 2: the coding wavefronts at issue priority 3 (ENET_RC_ENC2_PRIO)
 };
 
 // the last element slot: buckets of 1918 positions, each padded to 4, end
@@ -1285,7 +1284,6 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     if (helper) atomicMax(bmax, len);
     __syncthreads();
     const uint32_t parts = (*bmax + kQPart - 1) / kQPart;
-    if (!helper && e.prio) __builtin_amdgcn_s_setprio(3);
     if (helper) {
         uint8_t* root = smem + lane * kCodeLds;
         {
@@ -2343,12 +2341,6 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     static const char* lanes = getenv("ENET_RC_ENC2_LANES");      // experiment: 32 packets per wavefront
     e.act = (lanes && atoi(lanes) == 32) ? 32u : 64u;
     e.slow = ws->enc2_slow;
-    static int prio = -1;
-    if (prio < 0) {
-        const char* pe = getenv("ENET_RC_ENC2_PRIO");
-        prio = pe ? atoi(pe) != 0 : 0;
-    }
-    e.prio = static_cast<uint32_t>(prio);
     for (uint64_t lo = 0; lo < b->n; lo += per) {
         const uint64_t hi = lo + per < b->n ? lo + per : b->n;
         e.lo = static_cast<uint32_t>(lo);
