@@ -134,7 +134,11 @@ static int lanes_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     uint32_t region = rc_hip_lane3_region_bytes(max_len ? max_len : 4096);
     const char *ov = getenv("ENET_RC_REGION");      /* diagnostic: smaller regions (overflows take the exact path) */
     if (ov && atoi(ov) > 0 && (uint32_t) atoi(ov) < region) region = ((uint32_t) atoi(ov) + 255) & ~255u;
-    size_t slots = n < c->max_slots ? n : c->max_slots;
+    /* (whole 8192-slot groups: the pieces of a split host batch differ by a
+       few thousand packets between calls, and a pool that grew by each would
+       be reallocated -- a device-wide wait -- on the calls after the first) */
+    size_t slots = n >= 8192 ? (n + 8191) & ~(size_t) 8191 : n;
+    if (slots > c->max_slots) slots = c->max_slots;
     slots = (slots + 255) & ~(size_t) 255;
     if (slots <= c->ws.lane_slots && region <= c->ws.lane_region) return 0;
     if (slots < c->ws.lane_slots) slots = c->ws.lane_slots;
@@ -185,7 +189,7 @@ static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     const uint32_t ml = max_len ? max_len : 4096;
     const uint64_t slot = rc_hip_enc2_slot_bytes(ml);
     const uint64_t cap = c->enc2_stream_max;
-    uint64_t want = (uint64_t) n * slot;
+    uint64_t want = (uint64_t) (n >= 8192 ? (n + 8191) & ~(size_t) 8191 : n) * slot;   /* (as lanes_reserve) */
     if (want > cap) want = cap > slot ? cap : slot;
     if (want > c->ws.enc2_cap) {
         hipDeviceSynchronize();

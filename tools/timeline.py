@@ -29,6 +29,13 @@ for e in ev:
     end = max(end, e[1]) if len(cur) > 1 else e[1]
 if cur:
     bursts.append(cur)
+if os.environ.get("TL_SUMMARY"):
+    for i, b in enumerate(bursts):
+        t0 = b[0][0]
+        print(f"burst {i}: {len(b)} events, {(max(e[1] for e in b) - t0) / 1e6:.3f} ms")
+    sel = [int(x) for x in os.environ["TL_SUMMARY"].split(",") if x]
+    bursts = [bursts[i] for i in sel]
+    nb = len(bursts)
 for b in bursts[-nb:]:
     t0 = b[0][0]
     t1 = max(e[1] for e in b)
