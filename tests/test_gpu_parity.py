@@ -535,6 +535,71 @@ def test_host_pointer_batches_pieces(pieces):
         c.close()
 
 
+def test_host_pointer_batches_pieces_ragged():
+    """Split host batches (three pieces, rc_host.c run_host_split) on a ragged
+    batch: 52100 packets of 0-2000 B (every 50th empty, a packet count that
+    is no multiple of the 2048-packet piece groups), inputs in gapped slots
+    both ways and decompress outputs in gapped slots too (the slot-copy
+    result path instead of the one-DMA one); bit-exact against the oracle."""
+    import os
+    import ctypes as C
+    from enet_amd import RangeCoder
+    from oracle.pyoracle import compress_batch as ocompress, fnv_digest
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    old = os.environ.get("ENET_RC_HOST_SPLIT")
+    os.environ["ENET_RC_HOST_SPLIT"] = "3"
+    try:
+        c = RangeCoder()
+    finally:
+        if old is None:
+            os.environ.pop("ENET_RC_HOST_SPLIT", None)
+        else:
+            os.environ["ENET_RC_HOST_SPLIT"] = old
+    try:
+        n = 52100
+        rng = np.random.default_rng(31)
+        l = rng.integers(0, 2001, n).astype(np.uint32)
+        l[::50] = 0
+        gap = rng.integers(0, 40, n).astype(np.uint64)
+        o = np.zeros(n, np.uint64)
+        o[1:] = np.cumsum(l[:-1].astype(np.uint64) + gap[:-1])
+        d = rng.integers(0, 256, int(o[-1] + l[-1]) + 16, dtype=np.uint8)
+        d[: d.size // 8] //= 16                      # (a low-entropy part: wide and lane paths too)
+        lib = c.lib
+        cap = (2 * l.astype(np.int64) + 64).astype(np.uint32)
+        coff = np.zeros(n, np.uint64)
+        coff[1:] = np.cumsum(cap[:-1].astype(np.uint64) + 7)
+        cout = np.zeros(int(coff[-1] + cap[-1]) + 16, np.uint8)
+        clen = np.zeros(n, np.uint32)
+        p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+        assert lib.enet_rc_compress_batch_host(c.ctx, p(d), p(o), p(l), n, p(cout), p(coff), p(cap), p(clen)) == 0
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        assert lib.enet_rc_last_split(c.ctx) == min(3, max(queues - 1, 1))
+        want, wo, wcap, wl = ocompress(d, o, l, "port")
+        assert np.array_equal(clen, wl)
+        assert fnv_digest(cout, coff, clen) == fnv_digest(want, wo, wl)
+        # decompress into gapped slots (a slot a packet fills exactly, 5 spare bytes between)
+        doff = np.zeros(n, np.uint64)
+        doff[1:] = np.cumsum(l[:-1].astype(np.uint64) + 5)
+        dout = np.full(int(doff[-1] + l[-1]) + 16, 0xAB, np.uint8)
+        dlen = np.zeros(n, np.uint32)
+        assert lib.enet_rc_decompress_batch_host(c.ctx, p(cout), p(coff), p(clen), n, p(dout), p(doff), p(l),
+                                                 p(dlen)) == 0
+        assert lib.enet_rc_last_split(c.ctx) == min(3, max(queues - 1, 1))
+        assert np.array_equal(dlen, l)
+        bad = [i for i in range(n) if not np.array_equal(dout[int(doff[i]): int(doff[i]) + int(l[i])],
+                                                         d[int(o[i]): int(o[i]) + int(l[i])])]
+        assert not bad, bad[:8]
+        # the gaps between slots are untouched (results go exactly to out_len bytes of each slot)
+        mask = np.ones(dout.size, bool)
+        for i in range(n):
+            mask[int(doff[i]): int(doff[i]) + int(l[i])] = False
+        assert np.all(dout[mask] == 0xAB)
+    finally:
+        c.close()
+
+
 def test_host_pointer_batches_split(coder):
     """A host batch of >= 32768 packets and >= 32 MB runs in two halves on two
     contexts of the device (rc_host.c run_host_split: the second half's input
