@@ -76,9 +76,16 @@ typedef struct {
     /* test switch (ENET_RC_ENC2_SLOW=1): the scan takes its slow paths (every position
        exceptional, every bucket sorted and re-walked) */
     uint32_t  enc2_slow;
-    /* lane kernels: when set, run only the sub_count[0] packets of sub_list */
+    /* lane kernels: when set, run only the sub_count[0] packets of sub_list
+       (the wave kernels too: their block i takes sub_list[i]) */
     const uint32_t *sub_list;
     const uint32_t *sub_count;
+    /* the context compresses on the two-pass encoder (ENET_RC_ENC2): small
+       batches take it too (rc_kernels.hip small_route) */
+    uint32_t  enc2_on;
+    /* rc_route.hip: the packets the record-light decoder leaves go to the
+       wave kernel instead of the lane kernels (small batches) */
+    uint32_t  wave_tail;
 } rc_workspace_dev;
 
 #define RC_SMALL_AUTO 0xFFFFFFFFu

@@ -286,6 +286,7 @@ void *enet_range_coder_create(void)
         c->ws.cus = (uint32_t) cus;
         const char *e2 = getenv("ENET_RC_ENC2");
         c->enc2_on = !(e2 && strcmp(e2, "0") == 0);
+        c->ws.enc2_on = (uint32_t) c->enc2_on;
         const char *ew = getenv("ENET_RC_ENC2_WIDE");
         c->enc2_wide_on = !(ew && strcmp(ew, "0") == 0);
         c->enc2_stream_max = env_mb_cap("ENET_RC_ENC2_STREAM_MB", ENC2_STREAM_MAX);
@@ -338,6 +339,7 @@ static void ctx_copy_config(rc_ctx *dst, const rc_ctx *src)
     dst->ws.dec6_debug = src->ws.dec6_debug;
     dst->ws.enc2_slow = src->ws.enc2_slow;
     dst->enc2_on = src->enc2_on;
+    dst->ws.enc2_on = src->ws.enc2_on;
     dst->enc2_wide_on = src->enc2_wide_on;
     dst->enc2_stream_max = src->enc2_stream_max;
     dst->enc2_wide_max = src->enc2_wide_max;

@@ -482,7 +482,8 @@ extern "C" __global__ __launch_bounds__(64)
 void rc_compress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes, uint32_t lds_bytes)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t s[];
-    const uint32_t pkt = blockIdx.x;
+    if (ws.sub_list && blockIdx.x >= *ws.sub_count) return;        // (a sub-list: its first sub_count packets)
+    const uint32_t pkt = ws.sub_list ? ws.sub_list[blockIdx.x] : blockIdx.x;
     const uint32_t len = b.in_len[pkt];
     Out o;
     o.g = b.out + b.out_off[pkt];
@@ -592,7 +593,8 @@ extern "C" __global__ __launch_bounds__(64)
 void rc_decompress_wave(rc_batch_dev b, rc_workspace_dev ws, uint32_t stage_bytes, uint32_t lds_bytes)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t s[];
-    const uint32_t pkt = blockIdx.x;
+    if (ws.sub_list && blockIdx.x >= *ws.sub_count) return;        // (a sub-list: its first sub_count packets)
+    const uint32_t pkt = ws.sub_list ? ws.sub_list[blockIdx.x] : blockIdx.x;
     const uint32_t len = b.in_len[pkt];
     Out o;
     o.g = b.out + b.out_off[pkt];
@@ -1113,10 +1115,15 @@ uint32_t wave_lds(bool decompress, uint32_t max_len, uint32_t max_out)
 }
 
 // Batches that fit on the chip in one wave per packet (the per-datagram
-// drop-in calls and a live host's send / receive passes among them) go to
-// the wavefront-per-packet kernel: a packet's byte chain runs there with
-// its model in LDS, 1.4-2.9x sooner than on one lane of the lane kernels
-// (tools/smallbatch.py).  Larger batches are throughput work: lanes.
+// drop-in calls and a live host's send / receive passes among them) ran on
+// the wavefront-per-packet kernel: a packet's byte chain runs there with its
+// model in LDS, 1.4-2.9x sooner than on one lane of the v3 lane kernels
+// (tools/smallbatch.py).  The fast kernels in front of those are faster
+// still for such batches (small_route): compress takes the two-pass encoder
+// (one 1200-B datagram: 0.53 ms against 2.4 random, 0.62 against 1.5 game
+// state), decompress the record-light decoder, with the wave kernel (not the
+// lane kernels) taking what it leaves (1.5 ms against 2.9 random; game state
+// leaves it early).  Larger batches are throughput work: lanes.
 static bool small_batch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, uint32_t& lds_w)
 {
     const uint32_t max_len = b->max_len ? b->max_len : 4096;
@@ -1132,10 +1139,37 @@ static bool small_batch(bool decompress, const rc_batch_dev* b, const rc_workspa
     return ws->kernel == RC_KERNEL_LANE3 && b->n <= resident && b->n <= ws->small_max;
 }
 
+// a small batch: 0 = the wave kernel, 1 = the lane path (two-pass encoder),
+// 2 = the record-light decoder, then the wave kernel on what it leaves
+static int small_route(bool decompress, const rc_workspace_dev* ws)
+{
+    if (ws->kernel == RC_KERNEL_WAVE || ws->small_max != RC_SMALL_AUTO) return 0;   // (ENET_RC_SMALL_BATCH=n: as set)
+    if (!decompress) return ws->enc2_on ? 1 : 0;
+    return ws->fast_dec && ws->lane_active == 64 ? 2 : 0;
+}
+
 extern "C" int rc_hip_uses_lanes(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws)
 {
     uint32_t lds_w;
-    return ws->kernel != RC_KERNEL_WAVE && !small_batch(decompress != 0, b, ws, lds_w);
+    return ws->kernel != RC_KERNEL_WAVE &&
+           (!small_batch(decompress != 0, b, ws, lds_w) || small_route(decompress != 0, ws) != 0);
+}
+
+// The wave kernel over the sub-list ws->sub_list (count ws->sub_count[0],
+// at most b->n): a grid of b->n blocks, the ones past the count leave at once.
+extern "C" int rc_hip_wave_tail_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
+                                       void* stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint32_t max_len = b->max_len ? b->max_len : 4096;
+    uint32_t lds = wave_lds(decompress != 0, max_len, b->max_out);
+    uint32_t stage = stage_bytes_for(max_len);
+    if (stage + kInStage + kMinArena > lds) { stage = 16; lds = 16384; }
+    if (decompress)
+        hipLaunchKernelGGL(rc_decompress_wave, dim3(b->n), dim3(64), lds, st, *b, *ws, stage, lds);
+    else
+        hipLaunchKernelGGL(rc_compress_wave, dim3(b->n), dim3(64), lds, st, *b, *ws, stage, lds);
+    return static_cast<int>(hipGetLastError());
 }
 
 static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
@@ -1154,8 +1188,18 @@ static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev
         fprintf(stderr, "enet_rc: %s n=%u max_len=%u cus=%u lds=%u small_max=%u -> %s\n",
                 decompress ? "decompress" : "compress", b->n, max_len, ws->cus, lds_w,
                 ws->small_max, small || ws->kernel == RC_KERNEL_WAVE ? "wave" : "lanes");
-    if (ws->kernel != RC_KERNEL_WAVE && !small) {
-        const int rc = rc_hip_lane_launch(decompress ? 1 : 0, b, ws, stream);
+    // (the decoder's tail on the wave kernel up to twice what fits at once: a
+    // second round of wave blocks still beats the lane kernels' full packet
+    // time for up to ~3000 low-entropy packets, profiles/r5_smallbatch.log)
+    uint32_t lds2;
+    rc_batch_dev half = *b;
+    half.n = (b->n + 1) / 2;
+    const bool tail2 = decompress && small_batch(decompress, &half, ws, lds2) && small_route(decompress, ws) == 2;
+    const int route = small ? small_route(decompress, ws) : tail2 ? 2 : 1;
+    if (ws->kernel != RC_KERNEL_WAVE && route != 0) {
+        rc_workspace_dev w = *ws;
+        w.wave_tail = route == 2 ? 1u : 0u;
+        const int rc = rc_hip_lane_launch(decompress ? 1 : 0, b, &w, stream);
         if (rc != 0) return rc;
     } else {
         uint32_t stage = stage_bytes_for(max_len);

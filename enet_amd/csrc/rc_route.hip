@@ -108,6 +108,8 @@ void rc_len_scatter(const uint32_t* len, uint32_t n, uint32_t* bins, uint32_t* o
 
 extern "C" int rc_hip_lane3_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
                                    uint32_t blocks, void* stream);   // rc_lane3.hip
+extern "C" int rc_hip_wave_tail_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
+                                       void* stream);                // rc_kernels.hip
 
 extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const rc_workspace_dev* ws,
                                   void* stream)
@@ -144,6 +146,9 @@ extern "C" int rc_hip_lane_launch(int decompress, const rc_batch_dev* b, const r
         if (rc != 0) return rc;
         w.sub_list = ws->enc2_list;
         w.sub_count = ws->counters + 3;
+        // a small batch: what the decoder leaves goes to the wave kernel
+        // (its model in LDS: faster than a lane's for a few packets)
+        if (ws->wave_tail) return rc_hip_wave_tail_launch(1, b, &w, stream);
     }
     return rc_hip_lane3_launch(decompress, b, &w, blocks, stream);
 }
