@@ -445,6 +445,13 @@ DEV ScanPf scan_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t idx)
 constexpr uint32_t kRst = 1u << 15;
 constexpr uint32_t kMaxNodesE2 = 4096 - 2;       // compress.c:150
 
+// bucket ends from the scatter's fill counters (start << 16 | elements)
+DEV uint4 bucket_ends(const uint4 c)
+{
+    return make_uint4((c.x >> 16) + (c.x & 0xFFFFu), (c.y >> 16) + (c.y & 0xFFFFu), (c.z >> 16) + (c.z & 0xFFFFu),
+                      (c.w >> 16) + (c.w & 0xFFFFu));
+}
+
 // The nodes compress.c creates at each position of a window scanned as a
 // packet (compress.c:68-88 via :286-337): position 0 the root's; a position
 // found nowhere (its record visits the root) creates the root's node at the
@@ -458,8 +465,8 @@ template <class S>
 DEV uint32_t reset_after(S& s, uint32_t n, uint32_t x0, uint32_t t)
 {
     uint8_t* inc = s.x;                                   // per position: nodes | 0x80 = root visit
-    const uint4 e4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
     const uint4 b4 = *reinterpret_cast<const uint4*>(&s.start[4 * t]);
+    const uint4 e4 = bucket_ends(*reinterpret_cast<const uint4*>(&s.cnt[4 * t]));
     wave_sync();
     *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(~0u, ~0u, ~0u, ~0u);   // the first root visit per byte
     wave_sync();
@@ -648,7 +655,7 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
         const uint32_t st = wave_incl_scan(mine) - mine;
         const uint4 s4 = make_uint4(st, st + a0, st + a0 + a1, st + a0 + a1 + a2);
         *reinterpret_cast<uint4*>(&s.start[4 * t]) = s4;
-        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
+        *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(s4.x << 16, s4.y << 16, s4.z << 16, s4.w << 16);
         wave_sync();
         E2P(2)
         *reinterpret_cast<uint4*>(&s.xmask[4 * t]) = z;
@@ -665,7 +672,7 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
         uint2* rec = reinterpret_cast<uint2*>(slot) + s0;
         for (uint32_t i = 1 + t; i < n; i += 4 * kScanThreads) {
             // (branch-free as above: reads, then atomics and starts, then writes)
-            uint32_t b3[4], ew[4], w[4], k[4], bb[4], st[4];
+            uint32_t b3[4], ew[4], w[4], k[4], bb[4], jr[4];
             bool ok[4];
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
@@ -688,25 +695,28 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
-                k[m] = atomicAdd(ok[m] ? &s.cnt[bb[m]] : &s.dummy[0], 1u);
-                st[m] = s.start[bb[m]];
+                // (start << 16 | rank: one atomic gives the slot and the rank)
+                const uint32_t r = atomicAdd(ok[m] ? &s.cnt[bb[m]] : &s.dummy[0], 1u);
+                jr[m] = r & 0xFFFFu;
+                k[m] = (r >> 16) + jr[m];
             }
 #pragma unroll
             for (uint32_t m = 0; m < 4; ++m) {
                 s.e[ok[m] ? k[m] : S::kDummyE] = w[m];
-                const uint32_t j = k[m] - st[m];
+                const uint32_t j = jr[m];
                 if (ok[m]) {
                     rec[w[m] & 2047] = make_uint2(j ? (1u | j << 3 | j << 9) : 0u, ((w[m] >> 11) & 255) << 24);
                     if (w[m] & kExc) atomicOr(&s.xmask[bb[m]], 1u << min(j, 31u));
                 }
             }
         }
+        E2P(3)
         const uint32_t x0 = x[0];
         wave_sync();
         const bool disorder = !ordered;                // (wave-uniform)
         if (!fetched) pf = scan_prefetch(b, e, idx + gridDim.x);     // (the bytes in LDS are not read past here)
         fetched = true;
-        E2P(3)
+        E2P(6)
         // buckets with exceptional positions: compacted over the lanes, one
         // per lane, each walked in full
         {
@@ -724,7 +734,7 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
 #pragma unroll 1
             for (uint32_t q = t; q < nx; q += kScanThreads) {
                 const uint32_t bk = s.xlist[q];
-                const uint32_t bs = s.start[bk], kk = s.cnt[bk] - bs;
+                const uint32_t bs = s.start[bk], kk = s.cnt[bk] & 0xFFFFu;
                 walk_from(s, bs, kk, s.xmask[bk], rec);
             }
         }
@@ -2337,7 +2347,21 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     e.wcount = ws->counters + 4;
     const uint64_t wcap = e.wide ? ws->enc2_wide_cap / e.wslot_bytes : 0;
     e.wcap = static_cast<uint32_t>(wcap < 0xFFFFFFFFull ? wcap : 0xFFFFFFFFull);
-    const uint32_t scan_blocks_max = ws->cus * 16;
+    // The scans' grids: 64 workgroups per CU, each wavefront looping over a few
+    // packets (4 on C2), although only 9-11 are resident per CU (LDS).
+    // Workgroups that start as others finish keep the resident wavefronts in
+    // different phases of their packets (counting atomics, scatter, walks),
+    // where wavefronts started together and looping over many packets stay in
+    // step and contend for the same unit: rocprof, C2 rc_enc2_scan_s 0.438 ms
+    // at 16 per CU, 0.510 at 11 (the resident count), 0.367 at 64, 0.361 at
+    // 128; C3 rc_enc2_wscan_s 1.767 -> 1.558 at 64 (1.505 at 256, but an empty
+    // wide launch then costs 20 us on C2).  Fewer pays where the scan lists
+    // most packets for the wide kernels (C3 rc_enc2_scan_s 0.125 -> 0.207 ms
+    // at 64: one list append per workgroup on one counter).  ENET_RC_SCAN_BPC:
+    // workgroups per CU instead (experiments)
+    static const char* bpc_env = getenv("ENET_RC_SCAN_BPC");
+    const int bpc = bpc_env ? atoi(bpc_env) : 0;
+    const uint32_t scan_blocks_max = ws->cus * (bpc > 0 ? static_cast<uint32_t>(bpc) : 64u);
     static const char* lanes = getenv("ENET_RC_ENC2_LANES");      // experiment: 32 packets per wavefront
     e.act = (lanes && atoi(lanes) == 32) ? 32u : 64u;
     e.slow = ws->enc2_slow;

@@ -6,7 +6,7 @@ import os
 import sys
 
 os.environ["ENET_RC_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "enet_amd", "lib",
-                                         "libenet_rc_amd_e2prof.so")
+                                         os.environ.get("E2_LIB", "libenet_rc_amd_e2prof.so"))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import torch  # noqa: E402
 from enet_amd import RangeCoder, compress_batch, synth, get_lib  # noqa: E402
@@ -27,7 +27,7 @@ with RangeCoder() as rc:
     compress_batch(rc, din, doff, dlen, max_len=1200)
     torch.cuda.synchronize()
     lib.rc_enc2_prof_read(buf, 1)
-names = ["load+zero", "hist+bigrams", "sizes", "scatter", "exceptional", "plain+end", "-", "-"]
+names = ["load+zero", "hist+bigrams", "sizes", "scatter", "exceptional", "plain+end", "prefetch", "-"]
 tot = sum(buf[k] for k in range(8))
 for k, nm in enumerate(names):
     print(f"{nm:14s} {buf[k] / n:10.0f} cycles/packet  {100.0 * buf[k] / max(tot, 1):5.1f} %")
