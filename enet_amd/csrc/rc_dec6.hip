@@ -589,7 +589,7 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
 // only, so that waiting for an atomic's return never waits for them).  Other
 // packets take verify_slow.
 constexpr uint32_t kVerifyWaves = 4;
-constexpr uint32_t kVerifyBlocksPerCu = 5;      // 32 KB of LDS per workgroup
+constexpr uint32_t kVerifyBlocksPerCu = 10;     // 32 KB of LDS per workgroup: 5 resident per CU, two rounds
 constexpr uint32_t kVerDw = 8;                  // dwords per lane: packets to 2 KB - 4
 
 // the header words of packet k, lane l < 5: claims, out_len, out_off (2), resets
@@ -782,9 +782,13 @@ extern "C" int rc_hip_dec6_verify_launch(const rc_batch_dev* b, const rc_workspa
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint32_t vb = (b->n + kVerifyWaves - 1) / kVerifyWaves;
-    // resident workgroups only: each wave then walks several packets, the
-    // next one's loads in flight
-    const uint32_t cap = (ws->cus ? ws->cus : 256u) * kVerifyBlocksPerCu;
+    // twice the resident workgroups: each wave walks several packets, the next
+    // one's loads in flight, and the second round starts as first-round
+    // workgroups finish (C2: 66 -> 60 us against the resident count, 72 at 64
+    // per CU; profiles/r5_scan_grid/vbpc_c2.txt)
+    static const char* vb_env = getenv("ENET_RC_VERIFY_BPC");     // (experiments: workgroups per CU)
+    const uint32_t bpc = vb_env && atoi(vb_env) > 0 ? static_cast<uint32_t>(atoi(vb_env)) : kVerifyBlocksPerCu;
+    const uint32_t cap = (ws->cus ? ws->cus : 256u) * bpc;
     hipLaunchKernelGGL(rc_dec6_verify, dim3(vb < cap ? vb : cap), dim3(256), 0, st, *b, *ws);
     return static_cast<int>(hipGetLastError());
 }
