@@ -1143,13 +1143,16 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
 #endif
 constexpr uint32_t kQPart = 4;                                   // positions per part
 constexpr uint32_t kQEntry = 16;                                 // bytes per queued position
-constexpr uint32_t kC2Mtab = 256 * kCodeLds;                     // helper roots, then tables
+constexpr uint32_t kQSlots = 4;                                  // parts in the queue: two filled while two drain
+constexpr uint32_t kC2Root = 304;                                // helper root stride (76 dwords: b128 conflict-free)
+constexpr uint32_t kC2Mtab = 256 * kC2Root;                      // helper roots, then tables
 constexpr uint32_t kC2Itab = kC2Mtab + 256;
 constexpr uint32_t kC2Ring = kC2Itab + 544;                      // (row 16 of the increment table: zeros); coder rings, 32 B per packet
-constexpr uint32_t kC2Queue = kC2Ring + 256 * 32;                // [2 parts][kQPart][256 packets] entries
-constexpr uint32_t kC2Max = kC2Queue + 2 * kQPart * 256 * kQEntry;   // the block's longest packet
+constexpr uint32_t kC2Queue = kC2Ring + 256 * 32;                // [kQSlots parts][kQPart][256 packets] entries
+constexpr uint32_t kC2Max = kC2Queue + kQSlots * kQPart * 256 * kQEntry;   // the block's longest packet
 constexpr uint32_t kC2Rcp = kC2Max + 16;                         // rcp64 of the sub-context totals
 constexpr uint32_t kC2Lds = kC2Rcp + 8 * kRcpTab;
+static_assert(kC2Lds <= 160 * 1024, "rc_enc2_code2's LDS");
 
 // barrier for the block's LDS traffic only (a workgroup fence would also wait
 // for the helpers' record loads and the coders' output stores)
@@ -1162,7 +1165,7 @@ DEV void lds_barrier()
 
 DEV uint8_t* q_entry(uint8_t* smem, uint32_t part, uint32_t j, uint32_t lane)
 {
-    return smem + kC2Queue + (((part & 1) * kQPart + j) * 256 + lane) * kQEntry;
+    return smem + kC2Queue + (((part & (kQSlots - 1)) * kQPart + j) * 256 + lane) * kQEntry;
 }
 
 DEV bool root_codes(uint32_t w0) { const uint32_t typ = w0 & 7; return typ <= 1 || typ == 3 || typ == 4; }
@@ -1294,39 +1297,39 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     if (helper) atomicMax(bmax, len);
     __syncthreads();
     const uint32_t parts = (*bmax + kQPart - 1) / kQPart;
+    // The queue holds four parts: the helpers fill two while the coders drain
+    // the other two, one block barrier per pair (one per part before round 5:
+    // the coders then waited ~0.5 k cycles a part at the barrier)
     if (helper) {
-        uint8_t* root = smem + lane * kCodeLds;
+        uint8_t* root = smem + lane * kC2Root;
         {
             Root R;
             root3_clear<true>(root, R);
         }
         uint32_t rtot = 1 + 256;
-        // records: a part is two 16-B chunks; two register sets, each reloaded
-        // right after its part is queued with the part two ahead
+        // records: a part is two 16-B chunks; two register sets (even and odd
+        // parts), each reloaded right after its part is queued with the part
+        // two ahead
         uint4 x0 = gload16(base), x1 = gload16(min(base + 16, slot_last));
         uint4 y0 = gload16(min(base + 32, slot_last)), y1 = gload16(min(base + 48, slot_last));
         __builtin_amdgcn_s_waitcnt(0);
-        // part 0 before the loop
+        // parts 0 and 1 before the loop
         help_part(root, mtab, itab, x0, x1, 0, len, rtot, smem, 0, lane);
         x0 = gload16(min(base + 64, slot_last));
         x1 = gload16(min(base + 80, slot_last));
+        help_part(root, mtab, itab, y0, y1, 4, len, rtot, smem, 1, lane);
+        y0 = gload16(min(base + 96, slot_last));
+        y1 = gload16(min(base + 112, slot_last));
         lds_barrier();
         C2P_DECL
         for (uint32_t s = 0; s < parts; s += 2) {
-            // part s + 1 (set y) while the coders drain part s
-            uint32_t i = 4 * (s + 1);
-            help_part(root, mtab, itab, y0, y1, i, len, rtot, smem, s + 1, lane);
-            y0 = gload16(min(base + 32 * (s + 3), slot_last));
-            y1 = gload16(min(base + 32 * (s + 3) + 16, slot_last));
-            C2P_WORK
-            lds_barrier();
-            C2P_WAIT
-            if (s + 1 >= parts) break;
-            // part s + 2 (set x) while the coders drain part s + 1
-            i = 4 * (s + 2);
-            help_part(root, mtab, itab, x0, x1, i, len, rtot, smem, s + 2, lane);
+            // parts s + 2 (set x) and s + 3 (set y) while the coders drain s, s + 1
+            help_part(root, mtab, itab, x0, x1, 4 * (s + 2), len, rtot, smem, s + 2, lane);
             x0 = gload16(min(base + 32 * (s + 4), slot_last));
             x1 = gload16(min(base + 32 * (s + 4) + 16, slot_last));
+            help_part(root, mtab, itab, y0, y1, 4 * (s + 3), len, rtot, smem, s + 3, lane);
+            y0 = gload16(min(base + 32 * (s + 5), slot_last));
+            y1 = gload16(min(base + 32 * (s + 5) + 16, slot_last));
             C2P_WORK
             lds_barrier();
             C2P_WAIT
@@ -1345,7 +1348,7 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     o.ca = dummy;
     CodeState k;
     k.rtot = 0; k.rrt = 0.0; k.low = 0; k.range = ~0u;
-    lds_barrier();                                    // part 0 queued
+    lds_barrier();                                    // parts 0 and 1 queued
     C2P_DECL
     for (uint32_t s = 0; s < parts; ++s) {
         const uint4 q0 = *reinterpret_cast<const uint4*>(q_entry(smem, s, 0, lane));
@@ -1362,9 +1365,12 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
         code_pos(k, o, q2, p2, r02, dummy);
         code_pos(k, o, q3, p3, r03, dummy);
         C2P_WORK
-        lds_barrier();                                // (the helpers may overwrite this part now)
-        C2P_WAIT
+        if (s & 1) {
+            lds_barrier();                            // (the helpers may overwrite parts s - 1, s now)
+            C2P_WAIT
+        }
     }
+    if (parts & 1) lds_barrier();                     // (the helpers' last barrier)
     C2P_FLUSH(10)
     ring_store(o);
     ring_chunk(o, o.n, dummy);                        // (nothing new: the next store goes to the dummy)
