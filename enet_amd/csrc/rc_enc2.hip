@@ -2290,6 +2290,135 @@ DEV void wcode_main(const rc_batch_dev& b, const E2Params& e)
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void rc_enc2_wcode(rc_batch_dev b, E2Params e) { wcode_main<false>(b, e); }
 
+// The wide code pass on a helper and a coder wavefront per packet, as
+// rc_enc2_code2 (one wavefront per packet: rc_enc2_wcode, 28 % slower on the
+// narrow records, 0.853 against 0.614 ms on C2): the helpers keep the root and
+// queue each position's root interval and total, the coders read the explicit
+// records themselves (two parts ahead; the helpers read them first, so they
+// come from the L2) and run the range coder.  Packets without model resets
+// (slot_len <= kE2MaxLen); rc_enc2_wcode_r takes the others.
+//
+// help_part's record words for two wide records: type 1 where the root codes
+// the byte, 2 where it does not (root_codes), no reset; the byte in w1
+DEV uint4 wide_as_plain(const uint4& ra, const uint4& rb)
+{
+    return make_uint4(((ra.w >> 17) & 1u) ? 1u : 2u, ((ra.y >> 16) & 255u) << 24,
+                      ((rb.w >> 17) & 1u) ? 1u : 2u, ((rb.y >> 16) & 255u) << 24);
+}
+
+// a part's four wide records (clamped to the slot: parts past the packet read its end)
+DEV void wload4(uintptr_t a, uintptr_t last, uint4* r)
+{
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) r[j] = gload16(min(a + 16 * j, last));
+}
+
+extern "C" __global__ __launch_bounds__(512)
+void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint8_t* mtab = smem + kC2Mtab;
+    const uint8_t* itab = smem + kC2Itab;
+    uint32_t* bmax = reinterpret_cast<uint32_t*>(smem + kC2Max);
+    const uint32_t nw = min(*e.wcount, e.wcap);
+    if (blockIdx.x * 256 >= nw) return;               // (the whole block)
+    const bool helper = threadIdx.x >= 256;
+    const uint32_t lane = threadIdx.x & 255;
+    if (threadIdx.x < 16) root3_mask_init(smem + kC2Mtab, threadIdx.x);
+    if (threadIdx.x < 16) root3_inc_init(smem + kC2Itab, threadIdx.x);
+    if (threadIdx.x == 16)
+        reinterpret_cast<uint4*>(smem + kC2Itab)[32] = reinterpret_cast<uint4*>(smem + kC2Itab)[33] = make_uint4(0u, 0u, 0u, 0u);
+    if (threadIdx.x == 0) *bmax = 0;
+    const uint32_t q = blockIdx.x * 256 + lane;
+    const bool live = q < nw;
+    const uint32_t pkt = live ? packet_of(e, e.wlist[q]) : 0u;
+    const uint32_t len = live ? b.in_len[pkt] : 0u;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(e.wide) + static_cast<size_t>(live ? q : 0u) * e.wslot_bytes;
+    const uintptr_t last = base + e.wslot_bytes - 16;
+    __syncthreads();
+    if (helper) atomicMax(bmax, len);
+    __syncthreads();
+    const uint32_t parts = (*bmax + kQPart - 1) / kQPart;
+    if (helper) {
+        uint8_t* root = smem + lane * kC2Root;
+        {
+            Root R;
+            root3_clear<true>(root, R);
+        }
+        uint32_t rtot = 1 + 256;
+        uint4 x[4], y[4];                             // even and odd parts' records
+        wload4(base, last, x);
+        wload4(base + 64, last, y);
+        __builtin_amdgcn_s_waitcnt(0);
+        help_part(root, mtab, itab, wide_as_plain(x[0], x[1]), wide_as_plain(x[2], x[3]), 0, len, rtot, smem, 0, lane);
+        wload4(base + 128, last, x);
+        help_part(root, mtab, itab, wide_as_plain(y[0], y[1]), wide_as_plain(y[2], y[3]), 4, len, rtot, smem, 1, lane);
+        wload4(base + 192, last, y);
+        lds_barrier();
+        for (uint32_t s = 0; s < parts; s += 2) {
+            help_part(root, mtab, itab, wide_as_plain(x[0], x[1]), wide_as_plain(x[2], x[3]), 4 * (s + 2), len, rtot,
+                      smem, s + 2, lane);
+            wload4(base + 64 * (s + 4), last, x);
+            help_part(root, mtab, itab, wide_as_plain(y[0], y[1]), wide_as_plain(y[2], y[3]), 4 * (s + 3), len, rtot,
+                      smem, s + 3, lane);
+            wload4(base + 64 * (s + 5), last, y);
+            lds_barrier();
+        }
+        return;
+    }
+    // coder
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(e.dummy) + ((blockIdx.x * 256u + lane) & 65535u) * 16u;
+    Ring o;
+    o.r = smem + kC2Ring + 32 * lane;
+    o.lo = reinterpret_cast<uintptr_t>(b.out + (live ? b.out_off[pkt] : 0));
+    o.n = 0;
+    o.cap = live ? b.out_cap[pkt] : 0u;
+    o.ch = make_uint4(0u, 0u, 0u, 0u);
+    o.ca = dummy;
+    CodeState k;
+    k.rtot = 0; k.rrt = 0.0; k.low = 0; k.range = ~0u;
+    uint4 x[4], y[4];                                 // this pair of parts' records
+    wload4(base, last, x);
+    wload4(base + 64, last, y);
+    lds_barrier();                                    // parts 0 and 1 queued
+    for (uint32_t s = 0; s < parts; s += 2) {
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            uint4* r = h ? y : x;
+            const uint32_t i = 4 * (s + h);
+            Pre p[4];
+            double r0[4];
+            uint4 qe[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                qe[j] = *reinterpret_cast<const uint4*>(q_entry(smem, s + h, j, lane));
+                p[j] = prep_wide(r[j], i + j < len);
+                r0[j] = rcp64(p[j].e0 ? qe[j].w : 1u);
+            }
+            wload4(base + 64 * (s + h + 2), last, r);     // (the pair after this one)
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) code_pos(k, o, qe[j], p[j], r0[j], dummy);
+        }
+        lds_barrier();                                // (the helpers may overwrite parts s, s + 1 now)
+    }
+    ring_store(o);
+    ring_chunk(o, o.n, dummy);
+    bool ok = live && o.n <= o.cap;
+    uint32_t low = k.low;
+    while (any_lane(ok && low != 0)) {
+        const bool more = ok && low != 0;
+        const bool full = more && o.n >= o.cap;
+        ok = ok && !full;
+        const uint32_t n0 = o.n;
+        ring_put(o, low, 1, more && !full);
+        low = (more && !full) ? low << 8 : low;
+        ring_chunk(o, n0, dummy);
+        ring_store(o);
+    }
+    ring_finish(o, ok);
+    if (live) b.out_len[pkt] = ok ? o.n : 0u;
+}
+
 // launches with packets over 1919 bytes: model resets (kWRst) and left packets (kWLeft)
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void rc_enc2_wcode_r(rc_batch_dev b, E2Params e) { wcode_main<true>(b, e); }
@@ -2400,7 +2529,10 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
                 hipLaunchKernelGGL(rc_enc2_wscan, g, dim3(kScanThreads), 0, st, *b, e);
             else
                 hipLaunchKernelGGL(rc_enc2_wscan_l, g, dim3(kScanThreads), 0, st, *b, e);
-            if (e.slot_len <= kE2MaxLen)
+            static const char* w1 = getenv("ENET_RC_WCODE1");            // the one-wavefront wide code pass (A/B)
+            if (e.slot_len <= kE2MaxLen && !(w1 && atoi(w1) == 1))
+                hipLaunchKernelGGL(rc_enc2_wcode2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
+            else if (e.slot_len <= kE2MaxLen)
                 hipLaunchKernelGGL(rc_enc2_wcode, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
             else
                 hipLaunchKernelGGL(rc_enc2_wcode_r, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
