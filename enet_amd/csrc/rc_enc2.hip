@@ -1125,9 +1125,9 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
 // the root in LDS and queue per position its record words with the root's
 // interval and total at that position (a 16-B entry); wavefronts 0-3
 // (coders) prepare the sub-context intervals from the record words and run
-// the range coder and the output ring.  The queue holds two parts of four
-// positions per packet: the helpers fill one while the coders drain the
-// other, a block barrier between parts.  With two wavefronts per SIMD the
+// the range coder and the output ring.  The queue holds four parts of four
+// positions per packet: the helpers fill two while the coders drain the
+// other two, a block barrier between pairs.  With two wavefronts per SIMD the
 // SIMD issues a vector instruction every 2 cycles instead of every 4 for one
 // wavefront alone.
 #ifdef E2_PROF
