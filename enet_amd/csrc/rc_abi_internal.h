@@ -56,7 +56,8 @@ typedef struct {
     uint64_t  enc2_cap;     /* bytes */
     uint32_t *enc2_list;    /* [n_cap] */
     /* its wide mode (packets with a bucket over 64 positions): 16-B records per position,
-       one slot per packet listed in enc2_wlist (count counters[4]); NULL: off (ENET_RC_ENC2_WIDE=0) */
+       one slot per packet listed in enc2_wlist (RC_WSHARDS regions, counts at counters +
+       RC_WSHARD_AT); NULL: off (ENET_RC_ENC2_WIDE=0) */
     void     *enc2_wide;
     uint64_t  enc2_wide_cap;  /* bytes */
     uint32_t *enc2_wlist;     /* [n_cap] */
@@ -94,7 +95,12 @@ typedef struct {
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */
 #define RC_LEN_TICKET (RC_LEN_BINS + 1u)   /* bins[]: rc_len_hist's workgroups done */
-#define RC_CTL_WORDS (8u + ((RC_LEN_TICKET + 1u + 3u) & ~3u))   /* counters[8], bins: 16-B multiple */
+#define RC_CTL_BINS_END (8u + ((RC_LEN_TICKET + 1u + 3u) & ~3u))   /* counters[8], bins: 16-B multiple */
+/* the wide list's counters (rc_enc2.hip): RC_WSHARDS of them, 128 B apart, after the bins */
+#define RC_WSHARDS 8u
+#define RC_WSHARD_STRIDE 32u
+#define RC_WSHARD_AT ((RC_CTL_BINS_END + 31u) & ~31u)
+#define RC_CTL_WORDS (RC_WSHARD_AT + RC_WSHARDS * RC_WSHARD_STRIDE)
 #define RC_KERNEL_WAVE 1u   /* one packet per wavefront */
 #define RC_KERNEL_LANE3 2u  /* one packet per lane, model v3 (rc_lane3.hip, default) */
 

@@ -120,13 +120,61 @@ struct E2Params {
     // wide mode (below): packets with a bucket over kE2Bucket positions
     uint8_t*        wide;       // wide record stream, one slot per listed packet, or null (off)
     uint64_t        wslot_bytes;
-    uint32_t*       wlist;      // listed packets (batch indices), count *wcount, at most wcap slots
-    uint32_t*       wcount;
+    uint32_t*       wlist;      // listed packets (batch indices): RC_WSHARDS regions of wcap / RC_WSHARDS
+    uint32_t*       wcount;     // the regions' counts, RC_WSHARD_STRIDE words apart
     uint32_t        wcap;
+    uint32_t        wreg;       // entries per region: min(wcap, the chunk rounded up to RC_WSHARDS) / RC_WSHARDS
 };
 
 // the last element slot: buckets of 1918 positions, each padded to 4, end
 // below it (1918 + 3 * 255 < 2815); lanes past a packet's end write there
+
+// The wide list in RC_WSHARDS regions, each with its own counter (a
+// workgroup appends to region blockIdx.x % RC_WSHARDS): one counter for the
+// batch took one atomic per scan workgroup on one address, C3
+// rc_enc2_scan_s 0.125 -> 0.207 ms at 64 workgroups per CU.  List position q
+// (region q / C, C = e.wreg) is live when its region holds it; the wide
+// stream's slot of a listed packet is its list position.  A scan grid that
+// is a multiple of RC_WSHARDS (or one packet per workgroup) sends region r
+// only packets whose chunk index is r modulo RC_WSHARDS, so a chunk's wide
+// packets always fit when the stream has a slot per packet; past a region's
+// capacity a packet goes to the lane kernels.
+DEV uint32_t wreg_cap(const E2Params& e) { return e.wreg; }
+DEV uint32_t wreg_count(const E2Params& e, uint32_t r) { return min(e.wcount[r * RC_WSHARD_STRIDE], wreg_cap(e)); }
+DEV bool wq_live(const E2Params& e, uint32_t q)
+{
+    const uint32_t C = wreg_cap(e);
+    if (C == 0) return false;
+    const uint32_t r = q / C;
+    return r < RC_WSHARDS && q - r * C < wreg_count(e, r);
+}
+// the live list positions in order: d -> its position (d < the live count)
+struct WRegs { uint32_t pre[RC_WSHARDS + 1]; };
+DEV WRegs wregs(const E2Params& e)
+{
+    WRegs w;
+    w.pre[0] = 0;
+    for (uint32_t r = 0; r < RC_WSHARDS; ++r) w.pre[r + 1] = w.pre[r] + wreg_count(e, r);
+    return w;
+}
+DEV uint32_t wq_of(const E2Params& e, const WRegs& w, uint32_t d)
+{
+    uint32_t r = 0;
+    for (uint32_t k = 1; k < RC_WSHARDS; ++k) r += d >= w.pre[k] ? 1u : 0u;
+    return r * wreg_cap(e) + (d - w.pre[r]);
+}
+
+// list positions [q0, q0 + m): any live (wave-uniform arguments)
+DEV bool wq_any(const E2Params& e, uint32_t q0, uint32_t m)
+{
+    const uint32_t C = wreg_cap(e);
+    bool any = false;
+    for (uint32_t r = 0; r < RC_WSHARDS; ++r) {
+        const uint32_t lo = r * C, hi = lo + wreg_count(e, r);
+        any = any || (q0 < hi && q0 + m > lo);
+    }
+    return any;
+}
 
 DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 {
@@ -190,6 +238,68 @@ DEV uint32_t wave_max(uint32_t x)
     return __builtin_amdgcn_readlane(x, 63);
 }
 
+DEV uint32_t lane_id() { return threadIdx.x & 63; }
+DEV uint64_t below_mask() { return (1ull << lane_id()) - 1ull; }
+DEV uint32_t popc64(uint64_t m) { return static_cast<uint32_t>(__builtin_popcountll(m)); }
+
+// The lanes of `act` whose 8-bit key equals this lane's, from eight ballots
+// (one per key bit: at each bit, keep the lanes that agree with this lane);
+// lt: how many lanes below this one (of `act`) hold a smaller key (counted at
+// the highest bit where they differ).  No LDS, no atomics, any number of
+// distinct keys.
+DEV uint64_t match8(uint32_t key, uint64_t act, uint32_t& lt)
+{
+    const uint64_t below = below_mask();
+    uint64_t e = act;
+    lt = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const bool one = (key >> b) & 1u;
+        const uint64_t B = __builtin_amdgcn_ballot_w64(one);
+        lt += one ? popc64(e & ~B & below) : 0u;
+        e &= one ? B : ~B;
+    }
+    return e;
+}
+
+// match8 against ballots taken once (B[b] = lanes with key bit b set):
+// several matches on the same key share them
+struct KeyBits { uint64_t b[8]; };
+DEV KeyBits key_bits(uint32_t key)
+{
+    KeyBits k;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) k.b[b] = __builtin_amdgcn_ballot_w64((key >> b) & 1u);
+    return k;
+}
+DEV uint64_t match_bits(uint32_t key, const KeyBits& kb, uint64_t e, uint32_t& lt)
+{
+    const uint64_t below = below_mask();
+    lt = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const bool one = (key >> b) & 1u;
+        lt += one ? popc64(e & ~kb.b[b] & below) : 0u;
+        e &= one ? kb.b[b] : ~kb.b[b];
+    }
+    return e;
+}
+
+// match_bits as masks: the lanes of e with this lane's key (returned) and,
+// in ltm, the lanes of e with a smaller key -- counts over any subset of e
+// are then popcounts
+DEV uint64_t match_bits_lt(uint32_t key, const KeyBits& kb, uint64_t e, uint64_t& ltm)
+{
+    ltm = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+        const bool one = (key >> b) & 1u;
+        ltm |= one ? (e & ~kb.b[b]) : 0ull;
+        e &= one ? kb.b[b] : ~kb.b[b];
+    }
+    return e;
+}
+
 DEV bool bit_at(const uint32_t* m, uint32_t i) { return (m[i >> 5] >> (i & 31)) & 1; }
 
 // bytes q-2, q-1, q of the LDS byte array xb (q >= 4) in bits 0-23: two
@@ -251,14 +361,15 @@ DEV void wb_flush(S& s, const E2Params& e, uint32_t t)
     const uint32_t k = s.nwb;
     if (k == 0) return;
     uint32_t base = 0;
-    if (t == 0) base = atomicAdd(e.wcount, k);
+    const uint32_t r = blockIdx.x % RC_WSHARDS, C = wreg_cap(e);
+    if (t == 0) base = atomicAdd(e.wcount + r * RC_WSHARD_STRIDE, k);
     base = __shfl(base, 0, 64);
     if (t < k) {
         const uint32_t idx = s.wb[t];
         uint32_t* slot = reinterpret_cast<uint32_t*>(e.stream + static_cast<size_t>(idx - e.lo) * e.slot_bytes);
-        if (base + t < e.wcap) {
+        if (base + t < C) {
             slot[0] = kSkipWide;
-            e.wlist[base + t] = idx;
+            e.wlist[r * C + base + t] = idx;
         } else {
             slot[0] = kSkipFallback;
             e.list[atomicAdd(e.count, 1u)] = packet_of(e, idx);
@@ -1456,68 +1567,6 @@ struct WScanLdsT {
 };
 
 
-DEV uint32_t lane_id() { return threadIdx.x & 63; }
-DEV uint64_t below_mask() { return (1ull << lane_id()) - 1ull; }
-DEV uint32_t popc64(uint64_t m) { return static_cast<uint32_t>(__builtin_popcountll(m)); }
-
-// The lanes of `act` whose 8-bit key equals this lane's, from eight ballots
-// (one per key bit: at each bit, keep the lanes that agree with this lane);
-// lt: how many lanes below this one (of `act`) hold a smaller key (counted at
-// the highest bit where they differ).  No LDS, no atomics, any number of
-// distinct keys.
-DEV uint64_t match8(uint32_t key, uint64_t act, uint32_t& lt)
-{
-    const uint64_t below = below_mask();
-    uint64_t e = act;
-    lt = 0;
-#pragma unroll
-    for (int b = 7; b >= 0; --b) {
-        const bool one = (key >> b) & 1u;
-        const uint64_t B = __builtin_amdgcn_ballot_w64(one);
-        lt += one ? popc64(e & ~B & below) : 0u;
-        e &= one ? B : ~B;
-    }
-    return e;
-}
-
-// match8 against ballots taken once (B[b] = lanes with key bit b set):
-// several matches on the same key share them
-struct KeyBits { uint64_t b[8]; };
-DEV KeyBits key_bits(uint32_t key)
-{
-    KeyBits k;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) k.b[b] = __builtin_amdgcn_ballot_w64((key >> b) & 1u);
-    return k;
-}
-DEV uint64_t match_bits(uint32_t key, const KeyBits& kb, uint64_t e, uint32_t& lt)
-{
-    const uint64_t below = below_mask();
-    lt = 0;
-#pragma unroll
-    for (int b = 7; b >= 0; --b) {
-        const bool one = (key >> b) & 1u;
-        lt += one ? popc64(e & ~kb.b[b] & below) : 0u;
-        e &= one ? kb.b[b] : ~kb.b[b];
-    }
-    return e;
-}
-
-// match_bits as masks: the lanes of e with this lane's key (returned) and,
-// in ltm, the lanes of e with a smaller key -- counts over any subset of e
-// are then popcounts
-DEV uint64_t match_bits_lt(uint32_t key, const KeyBits& kb, uint64_t e, uint64_t& ltm)
-{
-    ltm = 0;
-#pragma unroll
-    for (int b = 7; b >= 0; --b) {
-        const bool one = (key >> b) & 1u;
-        ltm |= one ? (e & ~kb.b[b]) : 0ull;
-        e &= one ? kb.b[b] : ~kb.b[b];
-    }
-    return e;
-}
-
 // cnt[key] += 1 for every lane with ok: one LDS atomic per distinct key (its
 // lowest lane adds the group's size).  RET: returns the lane's slot, the old
 // value plus its rank among the lanes with its key (lane order).
@@ -1894,12 +1943,13 @@ struct WPf {
     uint4 r0, r1;
 };
 
-DEV WPf wide_prefetch(const rc_batch_dev& b, const E2Params& e, uint32_t q, uint32_t nw)
+DEV WPf wide_prefetch(const rc_batch_dev& b, const E2Params& e, const WRegs& w, uint32_t d)
 {
     WPf f;
     f.n = 0; f.mis = 0;
     uintptr_t a0 = reinterpret_cast<uintptr_t>(b.in) & ~static_cast<uintptr_t>(15), a1 = a0;
-    if (q < nw) {
+    if (d < w.pre[RC_WSHARDS]) {
+        const uint32_t q = wq_of(e, w, d);
         const uint32_t idx = const_load(e.wlist, q);
         const uint32_t pkt = (e.order && !const_load(e.bins, RC_LEN_BINS)) ? const_load(e.order, idx) : idx;
         f.n = const_load(b.in_len, pkt);
@@ -1986,7 +2036,8 @@ template <uint32_t L>
 DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
 {
     const uint32_t t = threadIdx.x;
-    const uint32_t nw = min(*e.wcount, e.wcap);
+    const WRegs wr = wregs(e);                        // the live list positions: d < nw
+    const uint32_t nw = wr.pre[RC_WSHARDS];
     // The stable scatters (elements into buckets in position order, a big
     // bucket's elements into runs) take one LDS atomic per lane where
     // same-address atomics apply in lane order (as in scan_main: gfx950,
@@ -1998,9 +2049,10 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
 #endif
     W2Prof wp;
     W2P_INIT
-    WPf pf = wide_prefetch(b, e, blockIdx.x, nw);
-    for (uint32_t q = blockIdx.x; q < nw; q += gridDim.x) {
+    WPf pf = wide_prefetch(b, e, wr, blockIdx.x);
+    for (uint32_t d = blockIdx.x; d < nw; d += gridDim.x) {
         const WPf cur = pf;
+        const uint32_t q = wq_of(e, wr, d);           // the list position
         const uint32_t len = cur.n;                   // (1 <= len <= slot_len: rc_enc2_scan)
         uint2* wrec0 = reinterpret_cast<uint2*>(e.wide + static_cast<size_t>(q) * e.wslot_bytes);
         const bool track = len > kE2MaxLen;           // (wave-uniform) the model can reset
@@ -2086,7 +2138,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         }
         const uint32_t x0 = s.x[q0];
         wave_sync();
-        if (!fetched) pf = wide_prefetch(b, e, q + gridDim.x, nw);  // (the next packet, while this one is walked)
+        if (!fetched) pf = wide_prefetch(b, e, wr, d + gridDim.x);  // (the next packet, while this one is walked)
         fetched = true;
         W2P(3)
         // buckets of <= kE2Bucket elements, whole buckets per round
@@ -2226,10 +2278,9 @@ DEV void wcode_main(const rc_batch_dev& b, const E2Params& e)
     if (threadIdx.x < 16) root3_mask_init(smem + kCodeMtab, threadIdx.x);
     if (threadIdx.x < 16) root3_inc_init(smem + kCodeItab, threadIdx.x);
     __syncthreads();
-    const uint32_t nw = min(*e.wcount, e.wcap);
     const uint32_t q = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x * 256 >= nw) return;               // (wave-uniform for whole blocks)
-    const bool live = q < nw;
+    if (!wq_any(e, blockIdx.x * 256, 256)) return;    // (the whole block)
+    const bool live = wq_live(e, q);
     const uint32_t pkt = live ? packet_of(e, e.wlist[q]) : 0u;
     const uint32_t len0 = live ? b.in_len[pkt] : 0u;
     const uintptr_t base = reinterpret_cast<uintptr_t>(e.wide) + static_cast<size_t>(live ? q : 0u) * e.wslot_bytes;
@@ -2320,8 +2371,7 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
     const uint8_t* mtab = smem + kC2Mtab;
     const uint8_t* itab = smem + kC2Itab;
     uint32_t* bmax = reinterpret_cast<uint32_t*>(smem + kC2Max);
-    const uint32_t nw = min(*e.wcount, e.wcap);
-    if (blockIdx.x * 256 >= nw) return;               // (the whole block)
+    if (!wq_any(e, blockIdx.x * 256, 256)) return;    // (the whole block)
     const bool helper = threadIdx.x >= 256;
     const uint32_t lane = threadIdx.x & 255;
     if (threadIdx.x < 16) root3_mask_init(smem + kC2Mtab, threadIdx.x);
@@ -2330,7 +2380,7 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
         reinterpret_cast<uint4*>(smem + kC2Itab)[32] = reinterpret_cast<uint4*>(smem + kC2Itab)[33] = make_uint4(0u, 0u, 0u, 0u);
     if (threadIdx.x == 0) *bmax = 0;
     const uint32_t q = blockIdx.x * 256 + lane;
-    const bool live = q < nw;
+    const bool live = wq_live(e, q);
     const uint32_t pkt = live ? packet_of(e, e.wlist[q]) : 0u;
     const uint32_t len = live ? b.in_len[pkt] : 0u;
     const uintptr_t base = reinterpret_cast<uintptr_t>(e.wide) + static_cast<size_t>(live ? q : 0u) * e.wslot_bytes;
@@ -2455,7 +2505,7 @@ extern "C" uint64_t rc_hip_enc2_wide_slot_bytes(uint32_t max_len)
 // Both passes over the batch, in chunks that fit the record stream; packets
 // off the fast path end up in ws->enc2_list / counters[3] for the lane kernels.
 // Per chunk: rc_enc2_scan, rc_enc2_code2 (narrow packets), then the wide
-// kernels over the packets the scan listed for them (counters[4]).
+// kernels over the packets the scan listed for them (the wide list's regions).
 extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -2479,7 +2529,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     e.wslot_bytes = rc_hip_enc2_wide_slot_bytes(ml);
     e.wide = ws->enc2_wide && ws->enc2_wide_cap >= e.wslot_bytes ? static_cast<uint8_t*>(ws->enc2_wide) : nullptr;
     e.wlist = ws->enc2_wlist;
-    e.wcount = ws->counters + 4;
+    e.wcount = ws->counters + RC_WSHARD_AT;
     const uint64_t wcap = e.wide ? ws->enc2_wide_cap / e.wslot_bytes : 0;
     e.wcap = static_cast<uint32_t>(wcap < 0xFFFFFFFFull ? wcap : 0xFFFFFFFFull);
     // The scans' grids: 64 workgroups per CU, each wavefront looping over a few
@@ -2505,8 +2555,12 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         e.lo = static_cast<uint32_t>(lo);
         e.hi = static_cast<uint32_t>(hi);
         const uint32_t cnt = static_cast<uint32_t>(hi - lo);
+        {
+            const uint32_t per = (cnt + RC_WSHARDS - 1) / RC_WSHARDS, cap = e.wcap / RC_WSHARDS;
+            e.wreg = per < cap ? per : cap;
+        }
         if (lo > 0 && e.wide) {                        // (the batch's memset cleared it for the first chunk)
-            const hipError_t err = hipMemsetAsync(e.wcount, 0, sizeof(uint32_t), st);
+            const hipError_t err = hipMemsetAsync(e.wcount, 0, RC_WSHARDS * RC_WSHARD_STRIDE * sizeof(uint32_t), st);
             if (err != hipSuccess) return static_cast<int>(err);
         }
         if (e.slot_len <= kWideSmallL)

@@ -207,9 +207,10 @@ static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
         c->ws.enc2_cap = want;
     }
     if (c->enc2_wide_on) {
-        /* a slot per packet of a chunk */
+        /* a slot per packet of a chunk, and the rounding of its RC_WSHARDS
+           list regions (rc_enc2.hip wreg_cap) */
         const uint64_t wslot = rc_hip_enc2_wide_slot_bytes(ml);
-        uint64_t wwant = (want / slot) * wslot;
+        uint64_t wwant = (want / slot + RC_WSHARDS) * wslot;
         const uint64_t wcap = c->enc2_wide_max;
         if (wwant > wcap) wwant = wcap > wslot ? wcap : wslot;
         if (wwant > c->ws.enc2_wide_cap) {

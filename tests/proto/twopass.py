@@ -102,66 +102,6 @@ def scan(p: bytes):
     return prim, ext
 
 
-def scan_masks(p: bytes):
-    """Pass 1 as rc_enc2.hip's xbuckets_ballot computes it for the buckets with
-    exceptional positions: a bucket's elements side by side (one per lane, in
-    position order), every statistic a count over lane masks -- mine (the
-    bucket), ctx2 (mine with my a), eq / lt (mine with my / a smaller v), F2 /
-    F1 (the lanes found at order 2 / 1) -- with no element after another.
-    Same result as scan()."""
-    n = len(p)
-    if n == 0 or n > MAX_LEN:
-        return None
-    buckets = defaultdict(list)
-    for i in range(1, n):
-        buckets[p[i - 1]].append(i)
-    if buckets and max(len(v) for v in buckets.values()) > MAX_BUCKET:
-        return None
-    prim = [0] * n
-    ext = [0] * n
-    popc = lambda m: bin(m).count("1")  # noqa: E731
-    for lst in buckets.values():
-        k = len(lst)
-        mine = (1 << k) - 1
-        below = [(1 << j) - 1 for j in range(k)]
-        has = [i >= 2 for i in lst]
-        ctx2 = [sum(1 << q for q in range(k) if has[j] and has[q] and p[lst[q] - 2] == p[i - 2]) & mine
-                for j, i in enumerate(lst)]
-        eq = [sum(1 << q for q in range(k) if p[lst[q]] == p[i]) for i in lst]
-        lt = [sum(1 << q for q in range(k) if p[lst[q]] < p[i]) for i in lst]
-        f2 = [(eq[j] & ctx2[j] & below[j]) != 0 for j in range(k)]
-        F2 = sum(1 << j for j in range(k) if f2[j])
-        vis1 = mine & ~F2
-        f1 = [not f2[j] and (eq[j] & vis1 & below[j]) != 0 for j in range(k)]
-        F1 = sum(1 << j for j in range(k) if f1[j])
-        for j, i in enumerate(lst):
-            b = below[j]
-            t2, same2, less2 = popc(ctx2[j] & b), popc(eq[j] & ctx2[j] & b), popc(lt[j] & ctx2[j] & b)
-            dist2 = popc(ctx2[j] & b & ~F2)
-            t1 = same1 = less1 = dist1 = 0
-            if not f2[j]:
-                t1, same1, less1 = popc(vis1 & b), popc(eq[j] & vis1 & b), popc(lt[j] & vis1 & b)
-                dist1 = popc(vis1 & b & ~F1)
-            if f2[j]:
-                typ, a, e = 6, (t2, dist2), (same2, less2)
-            elif t2 > 0:
-                if t1 == 0:
-                    typ, a, e = 3, (t2, dist2), ()
-                elif f1[j]:
-                    typ, a, e = 5, (t2, dist2), (t1, dist1, same1, less1)
-                else:
-                    typ, a, e = 4, (t2, dist2), (t1, dist1)
-            elif t1 == 0:
-                typ, a, e = 0, (0, 0), ()
-            elif f1[j]:
-                typ, a, e = 2, (t1, dist1), (same1, less1)
-            else:
-                typ, a, e = 1, (t1, dist1), ()
-            prim[i] = typ | a[0] << 3 | a[1] << 9
-            ext[i] = sum(f << (6 * q) for q, f in enumerate(e))
-    return prim, ext
-
-
 class _Enc:
     """compress.c:114-146 (carry-less range coder, output bounded by out_limit)."""
 

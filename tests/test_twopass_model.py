@@ -68,24 +68,6 @@ def test_gamestate_prefixes(port):
     assert fast > 10
 
 
-def test_element_parallel_statistics():
-    """rc_enc2.hip's xbuckets_ballot (lane masks, a bucket's elements side by
-    side) gives every position the record the element-by-element walk does."""
-    rng = np.random.default_rng(5)
-    d, o, l = synth.random_batch(6, 1200)
-    pk = [d[int(o[i]): int(o[i]) + 1200].tobytes() for i in range(6)]
-    pk += [rng.integers(0, a, size=int(rng.integers(2, 600)), dtype=np.uint8).tobytes()
-           for a in (3, 7, 16, 40) for _ in range(4)]
-    checked = 0
-    for p in pk:
-        r = twopass.scan(p)
-        if r is None:
-            continue
-        checked += 1
-        assert twopass.scan_masks(p) == r
-    assert checked >= 10
-
-
 def test_fast_path_limits():
     assert twopass.scan(b"") is None
     assert twopass.scan(bytes(1920)) is None                  # long: possible model reset
