@@ -2405,6 +2405,7 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
         help_part(root, mtab, itab, wide_as_plain(y[0], y[1]), wide_as_plain(y[2], y[3]), 4, len, rtot, smem, 1, lane);
         wload4(base + 192, last, y);
         lds_barrier();
+        C2P_DECL
         for (uint32_t s = 0; s < parts; s += 2) {
             help_part(root, mtab, itab, wide_as_plain(x[0], x[1]), wide_as_plain(x[2], x[3]), 4 * (s + 2), len, rtot,
                       smem, s + 2, lane);
@@ -2412,8 +2413,11 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
             help_part(root, mtab, itab, wide_as_plain(y[0], y[1]), wide_as_plain(y[2], y[3]), 4 * (s + 3), len, rtot,
                       smem, s + 3, lane);
             wload4(base + 64 * (s + 5), last, y);
+            C2P_WORK
             lds_barrier();
+            C2P_WAIT
         }
+        C2P_FLUSH(8)
         return;
     }
     // coder
@@ -2431,6 +2435,7 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
     wload4(base, last, x);
     wload4(base + 64, last, y);
     lds_barrier();                                    // parts 0 and 1 queued
+    C2P_DECL
     for (uint32_t s = 0; s < parts; s += 2) {
 #pragma unroll
         for (uint32_t h = 0; h < 2; ++h) {
@@ -2449,8 +2454,11 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) code_pos(k, o, qe[j], p[j], r0[j], dummy);
         }
+        C2P_WORK
         lds_barrier();                                // (the helpers may overwrite parts s, s + 1 now)
+        C2P_WAIT
     }
+    C2P_FLUSH(10)
     ring_store(o);
     ring_chunk(o, o.n, dummy);
     bool ok = live && o.n <= o.cap;
