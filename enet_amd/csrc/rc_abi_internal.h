@@ -45,8 +45,8 @@ typedef struct {
     uint32_t  kernel;       /* RC_KERNEL_* */
     uint32_t  lane_active;  /* lane kernels: packets per wavefront (64, 32 or 16) */
     uint32_t *order;        /* [n_cap] processing order (packets binned by length), lane kernels */
-    uint32_t *bins;         /* [RC_LEN_BINS + 2] length-bin counters, uniform flag, the binning's
-                               ticket; = counters + 8 (one control block, RC_CTL_WORDS, cleared
+    uint32_t *bins;         /* length-bin counts [RC_LEN_BINS], uniform flag, fill counters at
+                               RC_LEN_FILL; = counters + 8 (one control block, RC_CTL_WORDS, cleared
                                by one fill per call) */
     uint32_t  cus;          /* compute units of the device */
     uint32_t  small_max;    /* lane3 contexts: batches of up to this many packets (and no more than
@@ -94,8 +94,8 @@ typedef struct {
                                      (the 16-B records of all lanes first, then the rest: rc_dec6_rare.h) */
 
 #define RC_LEN_BINS 256u     /* 16-byte length bins, longest first; 4096 B / 16 */
-#define RC_LEN_TICKET (RC_LEN_BINS + 1u)   /* bins[]: rc_len_hist's workgroups done */
-#define RC_CTL_BINS_END (8u + ((RC_LEN_TICKET + 1u + 3u) & ~3u))   /* counters[8], bins: 16-B multiple */
+#define RC_LEN_FILL (RC_LEN_BINS + 4u)     /* bins[]: rc_len_scatter's fill counters, one per bin */
+#define RC_CTL_BINS_END (8u + RC_LEN_FILL + RC_LEN_BINS)   /* counters[8], bins (counts, uniform flag, fills) */
 /* the wide list's counters (rc_enc2.hip): RC_WSHARDS of them, 128 B apart, after the bins */
 #define RC_WSHARDS 8u
 #define RC_WSHARD_STRIDE 32u

@@ -20,37 +20,37 @@ __device__ __forceinline__ uint32_t len_bin(uint32_t len)
 
 constexpr uint32_t kBinChunk = 1024;     // packets per binning workgroup (4 per thread: 64 workgroups for 64 Ki packets)
 
-// Wave-aggregated LDS histogram of one element per lane: lanes that share a
-// bin are served by one LDS atomic (uniform batches take a single pass).
-// Returns the element's rank among the workgroup's elements of its bin.
+// LDS histogram of one element per lane; returns the element's rank among
+// the workgroup's elements of its bin (any order inside a bin).  A
+// wavefront whose elements share one bin (uniform batches) takes a single
+// LDS atomic; a ragged one takes one per lane (the LDS serialises the lanes
+// of one address in hardware: a loop over the wavefront's distinct bins --
+// ~50 for C4's lengths -- cost 81 + 57 us per binning of 1 Mi packets).
 __device__ __forceinline__ uint32_t bin_rank(uint32_t* hist, uint32_t bin, bool valid)
 {
-    uint64_t rem = __ballot(valid);
-    const uint64_t below = (1ull << (threadIdx.x & 63)) - 1;
-    uint32_t rank = 0;
-    while (rem) {
-        const int leader = __ffsll(static_cast<unsigned long long>(rem)) - 1;
-        const uint32_t lb = __shfl(bin, leader);
-        const bool mine = valid && bin == lb;
-        const uint64_t peers = __ballot(mine);
+    const uint64_t vm = __ballot(valid);
+    if (vm == 0) return 0;
+    const int leader = __ffsll(static_cast<unsigned long long>(vm)) - 1;
+    const uint32_t lb = __shfl(bin, leader);
+    if (__ballot(valid && bin != lb) == 0) {
+        const uint64_t below = (1ull << (threadIdx.x & 63)) - 1;
         uint32_t base = 0;
         if ((threadIdx.x & 63) == static_cast<uint32_t>(leader))
-            base = atomicAdd(&hist[lb], static_cast<uint32_t>(__popcll(peers)));
+            base = atomicAdd(&hist[lb], static_cast<uint32_t>(__popcll(vm)));
         base = __shfl(base, leader);
-        if (mine) rank = base + static_cast<uint32_t>(__popcll(peers & below));
-        rem &= ~peers;
+        return valid ? base + static_cast<uint32_t>(__popcll(vm & below)) : 0u;
     }
-    return rank;
+    return valid ? atomicAdd(&hist[bin], 1u) : 0u;
 }
 
-// The histogram, then -- in the workgroup that finishes last (its ticket in
-// bins[RC_LEN_TICKET], cleared with the counters by launch()) -- the exclusive
-// prefix over the bins; bins[RC_LEN_BINS] = 1 when every packet falls in one
-// bin (uniform lengths: the lane kernels then keep batch order).
+// The histogram: each workgroup's counts added into bins[0, RC_LEN_BINS)
+// (cleared with the counters by launch()).  (Until round 5 the workgroup that
+// finished last also turned the counts into bin starts: a ticket, a fence
+// and a 256-entry scan behind every other workgroup, 9.6 us of a 14-us
+// binning per call; rc_len_scatter now scans the counts itself.)
 extern "C" __global__ __launch_bounds__(RC_LEN_BINS) void rc_len_hist(const uint32_t* len, uint32_t n, uint32_t* bins)
 {
     __shared__ uint32_t h[RC_LEN_BINS];
-    __shared__ uint32_t last;
     h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * kBinChunk;
@@ -60,48 +60,50 @@ extern "C" __global__ __launch_bounds__(RC_LEN_BINS) void rc_len_hist(const uint
     }
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(&bins[RC_LEN_TICKET], 1u) == gridDim.x - 1 ? 1u : 0u;
-    __syncthreads();
-    if (!last) return;
-    // every workgroup's counts are in: the scan (atomic reads: device-coherent)
-    const uint32_t t = threadIdx.x;
-    const uint32_t mine = atomicAdd(&bins[t], 0u);
-    h[t] = mine;
-    const int used = __syncthreads_count(mine != 0);
-    for (uint32_t d = 1; d < RC_LEN_BINS; d <<= 1) {
-        const uint32_t x = t >= d ? h[t - d] : 0u;
-        __syncthreads();
-        h[t] += x;
-        __syncthreads();
-    }
-    bins[t] = h[t] - mine;               // exclusive prefix = first slot of the bin
-    if (t == 0) bins[RC_LEN_BINS] = used <= 1 ? 1u : 0u;
 }
 
+// The packets in bin order: each workgroup scans the bin counts (exclusive
+// prefix = the first slot of each bin), claims its slots in each bin from
+// the fill counters bins[RC_LEN_FILL ..] and writes its packets there.  When
+// every packet falls in one bin, workgroup 0 sets bins[RC_LEN_BINS] (uniform
+// lengths: the lane kernels keep batch order) and nothing is written.
 extern "C" __global__ __launch_bounds__(256)
 void rc_len_scatter(const uint32_t* len, uint32_t n, uint32_t* bins, uint32_t* order)
 {
-    if (bins[RC_LEN_BINS]) return;       // uniform: identity order
-    __shared__ uint32_t h[RC_LEN_BINS];
-    h[threadIdx.x] = 0;
+    __shared__ uint32_t h[RC_LEN_BINS], pre[RC_LEN_BINS];
+    const uint32_t t = threadIdx.x;
+    const uint32_t cnt = bins[t];
+    const int used = __syncthreads_count(cnt != 0);
+    if (used <= 1) {
+        if (blockIdx.x == 0 && t == 0) bins[RC_LEN_BINS] = 1u;
+        return;
+    }
+    pre[t] = cnt;
+    h[t] = 0;
+    __syncthreads();
+    for (uint32_t d = 1; d < RC_LEN_BINS; d <<= 1) {
+        const uint32_t x = t >= d ? pre[t - d] : 0u;
+        __syncthreads();
+        pre[t] += x;
+        __syncthreads();
+    }
+    const uint32_t first = pre[t] - cnt;             // exclusive prefix: the bin's first slot
     __syncthreads();
     const uint32_t base = blockIdx.x * kBinChunk;
     uint32_t rank[kBinChunk / 256], bin[kBinChunk / 256];
 #pragma unroll
     for (uint32_t k = 0; k < kBinChunk / 256; ++k) {
-        const uint32_t i = base + k * 256 + threadIdx.x;
+        const uint32_t i = base + k * 256 + t;
         bin[k] = i < n ? len_bin(len[i]) : 0u;
         rank[k] = bin_rank(h, bin[k], i < n);
     }
     __syncthreads();
-    const uint32_t c = h[threadIdx.x];
-    if (c) h[threadIdx.x] = atomicAdd(&bins[threadIdx.x], c);   // this workgroup's slots in the bin
+    const uint32_t c = h[t];
+    if (c) h[t] = first + atomicAdd(&bins[RC_LEN_FILL + t], c);   // this workgroup's slots in the bin
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < kBinChunk / 256; ++k) {
-        const uint32_t i = base + k * 256 + threadIdx.x;
+        const uint32_t i = base + k * 256 + t;
         if (i < n) order[h[bin[k]] + rank[k]] = i;
     }
 }
