@@ -63,6 +63,18 @@
 #include "rc_lane_common.h"
 #include "rc_root3.h"
 
+// The file is compiled twice for the library (Makefile): RC_ENC2_PART=1, the
+// plain kernels and the launcher (rc_enc2.o), and RC_ENC2_PART=2, the wide
+// kernels and their launches (rc_enc2_wide.o, built with the iterative ILP
+// scheduler: C3 rc_enc2_wcode2 -9 %, where the plain kernels gain nothing;
+// the scheduling strategy is per object file).  Unset (0): the whole file in
+// one object (the diagnostic builds).
+#ifndef RC_ENC2_PART
+#define RC_ENC2_PART 0
+#endif
+#define E2_PLAIN (RC_ENC2_PART != 2)
+#define E2_WIDE (RC_ENC2_PART != 1)
+
 // Diagnostic build only (-DE2_PROF, tools/enc2_prof.py): per-phase cycles of
 // the scan pass, summed over wavefronts.  The product build has no stamps.
 #ifdef E2_PROF
@@ -98,7 +110,7 @@ struct E2Prof {};
 namespace {
 
 constexpr uint32_t kE2MaxLen = 1919;          // compress.c:148-157: no reset below 1920 B
-constexpr uint32_t kE2SlotMax = 4096;         // longest packet of the narrow scan (windows past a reset)
+[[maybe_unused]] constexpr uint32_t kE2SlotMax = 4096;        // longest packet of the narrow scan (windows past a reset)
 constexpr uint32_t kE2Bucket = 64;            // statistics <= 63
 constexpr uint32_t kScanThreads = 64;         // one wavefront per packet, four buckets per lane
 constexpr uint32_t kSkipFallback = 0xFFFFFFFFu;   // first word of a slot: lane kernels
@@ -888,20 +900,24 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
     E2P_FLUSH
 }
 
+#if E2_PLAIN
 extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_scan(rc_batch_dev b, E2Params e)
 {
     __shared__ __attribute__((aligned(16))) ScanLdsT<2048> s;
     scan_main(b, e, s);
 }
+#endif
 
 // the same for launches whose packets are at most kWideSmallL bytes
+#if E2_PLAIN
 extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_scan_s(rc_batch_dev b, E2Params e)
 {
     __shared__ __attribute__((aligned(16))) ScanLdsT<kWideSmallL> s;
     scan_main(b, e, s);
 }
+#endif
 
 // ------------------------------------------------------------------ pass 2
 
@@ -1145,6 +1161,7 @@ constexpr uint32_t kCodeLds = 336;
 constexpr uint32_t kCodeMtab = 256 * kCodeLds;         // the block's prefix-mask table (rc_root3.h)
 constexpr uint32_t kCodeItab = kCodeMtab + 256;        // the block's D increment table
 
+#if E2_PLAIN
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void rc_enc2_code(rc_batch_dev b, E2Params e)
 {
@@ -1228,6 +1245,7 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
     ring_finish(o, ok);
     b.out_len[pkt] = ok ? o.n : 0u;
 }
+#endif
 
 // ---- pass 2, two wavefronts per SIMD: a helper and a coder per packet.
 // The root model (order 0) evolves with the packet's symbols only, never with
@@ -1382,6 +1400,7 @@ DEV void code_pos(CodeState& k, Ring& o, const uint4& qe, const Pre& p, double r
     ring_chunk(o, n0, dummy);
 }
 
+#if E2_PLAIN
 extern "C" __global__ __launch_bounds__(512)
 void rc_enc2_code2(rc_batch_dev b, E2Params e)
 {
@@ -1501,6 +1520,7 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     ring_finish(o, ok);
     if (live) b.out_len[pkt] = ok ? o.n : 0u;
 }
+#endif
 
 // ------------------------------------------------------------------ wide mode
 //
@@ -1545,7 +1565,7 @@ DEV uint32_t wa_of(uint32_t w) { return (w >> kWA) & 255; }
 // model reset before this position << 18 (compress.c:148-157, the first position
 // of a segment after the first) | packet left to the lane kernels << 19 (position 0)
 constexpr uint32_t kWRst = 1u << 18, kWLeft = 1u << 19;
-constexpr uint32_t kWideLong = 4096;           // rc_enc2_wscan_l: segments of up to this many positions
+[[maybe_unused]] constexpr uint32_t kWideLong = 4096;          // rc_enc2_wscan_l: segments of up to this many positions
 
 // L: the longest packet of the launch (its positions); two sizes are built,
 // 2048 and 1216 -- the smaller one leaves room for 9 wavefronts per CU
@@ -2188,6 +2208,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
     W2P_FLUSH
 }
 
+#if E2_WIDE
 extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_wscan(rc_batch_dev b, E2Params e)
 {
@@ -2480,8 +2501,39 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
 // launches with packets over 1919 bytes: model resets (kWRst) and left packets (kWLeft)
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void rc_enc2_wcode_r(rc_batch_dev b, E2Params e) { wcode_main<true>(b, e); }
+#endif  // E2_WIDE
 
 }  // namespace
+
+#if E2_WIDE
+// The wide kernels over the packets the scan listed (its chunk of cnt
+// packets, scan-sized grid g); e: the chunk's E2Params (rc_hip_enc2_launch).
+extern "C" int rc_hip_enc2_wide_launch(const rc_batch_dev* b, const void* ep, uint32_t g, uint32_t cnt, void* stream)
+{
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const E2Params& e = *static_cast<const E2Params*>(ep);
+    if (e.slot_len <= kWideSmallL)
+        hipLaunchKernelGGL(rc_enc2_wscan_s, dim3(g), dim3(kScanThreads), 0, st, *b, e);
+    else if (e.slot_len <= 2048)
+        hipLaunchKernelGGL(rc_enc2_wscan, dim3(g), dim3(kScanThreads), 0, st, *b, e);
+    else
+        hipLaunchKernelGGL(rc_enc2_wscan_l, dim3(g), dim3(kScanThreads), 0, st, *b, e);
+    static const char* w1 = getenv("ENET_RC_WCODE1");            // the one-wavefront wide code pass (A/B)
+    if (e.slot_len <= kE2MaxLen && !(w1 && atoi(w1) == 1))
+        hipLaunchKernelGGL(rc_enc2_wcode2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
+    else if (e.slot_len <= kE2MaxLen)
+        hipLaunchKernelGGL(rc_enc2_wcode, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
+    else
+        hipLaunchKernelGGL(rc_enc2_wcode_r, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
+    return static_cast<int>(hipGetLastError());
+}
+#endif
+
+#if E2_PLAIN
+#if RC_ENC2_PART == 1
+extern "C" int rc_hip_enc2_wide_launch(const rc_batch_dev* b, const void* ep, uint32_t g, uint32_t cnt,
+                                       void* stream);   // rc_enc2_wide.o
+#endif
 
 #ifdef E2_PROF
 extern "C" int rc_enc2_prof_read(unsigned long long* out, int reset)
@@ -2584,21 +2636,10 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         else
             hipLaunchKernelGGL(rc_enc2_code2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
         if (e.wide) {
-            const dim3 g(cnt < scan_blocks_max ? cnt : scan_blocks_max);
-            if (e.slot_len <= kWideSmallL)
-                hipLaunchKernelGGL(rc_enc2_wscan_s, g, dim3(kScanThreads), 0, st, *b, e);
-            else if (e.slot_len <= 2048)
-                hipLaunchKernelGGL(rc_enc2_wscan, g, dim3(kScanThreads), 0, st, *b, e);
-            else
-                hipLaunchKernelGGL(rc_enc2_wscan_l, g, dim3(kScanThreads), 0, st, *b, e);
-            static const char* w1 = getenv("ENET_RC_WCODE1");            // the one-wavefront wide code pass (A/B)
-            if (e.slot_len <= kE2MaxLen && !(w1 && atoi(w1) == 1))
-                hipLaunchKernelGGL(rc_enc2_wcode2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
-            else if (e.slot_len <= kE2MaxLen)
-                hipLaunchKernelGGL(rc_enc2_wcode, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
-            else
-                hipLaunchKernelGGL(rc_enc2_wcode_r, dim3((cnt + 255) / 256), dim3(256), kCodeItab + 512, st, *b, e);
+            const int rc = rc_hip_enc2_wide_launch(b, &e, cnt < scan_blocks_max ? cnt : scan_blocks_max, cnt, stream);
+            if (rc != 0) return rc;
         }
     }
     return static_cast<int>(hipGetLastError());
 }
+#endif  // E2_PLAIN
