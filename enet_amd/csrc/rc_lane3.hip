@@ -249,6 +249,46 @@ DEV Look<NV> ctx_find(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV, O2>
     return h;
 }
 
+// ctx_find for the decoder's order-1 lookups, with a dense context's group and
+// link already loaded (zp, issued before the next record's load: loads return
+// in order, so waiting for them no longer waits for that record) and its C
+// from the record
+DEV Look<3> ctx_find_pre(const Rec1& c, uint32_t v, const Dense& zp)
+{
+    Look<3> h;
+    h.k = 0; h.under = 0; h.cnt = 0;
+    const uint32_t ny = 0x01000100u - v * 0x00010001u;
+    const uint32_t ny1 = ny - 0x00010001u;
+#pragma unroll
+    for (uint32_t d = 0; d < 3; ++d) {
+        const uint32_t ge = swar_ge(c.val[d], ny);
+        const uint32_t lt = ge ^ 0x01010101u;
+        h.eq[d] = (ge ^ swar_ge(c.val[d], ny1)) & below_mask(static_cast<int>(c.len), d) & 0x01010101u;
+        h.k = sad(lt, h.k);
+        h.under = dot4(c.cnt[d], lt, h.under);
+        h.cnt = dot4(c.cnt[d], h.eq[d], h.cnt);
+    }
+    h.info = slot_info<3, true>(c, h.eq);
+    if (c.dense != 0) {
+        rec_c_get(c, h.z.c0, h.z.c1);
+        h.z.grp = zp.grp;
+        h.z.link = zp.link;
+        const uint32_t g = v >> 4, j = v & 15;
+        uint32_t within = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < 4; ++d) {
+            const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
+            const uint32_t mask = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+            within = sad(pick4(d, h.z.grp) & mask, within);
+        }
+        h.under = (g ? dense_c(h.z, g - 1) : 0u) + within;
+        h.cnt = (pick4(j >> 2, h.z.grp) >> (8 * (j & 3))) & 0xFF;
+        h.info = h.z.link;
+    }
+    h.found = h.cnt != 0 ? 1u : 0u;
+    return h;
+}
+
 // Decoder: the symbol whose interval [under, under + count) holds code
 // (minimum 0): the dword whose running byte sum passes code, then halving
 // on byte sums inside it.  False = no such symbol (corrupt, compress.c:416).
@@ -878,6 +918,14 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             prof_acc[11] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(at == 0));
         }
 #endif
+        // the dense order-1 lookup of this step (a root step, or an order-2
+        // hit whose link the LDS cache lacks): its group and link loaded
+        // before the next record (the scratch record for lanes without one)
+        const bool lcv = L.cur.dense != 0 && L.cext != 0 && L.cur.ext == L.cext && v < kLinkCache;
+        const bool lk = L.order >= 1 && L.cur.dense != 0 && (at == 0 || (at == 2 && !lcv));
+        Dense zp;
+        zp.grp = *reinterpret_cast<const uint4*>(reg + (lk ? L.cur.ext + 32 + 16 * (v >> 4) : kDummyRec));
+        zp.link = *reinterpret_cast<const uint16_t*>(reg + (lk ? L.cur.ext + 288 + 2 * v : kDummyRec));
         lane_prefetch(L, reg, v);
         // the step's last code and the root's update: only the next step
         // needs them, so they run after the record load is issued (as in
@@ -888,16 +936,11 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             rtot = (rtot + kRootDelta) & 0xFFFF;
             if (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit) rtot = root3_rescale<false>(root, R);
         }
-        // the patched o1 context needs v's lookup (compress.c:598-615)
-        if (at == 0 && L.order >= 1) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
-        if (at == 2 && L.order >= 1) {
-            // (the next step's order-2 info: the link cache where it holds v)
-            const bool lcv = L.cur.dense != 0 && L.cext != 0 && L.cur.ext == L.cext && v < kLinkCache;
-            if (any_lane(!lcv)) {
-                if (!lcv) h1 = ctx_find<3, true>(reg, ldsb, L.cur, v);
-            }
-            if (lcv) { h1.info = lc[v]; h1.found = 1u; }
-        }
+        // the patched o1 context needs v's lookup (compress.c:598-615); an
+        // order-2 step needs the link of (b, v), from the LDS cache where it
+        // holds v
+        if (L.order >= 1 && (at == 0 || (at == 2 && !lcv))) h1 = ctx_find_pre(L.cur, v, zp);
+        if (at == 2 && L.order >= 1 && lcv) { h1.info = lc[v]; h1.found = 1u; }
         if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, ldsb, L.q, v);
         fail = o.n >= o.cap;                                         // compress.c:617
         PROF(4)
