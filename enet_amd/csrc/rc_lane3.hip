@@ -269,21 +269,27 @@ DEV Look<3> ctx_find_pre(const Rec1& c, uint32_t v, const Dense& zp)
         h.cnt = dot4(c.cnt[d], h.eq[d], h.cnt);
     }
     h.info = slot_info<3, true>(c, h.eq);
-    if (c.dense != 0) {
-        rec_c_get(c, h.z.c0, h.z.c1);
-        h.z.grp = zp.grp;
-        h.z.link = zp.link;
+    // (selects, not a branch: the preloaded registers are read, never
+    // overwritten in place, so no later write to them waits for the load --
+    // and for the record load behind it)
+    {
+        Dense z;
+        rec_c_get(c, z.c0, z.c1);
+        z.grp = zp.grp;
+        z.link = zp.link;
         const uint32_t g = v >> 4, j = v & 15;
         uint32_t within = 0;
 #pragma unroll
         for (uint32_t d = 0; d < 4; ++d) {
             const uint32_t nb = j > 4 * d ? min(j - 4 * d, 4u) : 0u;
             const uint32_t mask = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-            within = sad(pick4(d, h.z.grp) & mask, within);
+            within = sad(pick4(d, z.grp) & mask, within);
         }
-        h.under = (g ? dense_c(h.z, g - 1) : 0u) + within;
-        h.cnt = (pick4(j >> 2, h.z.grp) >> (8 * (j & 3))) & 0xFF;
-        h.info = h.z.link;
+        const bool dn = c.dense != 0;
+        h.under = dn ? (g ? dense_c(z, g - 1) : 0u) + within : h.under;
+        h.cnt = dn ? (pick4(j >> 2, z.grp) >> (8 * (j & 3))) & 0xFF : h.cnt;
+        h.info = dn ? z.link : h.info;
+        h.z = z;
     }
     h.found = h.cnt != 0 ? 1u : 0u;
     return h;
@@ -939,8 +945,13 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // the patched o1 context needs v's lookup (compress.c:598-615); an
         // order-2 step needs the link of (b, v), from the LDS cache where it
         // holds v
-        if (L.order >= 1 && (at == 0 || (at == 2 && !lcv))) h1 = ctx_find_pre(L.cur, v, zp);
-        if (at == 2 && L.order >= 1 && lcv) { h1.info = lc[v]; h1.found = 1u; }
+        {
+            const uint32_t lcl = lc[v & (kLinkCache - 1)];     // (read by every lane: its own register)
+            if (L.order >= 1 && (at == 0 || (at == 2 && !lcv))) h1 = ctx_find_pre(L.cur, v, zp);
+            const bool ul = at == 2 && L.order >= 1 && lcv;
+            h1.info = ul ? lcl : h1.info;
+            h1.found = ul ? 1u : h1.found;
+        }
         if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, ldsb, L.q, v);
         fail = o.n >= o.cap;                                         // compress.c:617
         PROF(4)
