@@ -204,6 +204,22 @@ template <uint32_t NV, bool O2>
 DEV void ctx_dense_find(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV, O2>& c, uint32_t v, Dense& z,
                         uint32_t& u, uint32_t& n)
 {
+    if constexpr (!O2) {
+        // The arena path in a branch of its own that waits for its loads:
+        // LDS reads into registers of an arena load the compiler must assume
+        // pending would wait vmcnt(0) for it -- and, in the decoder, for the
+        // record load issued before it -- even in wavefronts where no lane
+        // read the arena (game state: the dense order-2 block is the LDS one).
+        const uint4 zz = make_uint4(0u, 0u, 0u, 0u);
+        z.c0 = zz; z.c1 = zz; z.grp = zz; z.link = 0;
+        u = 0; n = 0;
+        if (any_lane(c.dense == 1)) {
+            if (c.dense == 1) dense_find(reg + c.ext, v, O2, z, u, n);
+            __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+        }
+        if (c.dense == 2) dense_find(ldsb, v, O2, z, u, n);
+        return;
+    }
     if (!O2 && c.dense == 2) dense_find(ldsb, v, O2, z, u, n);
     else dense_find(reg + c.ext, v, O2, z, u, n);
 }
