@@ -182,8 +182,83 @@ def run_workload(coder, dev, stream, kind, n, size, rank, steps, warmup, dist=No
     return raw, summary
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) outside a torchrun job: one process per GPU, started
+    here as torch.distributed.run's children before anything touches a GPU
+    (the parent only counts devices, which does not initialise HIP), and the
+    parent exits with their status.  Fewer than N visible GPUs: a message and
+    exit status 2, never a one-GPU number under an N-GPU request.  Returns
+    None when this process is to run the bench itself."""
+    n = args.gpus
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if n > 1 and int(env_world) != n:
+            print(f"bench.py: --gpus {n} but WORLD_SIZE={env_world}: launch one rank per requested GPU",
+                  file=sys.stderr)
+            return 2
+        return None
+    if n <= 1:
+        return None
+    if os.environ.get("ENET_BENCH_STUB") != "1":
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} requested but {have} GPU(s) visible; refusing to report a "
+                  f"{max(have, 1)}-GPU measurement as {n}-GPU", file=sys.stderr)
+            return 2
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def stub_main(args):
+    """ENET_BENCH_STUB=1 (CPU tests of the launcher, tests/test_bench_launch.py):
+    the same rank/barrier/max-over-ranks reporting over gloo with a host
+    memcpy in place of the coder; never a measurement of this library."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    src = np.full(1 << 16, rank, np.uint8)
+    dst = np.empty_like(src)
+    for _ in range(args.warmup):
+        dst[:] = src
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dst[:] = src
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": src.size * world * args.steps / max(float(t.item()), 1e-9) / GIB,
+                          "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "data": "stub (launcher test: host memcpy, no coder)"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if os.environ.get("ENET_BENCH_STUB") == "1":
+        return stub_main(args)
     import torch
     import torch.distributed as dist
 
