@@ -72,6 +72,11 @@ typedef struct {
     /* rc_dec6.hip: per packet, where its model segments after the first start (the resets of
        compress.c:148-157): 12 bits each, their count in bits 24-25 */
     uint32_t *dec6_resets;  /* [n_cap] */
+    /* rc_dec6.hip: per packet, the sums of the input chunks that passed through the decoder's
+       LDS slot (rc_slot.h slot_mix) as the decoder took them and as its helper loaded them;
+       rc_dec6_verify sends a packet whose sums differ to the lane kernels */
+    uint32_t *dec6_icks;    /* [n_cap] */
+    uint32_t *dec6_hcks;    /* [2 n_cap]: the helper's sums, then its last chunk's terms */
     uint32_t  dec6_debug;   /* diagnostic (ENET_RC_DEC6_DEBUG): 1 = the check lists every packet */
     void     *dec6_pool;    /* lane_slots * RC_DEC6_TAB_BYTES: rc_dec6.hip's bucket records */
     /* test switch (ENET_RC_ENC2_SLOW=1): the scan takes its slow paths (every position

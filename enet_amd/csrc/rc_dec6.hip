@@ -517,8 +517,23 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         if (!any_lane(!done)) break;
     }
     PROF_FLUSH(16)
+#ifndef DEC6_NO_USED_CHECK            // (tests/test_lane_host.py: the build without it, for comparison)
+    if constexpr (kSlot) {
+        // Every stream compress.c writes is read to its end: the seed takes 4
+        // bytes and each settled byte of the coder one more, as the encoder
+        // emitted them, and the flush wrote 0-4 bytes past those
+        // (compress.c:114-146, :344-371), so a decode that reaches its end of
+        // stream has taken between C and C + 4 bytes (zeros past the end).  A
+        // decode that took otherwise saw other bytes than the packet's -- or
+        // is a corrupt stream's, which the lane kernels decode as well -- and
+        // goes to them (tests/test_lane_host.py stale-chunk injections).
+        const uint32_t used = 16 * in.j + 4 * in.q - in.lo15 - in.na;
+        off = off || (!fail && (used < len || used > len + 4));
+    }
+#endif
     if (off) { bail6(ws, pkt); ws.claims[pkt] = 0xFFFFFFFFu; return; }
     ws.dec6_resets[pkt] = rst;
+    if constexpr (kSlot) ws.dec6_icks[pkt] = in.cks;       // (rc_slot.h slot_mix; the helper's in dec6_hcks)
     // an output that does not fit returns 0 (compress.c:617) once the check has
     // passed: until then out_len holds the bytes decoded (bit 31 of the claims)
     sink1_finish(o);
@@ -556,7 +571,7 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
         slot_help_init(h);
         for (;;) {
             bool fin = false;
-            const bool busy = slot_help_iter(b, mctl, hctl, slotp, h, fin);
+            const bool busy = slot_help_iter(b, mctl, hctl, slotp, h, ws.dec6_hcks, ws.n_cap, fin);
             if (fin) break;
             if (!busy) __builtin_amdgcn_s_sleep(DEC6_HELP_SLEEP);
         }
@@ -592,20 +607,26 @@ constexpr uint32_t kVerifyWaves = 4;
 constexpr uint32_t kVerifyBlocksPerCu = 10;     // 32 KB of LDS per workgroup: 5 resident per CU, two rounds
 constexpr uint32_t kVerDw = 8;                  // dwords per lane: packets to 2 KB - 4
 
-// the header words of packet k, lane l < 5: claims, out_len, out_off (2), resets
+// the header words of packet k, lane l < 8: claims, out_len, out_off (2),
+// resets, and the hand-off's check sums (the decoder's, the helper's and its
+// last chunk's term: rc_slot.h)
 DEV uint32_t vhead_load(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, uint32_t l)
 {
     const uint32_t* src = l == 0 ? ws.claims + k
                         : l == 1 ? b.out_len + k
                         : l < 4 ? reinterpret_cast<const uint32_t*>(b.out_off + k) + (l - 2)
-                                : ws.dec6_resets + k;
-    return (k < b.n && l < 5) ? *src : 0u;
+                        : l == 4 ? ws.dec6_resets + k
+                        : l == 5 ? ws.dec6_icks + k
+                        : l == 6 ? ws.dec6_hcks + k
+                                 : ws.dec6_hcks + ws.n_cap + k;
+    return (k < b.n && l < 8) ? *src : 0u;
 }
+
 
 struct VHead {
     uint32_t cl, n, rst, off, nd;   // off: lo - sb; nd: dwords from sb
     uintptr_t lo, sb;
-    bool skip, fast;
+    bool skip, fast, cks;           // cks: the hand-off's sums agree
 };
 
 DEV VHead vhead_get(const rc_batch_dev& b, uint32_t k, uint32_t hv)
@@ -616,6 +637,7 @@ DEV VHead vhead_get(const rc_batch_dev& b, uint32_t k, uint32_t hv)
     const uint64_t oo = static_cast<uint64_t>(static_cast<uint32_t>(__shfl(hv, 2))) |
                         static_cast<uint64_t>(static_cast<uint32_t>(__shfl(hv, 3))) << 32;
     h.rst = __shfl(hv, 4);
+    h.cks = cks_agree(__shfl(hv, 5), __shfl(hv, 6), __shfl(hv, 7));
     h.skip = k >= b.n || h.cl == 0xFFFFFFFFu;                    // none, or left to the lanes already
     h.lo = reinterpret_cast<uintptr_t>(b.out) + oo;
     h.sb = h.lo & ~static_cast<uintptr_t>(3);
@@ -635,15 +657,18 @@ DEV void vdata_load(const VHead& h, uint32_t l, uint32_t (&w)[kVerDw])
     }
 }
 
-DEV void vresult(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, uint32_t cl, uint32_t cnt, uint32_t l)
+// ck: the slot hand-off's check sums agree (rc_slot.h slot_mix)
+DEV void vresult(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, uint32_t cl, uint32_t cnt, bool ck,
+                 uint32_t l)
 {
     for (int sft = 32; sft >= 1; sft >>= 1) cnt += static_cast<uint32_t>(__shfl_xor(static_cast<int>(cnt), sft));
     const uint32_t want = cl & 0x7FFFFFFFu;
-    if (l == 0 && (cnt != want || (ws.dec6_debug & 1))) {
+    const bool ok = cnt == want && ck && !(ws.dec6_debug & 1);
+    if (l == 0 && !ok) {
         const uint32_t i = atomicAdd(&ws.counters[3], 1u);
         ws.enc2_list[i] = k;
     }
-    if (l == 0 && cnt == want && !(ws.dec6_debug & 1) && (cl >> 31)) b.out_len[k] = 0;     // compress.c:617
+    if (l == 0 && ok && (cl >> 31)) b.out_len[k] = 0;     // compress.c:617
 }
 
 DEV void vclear(uint4* set4, uint32_t l)
@@ -679,7 +704,7 @@ DEV void verify_fast(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t
             cnt += (in && !(old & bit)) ? 1u : 0u;
         }
     }
-    vresult(b, ws, k, h.cl, cnt, l);
+    vresult(b, ws, k, h.cl, cnt, h.cks, l);
 }
 
 // any other packet: per model segment (compress.c:148-157: bigrams are counted
@@ -730,7 +755,7 @@ DEV void verify_slow(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t
             cnt += sc;
             __builtin_amdgcn_wave_barrier();
         }
-        vresult(b, ws, pkt, cl, cnt, l);
+        vresult(b, ws, pkt, cl, cnt, cks_agree(ws.dec6_icks[pkt], ws.dec6_hcks[pkt], ws.dec6_hcks[ws.n_cap + pkt]), l);
     }
 }
 

@@ -51,6 +51,7 @@ typedef struct {
     int enc2_wide_on;               /* ... and its wide mode (ENET_RC_ENC2_WIDE=0: off) */
     uint64_t enc2_stream_max;       /* record-stream caps, read when the context is created */
     uint64_t enc2_wide_max;
+    uint64_t enc2_failed;     /* the smallest record-stream size an allocation failed for (0: none) */
     uint32_t *crc_tables;           /* device: slice-by-16 + shift tables (rc_crc32.hip) */
     /* datagram framing workspace (rc_dgram.hip): per-datagram arrays + checksum scratch */
     uint8_t *dg_arrays;
@@ -67,6 +68,7 @@ typedef struct {
     void *twin[SPLIT_MAX - 1];
     struct h2d_sync *sync_sig, *sync_wait;
     int last_split;                 /* pieces of the last host batch (0: one piece) */
+    uint32_t last_paths;            /* enet_rc_last_host_paths */
     int split_k;                    /* pieces of a large host batch (ENET_RC_HOST_SPLIT) */
 } rc_ctx;
 
@@ -97,8 +99,8 @@ static int ws_reserve(rc_ctx *c, size_t n)
     size_t cap = c->ws.n_cap ? c->ws.n_cap : 1024;
     while (cap < n) cap *= 2;
     uint32_t *fl = NULL, *ord = NULL, *el = NULL, *wl = NULL, *cl = NULL;
-    /* claims and the decoder's reset positions side by side */
-    if (hipMalloc((void **) &cl, 2 * cap * sizeof(uint32_t)) != hipSuccess) return -1;
+    /* claims, the decoder's reset positions and its two hand-off sums side by side */
+    if (hipMalloc((void **) &cl, 5 * cap * sizeof(uint32_t)) != hipSuccess) return -1;
     if (hipMalloc((void **) &fl, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(cl); return -1; }
     if (hipMalloc((void **) &ord, cap * sizeof(uint32_t)) != hipSuccess) { hipFree(cl); hipFree(fl); return -1; }
     if (hipMalloc((void **) &el, cap * sizeof(uint32_t)) != hipSuccess) {
@@ -117,6 +119,8 @@ static int ws_reserve(rc_ctx *c, size_t n)
     }
     c->ws.claims = cl;
     c->ws.dec6_resets = cl + cap;
+    c->ws.dec6_icks = cl + 2 * cap;
+    c->ws.dec6_hcks = cl + 3 * cap;
     c->ws.flag_list = fl;
     c->ws.order = ord;
     c->ws.enc2_list = el;
@@ -191,6 +195,9 @@ static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
     const uint64_t cap = c->enc2_stream_max;
     uint64_t want = (uint64_t) (n >= 8192 ? (n + 8191) & ~(size_t) 8191 : n) * slot;   /* (as lanes_reserve) */
     if (want > cap) want = cap > slot ? cap : slot;
+    /* (a size that failed once is not retried: the stream the device could
+     * give then serves, in more chunks, without a device-wide sync per call) */
+    if (c->enc2_failed && want >= c->enc2_failed && c->ws.enc2_cap) want = c->ws.enc2_cap;
     if (want > c->ws.enc2_cap) {
         hipDeviceSynchronize();
         if (c->ws.enc2_stream) hipFree(c->ws.enc2_stream);
@@ -201,6 +208,7 @@ static int enc2_reserve(rc_ctx *c, size_t n, uint32_t max_len)
         while (hipMalloc(&c->ws.enc2_stream, want + (1u << 20)) != hipSuccess) {
             c->ws.enc2_stream = NULL;
             (void) hipGetLastError();
+            if (!c->enc2_failed || want < c->enc2_failed) c->enc2_failed = want;
             if (want <= slot) return -1;
             want = want / 2 > slot ? (want / 2) / slot * slot : slot;
         }
@@ -917,6 +925,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         host_unpin(in + zc_lo, zc_pin);
         return (int) err;
     }
+    c->last_paths = zc_dev ? 4u : pitch ? 3u : pin_in ? 2u : 1u;
     const int ig = pin_in || zc_pin ? 0 : in_bytes >= (16u << 20) ? 4 : 1;
     for (int g = 0; g < ig; ++g) {
         const size_t lo = n * (size_t) g / (size_t) ig, hi = n * (size_t) (g + 1) / (size_t) ig;
@@ -967,12 +976,17 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
         memcpy(out_len, h + a_olen, n * 4);
         for (size_t i = 0; i < n; ++i)
             if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
+        c->last_paths |= 1u << 4;
         return 0;
     }
     /* a decompress batch whose slots are back to back (out_cap = the packet
-     * lengths): the whole span in one DMA straight behind the kernels (a slot
-     * a packet did not fill gets unspecified bytes past its out_len, as the
-     * reference's outLimit allows) */
+     * lengths) and every one of them filled: the whole span in one DMA
+     * straight behind the kernels.  The lengths are read first: a slot a
+     * packet did not fill (a corrupt stream, an output that does not fit)
+     * keeps the caller's bytes past its out_len, as compress.c writes only
+     * what it decodes -- the span's DMA would put the staging memory's old
+     * contents there (an earlier batch's payload) -- so such a batch takes
+     * the slot copy below. */
     /* (a piece of a split batch of packets of >= 512 B on average: its slot
      * copy below with few workgroups, leaving the other pieces' kernels
      * their CUs' issue slots; the copy's wavefronts each move a packet, so
@@ -981,15 +995,20 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
     int contig_out = decompress;
     for (size_t i = 1; i < n && contig_out; ++i) contig_out = out_off[i] == out_off[i - 1] + out_cap[i - 1];
     if (contig_out) {
+        /* (the lengths, and the kernels done: registering the caller's range
+         * while they run made the copy 1.2 ms slower; a piece of a split
+         * batch finds its range registered already) */
+        err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+        if (err != hipSuccess) return (int) err;
+        const uint32_t *ol = (const uint32_t *) (h + a_olen);
+        for (size_t i = 0; i < n && contig_out; ++i) contig_out = ol[i] == out_cap[i];
+    }
+    if (contig_out) {
         const uint64_t span = out_off[n - 1] + out_cap[n - 1] - out_off[0];
-        /* (registering the caller's range while the kernels run made this
-         * copy 1.2 ms slower: register it once they are done; a piece of a
-         * split batch finds its range registered already) */
-        if (!c->sync_sig && !c->sync_wait) hipStreamSynchronize(c->stream);
         const int pin_out = allow_pin ? host_pin(out + out_off[0], span) : 0;
         if (pin_out) {
             err = d2h_copy(out + out_off[0], d + a_out + out_off[0], span, c->stream);
-            if (err == hipSuccess) err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
             if (err == hipSuccess)
                 err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
             const hipError_t e2 = hipStreamSynchronize(c->stream);
@@ -1004,6 +1023,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
                         in_bytes / 1e6, span / 1e6, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[5] - tp[3],
                         tp[5] - tp[0]);
             }
+            c->last_paths |= 2u << 4;
             return 0;
         }
     }
@@ -1037,6 +1057,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
                         "H2D drain %.3f, kernels %.3f, slot copy %.3f, total %.3f ms\n", decompress ? "dec" : "enc",
                         n, in_bytes / 1e6, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[5] - tp[3], tp[5] - tp[0]);
             }
+            c->last_paths |= 3u << 4;
             return 0;
         }
         (void) hipGetLastError();
@@ -1086,6 +1107,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
                 in_bytes / 1e6, packed / 1e6, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3],
                 tp[5] - tp[4], tp[5] - tp[0]);
     }
+    c->last_paths |= 4u << 4;
     return err == hipSuccess ? 0 : (int) err;
 }
 
@@ -1113,6 +1135,9 @@ static void *piece_worker(void *p)
     piece_job *j = (piece_job *) p;
     j->rc = run_host(j->c, j->decompress, j->in, j->in_off, j->in_len, j->n, j->out, j->out_off, j->out_cap,
                      j->out_len, 1, NULL, NULL);
+    /* (a failed piece may have left DMAs of the caller's page-locked ranges in
+     * flight: drained before run_host_split unregisters them) */
+    if (j->rc != 0) hipStreamSynchronize(j->c->stream);
     /* (a piece that ended before its input DMA: the next one waits for nothing) */
     if (j->c->sync_sig) h2d_sync_set(j->c->sync_sig, -1);
     return NULL;
@@ -1193,10 +1218,19 @@ static int run_host_split(rc_ctx *c, int decompress, const uint8_t *in, const ui
     piece_job job[SPLIT_MAX];
     pthread_t th[SPLIT_MAX];
     int threaded[SPLIT_MAX] = {0};
+    uint64_t *rebased[SPLIT_MAX] = {NULL};
     for (int p = 0; p < k; ++p) {
         rc_ctx *x = p ? (rc_ctx *) c->twin[p - 1] : c;
         const size_t a = first[p], m = first[p + 1] - a;
-        piece_job j = {x, decompress, in, in_off + a, in_len + a, m, out, out_off + a, out_cap + a, out_len + a, 0};
+        /* the piece's output offsets from its own first slot, so that its
+         * staging (sized from the largest out_off + out_cap) covers its slots
+         * only, not the output from byte 0 */
+        uint64_t lo = UINT64_MAX;
+        for (size_t i = a; i < a + m; ++i) if (out_off[i] < lo) lo = out_off[i];
+        rebased[p] = m ? (uint64_t *) malloc(m * sizeof(uint64_t)) : NULL;
+        if (rebased[p]) for (size_t i = 0; i < m; ++i) rebased[p][i] = out_off[a + i] - lo;
+        piece_job j = {x, decompress, in, in_off + a, in_len + a, m, rebased[p] ? out + lo : out,
+                       rebased[p] ? rebased[p] : out_off + a, out_cap + a, out_len + a, 0};
         job[p] = j;
         x->sync_wait = p ? &y[p - 1] : NULL;
         x->sync_sig = p < k - 1 ? &y[p] : NULL;
@@ -1216,6 +1250,7 @@ static int run_host_split(rc_ctx *c, int decompress, const uint8_t *in, const ui
         exact += x->last_exact;
     }
     c->last_exact = exact;
+    for (int p = 0; p < k; ++p) free(rebased[p]);
     for (int i = 0; i < k - 1; ++i) {
         hipEventDestroy(y[i].ev);
         pthread_cond_destroy(&y[i].cv);
@@ -1594,6 +1629,16 @@ uint32_t enet_rc_config_flags(void *context)
 }
 
 uint32_t enet_rc_last_split(void *context) { return context ? (uint32_t) ((rc_ctx *) context)->last_split : 0u; }
+
+uint32_t enet_rc_last_host_paths(void *context)
+{
+    const rc_ctx *c = (const rc_ctx *) context;
+    if (!c) return 0;
+    /* a split batch: its last piece's */
+    for (int i = c->last_split - 2; i >= 0; --i)
+        if (c->twin[i]) return ((const rc_ctx *) c->twin[i])->last_paths;
+    return c->last_paths;
+}
 
 /* ------------------------------------------------------ for rc_multi.c */
 

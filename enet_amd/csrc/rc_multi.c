@@ -17,16 +17,17 @@
  *                    device, nothing per packet); every other device's range
  *                    is copied to it over the peer link (hipMemcpyPeerAsync:
  *                    xGMI between MI355X), its offsets rebased there and
- *                    coded there; the root's stream waits for that device's
- *                    event and a copy kernel on the root reads each packet's
- *                    produced bytes straight out of the device's slots over
- *                    the link (peer access) into the root's slots -- only the
- *                    produced bytes cross the link, nothing outside
+ *                    coded there; its slot range comes back over the link in
+ *                    one copy into a root stage buffer sized from the plan,
+ *                    the root's stream waits for that device's event, and a
+ *                    copy kernel on the root moves each packet's produced
+ *                    bytes into the root's slots -- nothing outside
  *                    [out_off[i], out_off[i] + out_len[i]) is written, and the
  *                    host waits for nothing between the plan's read-back and
- *                    the end.  Without peer access (no xGMI path) the slot
- *                    range comes over in one runtime-staged copy into a root
- *                    buffer sized from the plan, then the same copy kernel.
+ *                    the end.  (ENET_RC_MULTI_PEER_READ=1: the copy kernel
+ *                    reads the device's slots over the link directly, no
+ *                    stage; cross-device visibility of that read after the
+ *                    event wait is unmeasured without a multi-GPU box.)
  * The split is enet_rc_multi_split (also exported, for tests and callers
  * that place packets themselves).
  */
@@ -125,17 +126,25 @@ void *enet_rc_multi_create(const int *devices, size_t n_devices)
         m->h_plan = NULL;
         goto fail;
     }
-    /* direct peer access between the root and every other device (xGMI);
-     * where it is unavailable (no link) the input copies are staged by the
-     * runtime and the results come back through the root's stage buffer */
+    /* peer access between the root and every other device (xGMI) for the
+     * copies.  The results of another device come back as a DMA of its slot
+     * range into the root's stage buffer (hipMemcpyPeerAsync), which the
+     * root's copy kernel then reads: that the root's kernel sees a peer's
+     * writes when it reads them across the link after only an event wait is
+     * unmeasured here (one GPU per test box), so the direct read of a peer's
+     * slots is opt-in, ENET_RC_MULTI_PEER_READ=1.  A range on the root's own
+     * device is read in place (ENET_RC_MULTI_NO_PEER=1: through the stage
+     * too -- the test switch that runs the stage path on one GPU). */
+    const char *pr = getenv("ENET_RC_MULTI_PEER_READ"), *np = getenv("ENET_RC_MULTI_NO_PEER");
+    const int peer_read = pr && atoi(pr) != 0, no_peer = np && atoi(np) != 0;
     m->d[0].peer = 1;
     for (size_t k = 1; k < n_devices; ++k) {
-        if (devices[k] == devices[0]) { m->d[k].peer = 1; continue; }
+        if (devices[k] == devices[0]) { m->d[k].peer = !no_peer; continue; }
         int can = 0;
         if (hipDeviceCanAccessPeer(&can, devices[0], devices[k]) == hipSuccess && can) {
             hipSetDevice(devices[0]);
             const hipError_t e = hipDeviceEnablePeerAccess(devices[k], 0);
-            m->d[k].peer = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+            m->d[k].peer = peer_read && !no_peer && (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled);
             hipSetDevice(devices[k]);
             hipDeviceEnablePeerAccess(devices[0], 0);
         }

@@ -39,9 +39,24 @@ constexpr uint32_t kNoPktS = 0xFFFFFFFEu;
 
 #ifndef RC_LANE_HOST_TEST
 #define SLOT_IDLE() __builtin_amdgcn_s_sleep(1)
+#define SLOT_POINT() ((void) 0)
+#define SLOT_TAKEN(s, sl) ((void) 0)
 #else
-static void slot_host_kick();     // tests/proto/lane_host.cpp: one helper pass
+// tests/proto/lane_host.cpp: one helper pass; tests/proto/slot_sched.cpp: the
+// decoding side hands the turn to the helper (it waits for it)
+static void slot_host_kick();
+static void slot_host_step();    // the end of a decoding step: lane_host.cpp runs a helper pass
+// tests/proto/slot_sched.cpp: a point between two of the protocol's LDS word
+// accesses where its seeded scheduler may switch sides; and the check of a
+// chunk the decoding side took against the packet's bytes (no-ops elsewhere)
+static void slot_host_point(int site);
+static void slot_host_taken(uint32_t j, uint4& sl);
+#ifndef SLOT_MUTANT
+#define SLOT_MUTANT 0
+#endif
 #define SLOT_IDLE() slot_host_kick()
+#define SLOT_POINT() slot_host_point(__LINE__)
+#define SLOT_TAKEN(s, sl) slot_host_taken((s).j, sl)
 #endif
 
 struct SlotSrc {
@@ -49,12 +64,38 @@ struct SlotSrc {
     uint32_t na, q, j, lo15;      // bytes in la; dwords of c taken; c is chunk j; packet start & 15
     uint4 c;                      // (shifted as taken: c.x is dword q of chunk j)
     uint32_t want, gen;
+    uint32_t cks;                 // the chunks taken from the slot, summed (slot_mix)
     uint32_t* mctl;               // [0] m_ctl, [1] m_pkt
     const uint32_t* hctl;
     const uint8_t* slot;
 };
 
-DEV void slot_publish(const SlotSrc& s) { s.mctl[0] = ((s.want & 0xFFFu) << 16) | s.gen; }
+// Chunk k of a packet's stream as a term of the hand-off's check sum: both
+// sides sum the chunks that pass through the slot -- the helper what it
+// loads, the decoder what it takes -- and rc_dec6_verify sends a packet
+// whose sums differ (but for the helper's last chunk, which a decoder that
+// stopped early never takes) to the lane kernels, which read the stream
+// themselves.  A chunk of zeros (past the stream's end) adds nothing.
+DEV uint32_t slot_mix(const uint4& c, uint32_t k)
+{
+    return ((c.x ^ (c.y * 0x9E3779B1u)) + (c.z ^ (c.w * 0x85EBCA77u))) * (2u * k + 1u);
+}
+
+// the decoder took what its helper loaded, but perhaps the last chunk
+DEV bool cks_agree(uint32_t icks, uint32_t hcks, uint32_t hlast)
+{
+#ifdef SLOT_NO_CKS
+    return true;                      // (tests/test_lane_host.py: the check without the sums, for comparison)
+#else
+    return icks == hcks || icks == hcks - hlast;
+#endif
+}
+
+DEV void slot_publish(const SlotSrc& s)
+{
+    s.mctl[0] = ((s.want & 0xFFFu) << 16) | s.gen;
+    SLOT_POINT();
+}
 
 // h_ctl, then the slot, in that order (see the header)
 DEV void slot_read(const SlotSrc& s, uint32_t& hc, uint4& sl)
@@ -62,10 +103,19 @@ DEV void slot_read(const SlotSrc& s, uint32_t& hc, uint4& sl)
 #ifndef RC_LANE_HOST_TEST
     hc = __hip_atomic_load(s.hctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     asm volatile("" ::: "memory");
-#else
-    hc = *s.hctl;
-#endif
     sl = *reinterpret_cast<const uint4*>(s.slot);
+#else
+    // (the host scheduler's model: every dword access on its own, either side
+    // may run between any two of them)
+    SLOT_POINT();
+    hc = *s.hctl;
+    SLOT_POINT();
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s.slot);
+    sl.x = w[0]; SLOT_POINT();
+    sl.y = w[1]; SLOT_POINT();
+    sl.z = w[2]; SLOT_POINT();
+    sl.w = w[3]; SLOT_POINT();
+#endif
 }
 
 DEV void slot_shift(SlotSrc& s, bool en)
@@ -86,11 +136,18 @@ DEV void slot_fill(SlotSrc& s, bool en)
 }
 
 // c used up: the slot's chunk if it is chunk j + 1 (hc: h_ctl as read, sl: the slot)
-DEV void slot_take(SlotSrc& s, const uint4& sl, uint32_t hc, bool en)
+DEV void slot_take(SlotSrc& s, const uint4& sl_in, uint32_t hc, bool en)
 {
     const bool ready = ((hc >> 16) & 0xFFFu) == ((s.j + 1) & 0xFFFu) && (hc & 0xFFFFu) == s.gen;
     const bool t = en && s.q == 4 && ready;
+#ifdef RC_LANE_HOST_TEST
+    uint4 sl = sl_in;                 // (the host tests check it, or replace it: a stale chunk)
+    if (t) SLOT_TAKEN(s, sl);
+#else
+    const uint4& sl = sl_in;
+#endif
     s.c.x = t ? sl.x : s.c.x; s.c.y = t ? sl.y : s.c.y; s.c.z = t ? sl.z : s.c.z; s.c.w = t ? sl.w : s.c.w;
+    s.cks += t ? slot_mix(sl, s.j + 1) : 0u;
     s.q = t ? 0u : s.q;
     s.j += t ? 1u : 0u;
     s.want = t ? s.j + 1 : s.want;
@@ -105,7 +162,7 @@ DEV void slot_step_end(SlotSrc& s, const uint4& sl, uint32_t hc)
     slot_fill(s, true);
     slot_publish(s);
 #ifdef RC_LANE_HOST_TEST
-    slot_host_kick();
+    slot_host_step();
 #endif
 }
 
@@ -209,7 +266,27 @@ DEV uint32_t slot_init(SlotSrc& s, const uint8_t* p, uint32_t len, uint32_t pkt)
     slot_adv0(s, c1);
     s.gen = s.gen % 0xFFFFu + 1u;
     s.want = s.j + 1;
-    *reinterpret_cast<uint2*>(s.mctl) = make_uint2(((s.want & 0xFFFu) << 16) | s.gen, pkt);
+    s.cks = 0;
+    // m_pkt, then m_ctl with the new generation (two word stores in that
+    // order; the helper reads m_ctl, then m_pkt): a helper that sees the new
+    // generation sees this packet, or a later one, whose chunk it would then
+    // announce under this generation after the decoder has left it -- never
+    // taken.  (One 64-bit store would do on gfx950, whose LDS performs an
+    // instruction whole; this order needs only word-sized accesses, which the
+    // host scheduler test, tests/proto/slot_sched.cpp, models.)
+#if defined(RC_LANE_HOST_TEST) && SLOT_MUTANT == 1
+    s.mctl[0] = ((s.want & 0xFFFu) << 16) | s.gen;      // (test mutant: the generation first)
+    SLOT_POINT();
+    s.mctl[1] = pkt;
+#else
+    s.mctl[1] = pkt;
+#ifndef RC_LANE_HOST_TEST
+    asm volatile("" ::: "memory");
+#endif
+    SLOT_POINT();
+    s.mctl[0] = ((s.want & 0xFFFu) << 16) | s.gen;
+#endif
+    SLOT_POINT();
     // (settled here: a load pending at the step loop's header makes the compiler
     // wait for vmcnt(0) at every step)
     __builtin_amdgcn_s_waitcnt(0);
@@ -218,29 +295,53 @@ DEV uint32_t slot_init(SlotSrc& s, const uint8_t* p, uint32_t len, uint32_t pkt)
 
 // ------------------------------------------------------------------ helper
 struct SlotHelp {
-    uint32_t have, hgen, cgen, pub, len, pkt;
+    uint32_t have, hgen, cgen, pub, len, pkt, cks, last;   // last: the last loaded chunk's term
     uintptr_t ib;
 };
 
 DEV void slot_help_init(SlotHelp& h)
 {
-    h.have = 0; h.hgen = 0; h.cgen = 0; h.pub = 0; h.len = 0; h.ib = 0; h.pkt = kNoPktS;
+    h.have = 0; h.hgen = 0; h.cgen = 0; h.pub = 0; h.len = 0; h.ib = 0; h.pkt = kNoPktS; h.cks = 0; h.last = 0;
 }
 
 // One pass over the helper's lanes: a new packet's input range, the wanted
 // chunk into the slot, h_ctl.  Returns whether it loaded anything; fin_all:
-// every decoding lane of the wavefront is done.
+// every decoding lane of the wavefront is done.  hcks[p]: the sum of the
+// chunks loaded for packet p (slot_mix), and hcks[p + stride] the last one's
+// term (a decoder that stops before the end of its stream -- an output that
+// does not fit -- never takes the chunk it asked for last), stored when the
+// lane moves on (a packet seen under a generation not its own -- the reads of
+// m_ctl and m_pkt straddling the decoder's start of the next packet -- is
+// stored again, with its full sum, when the lane leaves it: the last store is
+// the whole packet's).
 DEV bool slot_help_iter(const rc_batch_dev& bt, const uint32_t* mctl, uint32_t* hctl, uint8_t* slot, SlotHelp& h,
-                        bool& fin_all)
+                        uint32_t* hcks, uint32_t stride, bool& fin_all)
 {
-    const uint2 m = *reinterpret_cast<const uint2*>(mctl);
+    // m_ctl, then m_pkt (see slot_init)
+    SLOT_POINT();
+    uint2 m;
+    m.x = mctl[0];
+#ifndef RC_LANE_HOST_TEST
+    asm volatile("" ::: "memory");
+#endif
+    SLOT_POINT();
+    m.y = mctl[1];
+    SLOT_POINT();
     const bool fin = m.y == kFinS;
     const uint32_t want = (m.x >> 16) & 0xFFFu, mgen = m.x & 0xFFFFu;
     // a new packet: a new generation, or (should the generation have wrapped
     // round unseen) a new packet index; the chunk held is then forgotten
     const bool np = !fin && m.y != kNoPktS && (mgen != h.cgen || m.y != h.pkt);
-    if (any_lane(np)) {
+    const bool leave = (np || fin) && h.pkt != kNoPktS && h.pkt != kFinS;
+    if (any_lane(np || leave)) {
+        if (leave) {
+            hcks[h.pkt] = h.cks;
+            hcks[h.pkt + stride] = h.last;
+        }
+        h.pkt = leave && !np ? kFinS : h.pkt;         // (fin: stored once)
         if (np) {
+            h.cks = 0;
+            h.last = 0;
             h.len = bt.in_len[m.y];
             h.ib = reinterpret_cast<uintptr_t>(bt.in + bt.in_off[m.y]);
             h.cgen = mgen;
@@ -254,7 +355,26 @@ DEV bool slot_help_iter(const rc_batch_dev& bt, const uint32_t* mctl, uint32_t* 
         busy = true;
         const uintptr_t base = h.ib & ~static_cast<uintptr_t>(15);
         const uint4 c = chunk_load(h.ib, h.ib + h.len, base + 16 * static_cast<uintptr_t>(want), inq);
+#ifndef RC_LANE_HOST_TEST
         if (inq) *reinterpret_cast<uint4*>(slot) = c;
+#else
+        if (inq) {
+#if SLOT_MUTANT == 2
+            // (test mutant: the announcement before the slot)
+            *hctl = (want << 16) | h.cgen;
+            h.pub = *hctl;
+            SLOT_POINT();
+#endif
+            uint32_t* w = reinterpret_cast<uint32_t*>(slot);
+            w[0] = c.x; SLOT_POINT();
+            w[1] = c.y; SLOT_POINT();
+            w[2] = c.z; SLOT_POINT();
+            w[3] = c.w; SLOT_POINT();
+        }
+#endif
+        const uint32_t term = slot_mix(c, want);
+        h.cks += inq ? term : 0u;
+        h.last = inq ? term : h.last;
         h.have = inq ? want : h.have;
         h.hgen = inq ? h.cgen : h.hgen;
     }
@@ -266,6 +386,7 @@ DEV bool slot_help_iter(const rc_batch_dev& bt, const uint32_t* mctl, uint32_t* 
         __hip_atomic_store(hctl, hc, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #else
         *hctl = hc;
+        SLOT_POINT();
 #endif
         h.pub = hc;
     }

@@ -287,6 +287,14 @@ uint32_t enet_rc_config_flags(void *context);
  * context of the device (large batches: a piece's input copy under the
  * earlier pieces' kernels; ENET_RC_HOST_SPLIT), or 0 if it ran in one. */
 uint32_t enet_rc_last_split(void *context);
+/* How the last host-pointer batch (its last piece, if split) moved its data:
+ * bits 0-3 the input (1 pinned staging, 2 the caller's page-locked range by
+ * DMA, 3 strided DMA of uniform slots, 4 GPU gather over the caller's mapped
+ * range), bits 4-7 the results (1 one D2H of all slots (small batches), 2 one
+ * DMA of back-to-back slots every packet filled, 3 GPU copy into the caller's
+ * mapped slots, 4 packed on the device, D2H, scattered on the host); 0 before
+ * any host batch. */
+uint32_t enet_rc_last_host_paths(void *context);
 /* Library version string. */
 const char *enet_rc_version(void);
 

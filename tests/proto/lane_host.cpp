@@ -19,11 +19,27 @@ static const uint8_t* itab6()
 static uint32_t g_ctl6s[3];
 static SlotHelp g_sh6;
 static const rc_batch_dev* g_b6s = nullptr;
+static uint32_t g_hcks6[2], g_icks6[1];           // the hand-off's check sums (rc_slot.h slot_mix)
 namespace {
 static void slot_host_kick()
 {
     bool fin = false;
-    if (g_b6s) slot_help_iter(*g_b6s, g_ctl6s, g_ctl6s + 2, g_lds6 + 256, g_sh6, fin);
+    if (g_b6s) slot_help_iter(*g_b6s, g_ctl6s, g_ctl6s + 2, g_lds6 + 256, g_sh6, g_hcks6, 1, fin);
+}
+static void slot_host_step() { slot_host_kick(); }
+static void slot_host_point(int) {}                         // (interleavings: tests/proto/slot_sched.cpp)
+// stale-chunk injection (tests/test_lane_host.py): the k-th chunk the lane
+// takes from its slot replaced by kind 0: the chunk the slot held before it
+// (the one the lane is on), 1: the chunk after it, 2: zeros
+static int g_inj_take = -1, g_inj_kind = 0, g_inj_seen = 0;
+static uintptr_t g_inj_lo = 0, g_inj_hi = 0;
+static void slot_host_taken(uint32_t j, uint4& sl)
+{
+    if (g_inj_seen++ != g_inj_take) return;
+    const uintptr_t base = g_inj_lo & ~static_cast<uintptr_t>(15);
+    if (g_inj_kind == 0) sl = chunk_load(g_inj_lo, g_inj_hi, base + 16 * static_cast<uintptr_t>(j), true);
+    else if (g_inj_kind == 1) sl = chunk_load(g_inj_lo, g_inj_hi, base + 16 * static_cast<uintptr_t>(j + 2), true);
+    else sl = make_uint4(0u, 0u, 0u, 0u);
 }
 }  // namespace
 static uint8_t g_tab6[RC_DEC6_TAB_BYTES] __attribute__((aligned(16)));   // bucket records (never cleared)
@@ -62,6 +78,16 @@ static bool g_mtab_init = [] { for (uint32_t j = 0; j < 16; ++j) root3_mask_init
 
 static uint32_t g_dec6_unverified = 0;
 extern "C" uint32_t lane_host_dec6_unverified(void) { return g_dec6_unverified; }
+#ifdef DEC6S
+// the next decode's take-th slot chunk replaced (kind: see slot_host_taken);
+// returns the slot takes of the last decode
+extern "C" int lane_host_inject(int take, int kind)
+{
+    const int seen = g_inj_seen;
+    g_inj_take = take; g_inj_kind = kind;
+    return seen;
+}
+#endif
 
 extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, uint8_t* out, uint32_t cap,
                              uint32_t max_len, uint32_t* out_len)
@@ -87,16 +113,24 @@ extern "C" int lane_host_run(int decompress, const uint8_t* in, uint32_t len, ui
 #ifndef DEC6S
         ByteSrc src6;
         decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, g_tab6 + kTab1, itab6(), src6);
+        const bool ck = true;
 #else
         g_b6s = &b;
+        g_inj_seen = 0;
+        g_inj_lo = reinterpret_cast<uintptr_t>(in); g_inj_hi = g_inj_lo + len;
         g_ctl6s[0] = 0u; g_ctl6s[1] = kNoPktS; g_ctl6s[2] = 0u;
         slot_help_init(g_sh6);
         SlotSrc src6;
         src6.gen = 0; src6.mctl = g_ctl6s; src6.hctl = g_ctl6s + 2; src6.slot = g_lds6 + 256;
+        ws.dec6_icks = g_icks6; ws.dec6_hcks = g_hcks6;
+        g_icks6[0] = 0; g_hcks6[0] = 0; g_hcks6[1] = 0;
         decompress_one6(b, ws, 0, g_lds6, g_lds6 + kStats6, g_tab6, g_tab6 + kTab1, itab6(), src6);
+        g_ctl6s[1] = kFinS;                        // the lane is done: the helper stores its sum
+        slot_host_kick();
         g_b6s = nullptr;
+        const bool ck = cks_agree(g_icks6[0], g_hcks6[0], g_hcks6[1]);
 #endif
-        if (!counters[3] && (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len, resets[0])) {
+        if (!counters[3] && (!ck || (claims[0] & 0x7FFFFFFFu) != distinct_bigrams(out, *out_len, resets[0]))) {
             counters[3] = 1; g_dec6_unverified++;
         }
         if (!counters[3] && (claims[0] >> 31)) *out_len = 0;

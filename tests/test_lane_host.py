@@ -184,3 +184,65 @@ def test_lane_logic_dense_order2_contexts(lane):
         ref = port.compress(p, out_limit=cap)
         assert lane(0, p, cap, max_len=len(p)) == ref
         assert lane(1, ref[1], len(p), max_len=len(p)) == (len(p), p)
+
+
+def _injection_lib(extra, tag):
+    csrc = os.path.join(ROOT, "enet_amd", "csrc")
+    so = os.path.join(ROOT, "tests", "proto", f"liblanehost6s_{tag}.so")
+    src = [os.path.join(ROOT, "tests", "proto", "lane_host.cpp")] + \
+        [os.path.join(csrc, f) for f in ("rc_dec6.hip", "rc_dec6_rare.h", "rc_slot.h", "rc_lane_common.h")]
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(s) for s in src):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-DDEC6", "-DDEC6S"] + extra +
+                              ["-I", csrc, "-I", os.path.join(ROOT, "tests", "proto"), "-o", so, src[0]])
+    lib = C.CDLL(so)
+    lib.lane_host_run.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32,
+                                  C.POINTER(C.c_uint32)]
+    return lib
+
+
+def _inject_run(lib, packets):
+    """Each packet decoded once per injection kind with one chunk it takes from
+    its slot replaced (tests/proto/lane_host.cpp slot_host_taken: the chunk
+    before it -- the slot's stale content --, the one after it, or zeros);
+    returns (decodes, results that differ from the packet)."""
+    ol = C.c_uint32()
+    rng = np.random.default_rng(41)
+    total = wrong = 0
+    for p, c in packets:
+        a = np.frombuffer(c + b"\0" * 16, np.uint8).copy()
+        for kind in (0, 1, 2):
+            out = np.zeros(len(p) + 16, np.uint8)
+            lib.lane_host_inject(-1, 0)
+            lib.lane_host_run(1, a.ctypes.data, len(c), out.ctypes.data, len(p), 1400, C.byref(ol))
+            takes = lib.lane_host_inject(-1, 0)
+            if takes == 0:
+                continue
+            lib.lane_host_inject(int(rng.integers(0, takes)), kind)
+            out = np.zeros(len(p) + 16, np.uint8)
+            rc = lib.lane_host_run(1, a.ctypes.data, len(c), out.ctypes.data, len(p), 1400, C.byref(ol))
+            lib.lane_host_inject(-1, 0)
+            total += 1
+            if rc == 1 or (ol.value, out[: ol.value].tobytes()) != (len(p), p):
+                wrong += rc != 1            # (rc 1: the exact path, which reads the true stream)
+    return total, wrong
+
+
+def test_dec6s_stale_chunk_injection():
+    """A stale input chunk in the record-light decoder's slot (the r5a-type
+    failure mode: a wrong length with a success code).  The decode of other
+    bytes is a faithful decode of those bytes, so the bigram count alone lets
+    some of them through; the hand-off's check sums (rc_slot.h slot_mix,
+    compared by rc_dec6_verify) send every one to the lane kernels, which
+    decode the true stream."""
+    from oracle.pyoracle import Coder
+    port = Coder("port")
+    rng = np.random.default_rng(43)
+    packets = []
+    for _ in range(150):
+        n = int(rng.integers(100, 1400))
+        p = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        packets.append((p, port.compress(p, 2 * n + 64)[1]))
+    total, wrong = _inject_run(_injection_lib([], "cks"), packets)
+    assert total > 400 and wrong == 0, (total, wrong)
+    total0, wrong0 = _inject_run(_injection_lib(["-DSLOT_NO_CKS", "-DDEC6_NO_USED_CHECK"], "nocks"), packets)
+    assert total0 == total and wrong0 > 0, (total0, wrong0)   # the bigram count alone misses some

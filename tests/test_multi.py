@@ -139,11 +139,16 @@ def test_multi_host_batches_vs_oracle(devices):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
-def test_multi_device_batches_vs_oracle(devices):
+@pytest.mark.parametrize("devices,stage", [([0], False), ([0, 0, 0], False), ([0, 0, 0], True)])
+def test_multi_device_batches_vs_oracle(devices, stage, monkeypatch):
+    """stage: ENET_RC_MULTI_NO_PEER=1, the non-root ranges' results through the
+    root's stage buffer (rc_multi.c: the path of distinct devices) on the one
+    GPU of the test box; the gaps between slots stay untouched either way."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    if stage:
+        monkeypatch.setenv("ENET_RC_MULTI_NO_PEER", "1")
     from enet_amd import MultiCoder
     from oracle.pyoracle import fnv_digest
     d, o, l = synth.mixed_batch(20000, seed=0x4D554C55)
@@ -171,9 +176,22 @@ def test_multi_device_batches_vs_oracle(devices):
     assert (cb[mask] == 0xA5).all()
     dout = torch.zeros_like(din)
     dl = torch.zeros(n, dtype=torch.int32, device="cuda")
-    m.batch_device(True, cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
+    # decompress into gapped slots over a canary: nothing written past out_len
+    dcap = dlen + 5
+    doff2 = torch.zeros(n, dtype=torch.int64, device="cuda")
+    doff2[1:] = torch.cumsum(dcap[:-1].to(torch.int64) + gap, 0)
+    dtot = int(doff2[-1] + dcap[-1]) + gap
+    dout = torch.full((dtot,), 0x5A, dtype=torch.uint8, device="cuda")
+    dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    m.batch_device(True, cout, coff, clen, dout, doff2, dcap, dl, max_len=int(cl.max()))
     assert torch.equal(dl, dlen)
-    assert torch.equal(dout, din)
+    db, do2 = dout.cpu().numpy(), doff2.cpu().numpy()
+    dmask = np.ones(dtot, bool)
+    for i in range(n):
+        a = int(do2[i])
+        assert np.array_equal(db[a: a + int(l[i])], d[int(o[i]): int(o[i]) + int(l[i])]), i
+        dmask[a: a + int(l[i])] = False
+    assert (db[dmask] == 0x5A).all()
     m.close()
 
 
