@@ -992,7 +992,12 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
      * their CUs' issue slots; the copy's wavefronts each move a packet, so
      * smaller packets need them all to keep PCIe busy) */
     const uint32_t wgs = (c->sync_sig || c->sync_wait) && in_bytes >= 512 * (uint64_t) n ? piece_copy_wgs() : 0u;
-    int contig_out = decompress;
+    static int contig_dma = -1;       /* ENET_RC_CONTIG_DMA=0: back-to-back slots take the slot copy too */
+    if (contig_dma < 0) {
+        const char *e = getenv("ENET_RC_CONTIG_DMA");
+        contig_dma = e ? atoi(e) != 0 : 1;
+    }
+    int contig_out = decompress && contig_dma;
     for (size_t i = 1; i < n && contig_out; ++i) contig_out = out_off[i] == out_off[i - 1] + out_cap[i - 1];
     if (contig_out) {
         /* (the lengths, and the kernels done: registering the caller's range

@@ -147,7 +147,9 @@ DEV void slot_take(SlotSrc& s, const uint4& sl_in, uint32_t hc, bool en)
     const uint4& sl = sl_in;
 #endif
     s.c.x = t ? sl.x : s.c.x; s.c.y = t ? sl.y : s.c.y; s.c.z = t ? sl.z : s.c.z; s.c.w = t ? sl.w : s.c.w;
+#ifndef SLOT_NO_CKS
     s.cks += t ? slot_mix(sl, s.j + 1) : 0u;
+#endif
     s.q = t ? 0u : s.q;
     s.j += t ? 1u : 0u;
     s.want = t ? s.j + 1 : s.want;
@@ -372,9 +374,11 @@ DEV bool slot_help_iter(const rc_batch_dev& bt, const uint32_t* mctl, uint32_t* 
             w[3] = c.w; SLOT_POINT();
         }
 #endif
+#ifndef SLOT_NO_CKS
         const uint32_t term = slot_mix(c, want);
         h.cks += inq ? term : 0u;
         h.last = inq ? term : h.last;
+#endif
         h.have = inq ? want : h.have;
         h.hgen = inq ? h.cgen : h.hgen;
     }
