@@ -105,6 +105,8 @@ def _load() -> C.CDLL:
     lib.enet_rc_last_split.argtypes = [vp]
     lib.enet_rc_last_host_paths.restype = u32
     lib.enet_rc_last_host_paths.argtypes = [vp]
+    lib.enet_rc_debug_counter.restype = u32
+    lib.enet_rc_debug_counter.argtypes = [vp, u32]
     lib.enet_rc_version.restype = C.c_char_p
     lib.enet_rc_version.argtypes = []
     lib.rc_hip_lds_bytes.restype = u32

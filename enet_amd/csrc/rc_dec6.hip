@@ -192,7 +192,8 @@ DEV void sink1_finish(ByteSink1& o)
 // itself: the host build of tests/proto/lane_host.cpp, variant v6).
 template <class Src>
 DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* root,
-                         uint8_t* stats, uint8_t* tab, uint8_t* tab2, const uint8_t* itab, Src& in)
+                         uint8_t* stats, uint8_t* tab, uint8_t* tab2, const uint8_t* itab, Src& in,
+                         const double* rtab = nullptr)
 {
     constexpr bool kSlot = std::is_same<Src, SlotSrc>::value;
     const uint32_t len = bt.in_len[pkt];
@@ -277,6 +278,10 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const uint32_t esc1 = kSubEscDelta * d1, tot1 = o1 ? esc1 + kSubDelta * t1 : 1u;
 #ifdef DEC6_STATS_PREFETCH
             const uint32_t r1 = udiv16d(range, tot1, o1 ? rtn : 1.0);
+#elif defined(DEC6_RCP_TAB) && !defined(RC_LANE_HOST_TEST)
+            // (1 / the order-1 total from the block's table by the bucket byte: a
+            // lane without an order-1 code reads an entry it does not use)
+            const uint32_t r1 = udiv16d(range, tot1, rtab[st]);
 #else
             const uint32_t r1 = udiv16d(range, tot1, rcp64(tot1));
 #endif
@@ -565,16 +570,36 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
     if (!helper) *reinterpret_cast<uint2*>(mctl) = make_uint2(0u, slot < b.n ? kNoPktS : kFinS);
     else *hctl = 0u;
     if (threadIdx.x < 16) root3_inc_init(itab, threadIdx.x);
+    double* rtab = reinterpret_cast<double*>(itab + 512);
+#ifdef DEC6_RCP_TAB
+    // 1 / the order-1 total of every bucket byte (t1 | (t1 - d1) << 5: total
+    // 5 d1 + 2 t1, compress.c:536-568; 1 where t1 = 0)
+    if (threadIdx.x < 256) {
+        const uint32_t t1 = threadIdx.x & 31u, r1 = threadIdx.x >> 5;
+        const uint32_t tot = (t1 > 0 && r1 <= t1) ? kSubEscDelta * (t1 - r1) + kSubDelta * t1 : 1u;
+        rtab[threadIdx.x] = rcp64(tot);
+    }
+#endif
     __syncthreads();
     if (helper) {
         SlotHelp h;
         slot_help_init(h);
+#ifdef DEC6_HELP_COUNT
+        uint32_t nb = 0, ni = 0;     // (diagnostic: the helper's busy and idle passes, ws.counters[5..6])
+#endif
         for (;;) {
             bool fin = false;
             const bool busy = slot_help_iter(b, mctl, hctl, slotp, h, ws.dec6_hcks, ws.n_cap, fin);
+#ifdef DEC6_HELP_COUNT
+            nb += busy ? 1u : 0u;
+            ni += busy ? 0u : 1u;
+#endif
             if (fin) break;
             if (!busy) __builtin_amdgcn_s_sleep(DEC6_HELP_SLEEP);
         }
+#ifdef DEC6_HELP_COUNT
+        if ((threadIdx.x & 63) == 0) { atomicAdd(&ws.counters[5], nb); atomicAdd(&ws.counters[6], ni); }
+#endif
         return;
     }
     uint8_t* tab = static_cast<uint8_t*>(ws.dec6_pool) + static_cast<size_t>(slot) * kTab1;
@@ -588,7 +613,7 @@ extern "C" __global__ __launch_bounds__(512) void rc_decompress_dec6s(rc_batch_d
     in.gen = 0; in.mctl = mctl; in.hctl = hctl; in.slot = slotp;
     for (uint32_t i = slot; i < b.n; i += gridDim.x * kLanes6s) {
         const uint32_t pkt = order ? order[i] : i;
-        decompress_one6(b, ws, pkt, root, stats, tab, tab2, itab, in);
+        decompress_one6(b, ws, pkt, root, stats, tab, tab2, itab, in, rtab);
     }
     mctl[1] = kFinS;
 }
@@ -667,6 +692,7 @@ DEV void vresult(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t k, 
     if (l == 0 && !ok) {
         const uint32_t i = atomicAdd(&ws.counters[3], 1u);
         ws.enc2_list[i] = k;
+        if (!ck) atomicAdd(&ws.counters[7], 1u);      // (the hand-off sums disagreed: enet_rc_debug_counter 7)
     }
     if (l == 0 && ok && (cl >> 31)) b.out_len[k] = 0;     // compress.c:617
 }
@@ -823,7 +849,8 @@ extern "C" int rc_hip_dec6_launch(const rc_batch_dev* b, const rc_workspace_dev*
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (ws->lane_active != 64) return static_cast<int>(hipErrorInvalidValue);
     // (12 B more per lane than the model for the slot control words)
-    const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12) + 512;
+    // (+ root3_inc_init's table, 512 B, and the order-1 reciprocals, 2 KB)
+    const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12) + 512 + 2048;
     hipLaunchKernelGGL(rc_decompress_dec6s, dim3(blocks), dim3(512), lds, st, *b, *ws);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);

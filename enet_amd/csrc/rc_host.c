@@ -1635,6 +1635,19 @@ uint32_t enet_rc_config_flags(void *context)
 
 uint32_t enet_rc_last_split(void *context) { return context ? (uint32_t) ((rc_ctx *) context)->last_split : 0u; }
 
+uint32_t enet_rc_debug_counter(void *context, uint32_t i)
+{
+    rc_ctx *c = (rc_ctx *) context;
+    uint32_t v = 0;
+    if (!c || i >= 8 || !c->ws.counters || hipSetDevice(c->device) != hipSuccess) return 0;
+    if (hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(&v, c->ws.counters + i, 4, hipMemcpyDeviceToHost) != hipSuccess) {
+        (void) hipGetLastError();
+        return 0;
+    }
+    return v;
+}
+
 uint32_t enet_rc_last_host_paths(void *context)
 {
     const rc_ctx *c = (const rc_ctx *) context;

@@ -295,6 +295,9 @@ uint32_t enet_rc_last_split(void *context);
  * mapped slots, 4 packed on the device, D2H, scattered on the host); 0 before
  * any host batch. */
 uint32_t enet_rc_last_host_paths(void *context);
+/* Diagnostic: word i (< 8) of the context's device counter block after the
+ * last batch (synchronous read; 0 on error).  Used by tools/, not by ENet. */
+uint32_t enet_rc_debug_counter(void *context, uint32_t i);
 /* Library version string. */
 const char *enet_rc_version(void);
 

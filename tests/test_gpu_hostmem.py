@@ -118,3 +118,37 @@ def test_back_to_back_slots_keep_bytes_past_out_len(rc):
             s = int(o[i])
             assert np.array_equal(dout[s: s + int(got[i])], want[int(wo[i]): int(wo[i]) + int(wl[i])]), i
             assert (dout[s + int(got[i]): s + size] == 0x3C).all(), i
+
+
+def test_slot_handoff_many_packets_per_lane(rc):
+    """The record-light decoder's input hand-off on the hardware across packet
+    boundaries: 4 x 65536 short random packets, so every decoding lane takes
+    several packets in turn (new generations, the helper's new-packet path,
+    rc_slot.h), decoded through the device entry against the oracle; the
+    hand-off's check sums (rc_dec6_verify) must never disagree
+    (enet_rc_debug_counter 7 counts the packets they sent to the lane kernels)."""
+    import torch
+    from oracle.pyoracle import compress_batch, fnv_digest
+    n = 4 * 65536
+    d, o, l = synth.mixed_batch(n, lo=24, hi=300, seed=0x5A34)
+    want, wo, wcap, wl = compress_batch(d, o, l, "port")
+    dev = lambda a, t: torch.from_numpy(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
+    din, doff, dlen = dev(d, torch.uint8), dev(o, torch.int64), dev(l, torch.int32)
+    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+    coff = torch.zeros(n, dtype=torch.int64, device="cuda")
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64), 0)
+    cout = torch.zeros(int(coff[-1] + cap[-1]), dtype=torch.uint8, device="cuda")
+    clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    rc.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=int(l.max()))
+    torch.cuda.synchronize()
+    cl = clen.cpu().numpy().astype(np.uint32)
+    assert np.array_equal(cl, wl)
+    assert fnv_digest(cout.cpu().numpy(), coff.cpu().numpy().astype(np.uint64), cl) == fnv_digest(want, wo, wl)
+    for _ in range(3):
+        dout = torch.zeros_like(din)
+        dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+        rc.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
+        torch.cuda.synchronize()
+        assert torch.equal(dl, dlen) and torch.equal(dout, din)
+        assert rc.lib.enet_rc_debug_counter(rc.ctx, 7) == 0          # no hand-off sum mismatch
+        assert rc.last_lane_count() == 0
