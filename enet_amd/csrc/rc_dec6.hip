@@ -280,7 +280,8 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const uint32_t r1 = udiv16d(range, tot1, o1 ? rtn : 1.0);
 #elif defined(DEC6_RCP_TAB) && !defined(RC_LANE_HOST_TEST)
             // (1 / the order-1 total from the block's table by the bucket byte: a
-            // lane without an order-1 code reads an entry it does not use)
+            // lane without an order-1 code reads an entry it does not use; -0.3 %,
+            // within noise: profiles/r6/r6e_dec6_prefetch_rcptab_ab_c2.txt)
             const uint32_t r1 = udiv16d(range, tot1, rtab[st]);
 #else
             const uint32_t r1 = udiv16d(range, tot1, rcp64(tot1));
@@ -310,10 +311,19 @@ DEV void decompress_one6(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             const bool sym = rg && !eos && !past;
             range = sym ? r0 : range;
             uint32_t under0 = 0, cnt0 = 0;
+#ifndef DEC6_ITAB_LATE
+            uint4 i0, i1;
+            const uint32_t v = root3_search_inc(root, R, itab, sym ? cd0 - 1 : 0u, under0, cnt0, i0, i1);
+#else
             const uint32_t v = root3_search(root, R, sym ? cd0 - 1 : 0u, under0, cnt0);
+#endif
             dec_code_late(low, code, range, 1 + under0, 1 + cnt0, in, sym);
             if (sym) {
+#ifndef DEC6_ITAB_LATE
+                root3_add_pre(root, R, v, cnt0, i0, i1);
+#else
                 root3_add_inc(root, R, itab, v, cnt0);
+#endif
                 rtot = (rtot + kRootDelta) & 0xFFFF;
             }
             if (rare_lane(sym && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rtot > kTotalLimit))) {
@@ -849,8 +859,12 @@ extern "C" int rc_hip_dec6_launch(const rc_batch_dev* b, const rc_workspace_dev*
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (ws->lane_active != 64) return static_cast<int>(hipErrorInvalidValue);
     // (12 B more per lane than the model for the slot control words)
-    // (+ root3_inc_init's table, 512 B, and the order-1 reciprocals, 2 KB)
+    // (+ root3_inc_init's table, 512 B; -DDEC6_RCP_TAB: the order-1 reciprocals, 2 KB)
+#ifdef DEC6_RCP_TAB
     const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12) + 512 + 2048;
+#else
+    const size_t lds = static_cast<size_t>(kLanes6s) * (kLds6 + 12) + 512;
+#endif
     hipLaunchKernelGGL(rc_decompress_dec6s, dim3(blocks), dim3(512), lds, st, *b, *ws);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);

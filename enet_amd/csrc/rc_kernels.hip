@@ -1172,13 +1172,29 @@ extern "C" int rc_hip_wave_tail_launch(int decompress, const rc_batch_dev* b, co
     return static_cast<int>(hipGetLastError());
 }
 
+// The control block (counters, length bins, wide-list counters; rc_host.c)
+// cleared by one workgroup: 4.6 us, as the runtime's fill (hipMemsetAsync,
+// ENET_RC_CTL_FILL=1) of the same 3 KB (profiles/r6/r6g_ctl_clear_c2.txt).
+static_assert(RC_CTL_WORDS <= 4 * 256, "rc_ctl_clear: one uint4 per thread");
+extern "C" __global__ __launch_bounds__(256) void rc_ctl_clear(uint32_t* ctl)
+{
+    if (4 * threadIdx.x < RC_CTL_WORDS) reinterpret_cast<uint4*>(ctl)[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 static int launch(bool decompress, const rc_batch_dev* b, const rc_workspace_dev* ws, void* stream)
 {
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (b->n == 0) return 0;
     if (b->n > ws->n_cap) return static_cast<int>(hipErrorInvalidValue);
-    // the counters and the length bins (one block, rc_host.c): one fill
-    hipError_t err = hipMemsetAsync(ws->counters, 0, RC_CTL_WORDS * sizeof(uint32_t), st);
+    // the counters and the length bins (one block, rc_host.c)
+    static const bool fill = getenv("ENET_RC_CTL_FILL") != nullptr;     // (A/B: the runtime's fill)
+    hipError_t err = hipSuccess;
+    if (fill) {
+        err = hipMemsetAsync(ws->counters, 0, RC_CTL_WORDS * sizeof(uint32_t), st);
+    } else {
+        hipLaunchKernelGGL(rc_ctl_clear, dim3(1), dim3(256), 0, st, ws->counters);
+        err = hipGetLastError();
+    }
     if (err != hipSuccess) return static_cast<int>(err);
     const uint32_t max_len = b->max_len ? b->max_len : 4096;
     uint32_t lds_w;

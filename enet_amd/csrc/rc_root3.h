@@ -196,6 +196,59 @@ DEV uint32_t root3_search(const uint8_t* r, const Root& R, uint32_t code, uint32
     return 16 * g + j;
 }
 
+// root3_search that also reads the increment table's entry of the symbol's
+// group (root3_inc_init) right behind the group itself, so that the update
+// after it (root3_add_pre) waits for no LDS round trip of its own
+DEV uint32_t root3_search_inc(const uint8_t* r, const Root& R, const uint8_t* itab, uint32_t code, uint32_t& under,
+                              uint32_t& cnt, uint4& i0, uint4& i1)
+{
+    const uint32_t x1 = (code + 1) * 0x00010001u;
+    uint32_t b[8], m[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        b[i] = pk_min(pk_subsat(x1, R.d[i]), 0x00010001u);             // 1 where D <= code
+        m[i] = pk_mul(R.d[i], b[i]);
+    }
+    const uint32_t acc = pk_add(pk_add(pk_add(b[0], b[1]), pk_add(b[2], b[3])),
+                                pk_add(pk_add(b[4], b[5]), pk_add(b[6], b[7])));
+    const uint32_t pm = pk_max(pk_max(pk_max(m[0], m[1]), pk_max(m[2], m[3])),
+                               pk_max(pk_max(m[4], m[5]), pk_max(m[6], m[7])));
+    const uint32_t g = (acc & 0xFFFF) + (acc >> 16);
+    const uint32_t prev = max(pm & 0xFFFF, pm >> 16);                 // D[g - 1], 0 for g = 0
+    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (g & 15));
+    i0 = ip[0];
+    i1 = ip[1];
+    uint32_t base = prev, j = 0;
+    uint32_t s = sad(q.x, sad(q.y, 8u));
+    bool hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 8u : 0u;
+    const uint32_t d0 = hi ? q.z : q.x, d1 = hi ? q.w : q.y;
+    s = sad(d0, 4u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 4u : 0u;
+    uint32_t w = hi ? d1 : d0;
+    s = sad(w & 0xFFFFu, 2u);
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 2u : 0u;
+    w = hi ? (w >> 16) : w;
+    s = (w & 0xFFu) + 1u;
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 1u : 0u;
+    w = hi ? (w >> 8) : w;
+    under = base;
+    cnt = w & 0xFFu;
+    return 16 * g + j;
+}
+
+// root3_add_inc with the table entry of v's group already read (root3_search_inc)
+DEV void root3_add_pre(uint8_t* r, Root& R, uint32_t v, uint32_t cnt, const uint4& i0, const uint4& i1)
+{
+    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
+    R.d[0] += i0.x; R.d[1] += i0.y; R.d[2] += i0.z; R.d[3] += i0.w;
+    R.d[4] += i1.x; R.d[5] += i1.y; R.d[6] += i1.z; R.d[7] += i1.w;
+}
+
 // compress.c:90-112 for the root: halve the counts, rebuild D; returns the new total
 template <bool COPY>
 DEV uint32_t root3_rescale(uint8_t* r, Root& R)
