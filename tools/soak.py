@@ -1,0 +1,78 @@
+"""Soak run (diagnostic, GPU box): many batches through both entry kinds
+against the oracle, counting wrong results and the record-light decoder's
+hand-off sum disagreements (enet_rc_debug_counter 7).
+usage: python tools/soak.py SECONDS [OUT.json]
+Each round: a mixed batch (random packet count 20k-60k, sizes 1-1400 B or
+game state), compressed on the device and checked against the oracle by
+digest, decompressed from device memory and from host memory (gapped slots:
+the GPU gather over the caller's mapped range), each checked byte for byte."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from enet_amd import RangeCoder, synth  # noqa: E402
+from oracle.pyoracle import compress_batch, fnv_digest  # noqa: E402
+
+limit = float(sys.argv[1])
+out_path = sys.argv[2] if len(sys.argv) > 2 else None
+rc = RangeCoder()
+P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+rng = np.random.default_rng(int(time.time()) & 0xFFFF)
+t0 = time.time()
+stats = {"rounds": 0, "packets": 0, "bytes": 0, "compress_mismatch": 0, "device_wrong": 0, "host_wrong": 0,
+         "sum_disagreements": 0, "lane_handoffs": 0, "seeds": []}
+while time.time() - t0 < limit:
+    seed = int(rng.integers(1, 1 << 30))
+    n = int(rng.integers(20000, 60001))
+    if rng.random() < 0.25:
+        d, o, l = synth.gamestate_batch(n, 1200, seed=seed)
+    else:
+        d, o, l = synth.mixed_batch(n, lo=1, hi=1400, seed=seed)
+    want, wo, wcap, wl = compress_batch(d, o, l, "port")
+    din = torch.from_numpy(d).cuda()
+    doff = torch.from_numpy(o.astype(np.int64)).cuda()
+    dlen = torch.from_numpy(l.astype(np.int32)).cuda()
+    cap = (2 * dlen.to(torch.int64) + 64).to(torch.int32)
+    coff = torch.zeros(n, dtype=torch.int64, device="cuda")
+    coff[1:] = torch.cumsum(cap[:-1].to(torch.int64) + 5, 0)
+    cout = torch.zeros(int(coff[-1] + cap[-1]), dtype=torch.uint8, device="cuda")
+    clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    rc.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=int(l.max()))
+    torch.cuda.synchronize()
+    cl = clen.cpu().numpy().astype(np.uint32)
+    cb, co = cout.cpu().numpy(), coff.cpu().numpy().astype(np.uint64)
+    cm = int(not (np.array_equal(cl, wl) and fnv_digest(cb, co, cl) == fnv_digest(want, wo, wl)))
+    dout = torch.zeros_like(din)
+    dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    rc.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
+    torch.cuda.synchronize()
+    dw = int(not (torch.equal(dl, dlen) and torch.equal(dout, din)))
+    stats["sum_disagreements"] += rc.lib.enet_rc_debug_counter(rc.ctx, 7)
+    stats["lane_handoffs"] += rc.last_lane_count()
+    hout = np.zeros(d.size + 64, np.uint8)
+    hl = np.zeros(n, np.uint32)
+    l32 = l.astype(np.uint32)
+    assert rc.lib.enet_rc_decompress_batch_host(rc.ctx, P(cb), P(co), P(cl), n, P(hout), P(o), P(l32), P(hl)) == 0
+    stats["sum_disagreements"] += rc.lib.enet_rc_debug_counter(rc.ctx, 7)
+    hw = int(not (np.array_equal(hl, l32) and np.array_equal(hout[: d.size], d)))
+    stats["rounds"] += 1
+    stats["packets"] += 3 * n
+    stats["bytes"] += 3 * int(l.sum())
+    stats["compress_mismatch"] += cm
+    stats["device_wrong"] += dw
+    stats["host_wrong"] += hw
+    stats["seeds"].append(seed)
+    print(f"round {stats['rounds']} seed {seed} n {n} compress_ok {not cm} device_ok {not dw} host_ok {not hw} "
+          f"t {time.time() - t0:.0f}s", flush=True)
+stats["seconds"] = round(time.time() - t0, 1)
+rc.close()
+print(json.dumps({k: v for k, v in stats.items() if k != "seeds"}), flush=True)
+if out_path:
+    json.dump(stats, open(out_path, "w"), indent=1)
