@@ -10,6 +10,8 @@ Reads the per-dispatch counter CSVs written by tools/profile.sh (separate
           request as 64 B" under-count of MI355X_MICROARCH.md §HBM does not apply)
   write = 64*TCC_EA0_WRREQ_64B + 32*(TCC_EA0_WRREQ - TCC_EA0_WRREQ_64B)
 FETCH_SIZE / WRITE_SIZE (KiB) are reported beside them for reference.
+The request sizes are calibrated (tools/mb/calib.hip, tools/calib.sh,
+profiles/r6/calib_counters.json); the counters include Infinity-Cache hits.
 """
 import collections
 import csv
@@ -44,5 +46,11 @@ for k, cs in per.items():
         "counters": m,
     }
 json.dump({"workload": workload, "packets": packets, "source": os.path.basename(os.path.normpath(d)),
+           "note": "bytes the L2 requests from the fabric (TCC_EA0 request counters, request-size "
+                   "resolved), Infinity-Cache hits included: an upper bound of HBM traffic, not HBM "
+                   "traffic.  Request sizes calibrated on the decoders' access widths by "
+                   "tools/mb/calib.hip (profiles/r6/calib_counters.json): a 2/4/16-B store at a "
+                   "random address is one 32-B WRREQ, a 16/64-B random load one 128-B RDREQ, 48-B "
+                   "1.25; coalesced 16-B-per-lane streams exact.",
            "kernels": kernels}, open(out, "w"), indent=1)
 print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in kernels.items()}, indent=1))
