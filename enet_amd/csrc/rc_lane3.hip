@@ -538,10 +538,28 @@ struct Lane {
     uint32_t nodes;             // compress.c's nextSymbol: 1 (root) + the (context, value) pairs created
     uint32_t ldsu;              // the lane's LDS dense block holds a big order-2 context
     uint32_t cext;              // decoder: the dense order-1 block whose first links are in the LDS cache (0: none)
+    uint8_t* dm;                // the scratch record (see lane_dummy)
 };
 
-DEV void lane_init(Lane& L, uint8_t* reg)
+// The scratch record that the step's unconditional loads and stores use
+// when a lane needs none (lane_prefetch): one per wavefront, in the region
+// of its first lane, so that the lanes without a real access touch one line
+// between them -- one request that stays in the L1/L2 -- instead of 64
+// separate lines (rc_lane3's C3 fabric traffic).
+// LANE3_LANE_DUMMY (A/B): each lane's own scratch record.
+DEV uint8_t* lane_dummy(uint8_t* reg, uint8_t* wave_reg)
 {
+#ifdef LANE3_LANE_DUMMY
+    (void) wave_reg;
+    return reg + kDummyRec;
+#else
+    return (wave_reg ? wave_reg : reg) + kDummyRec;
+#endif
+}
+
+DEV void lane_init(Lane& L, uint8_t* reg, uint8_t* dm)
+{
+    L.dm = dm;
     L.epoch = next_epoch(reg, *reinterpret_cast<const uint32_t*>(reg)) & 0xFFFF;
     ctx_clear(L.cur); ctx_clear(L.prv); ctx_clear(L.q);
     L.info = 0; L.ipos = 0; L.a = 0; L.b = 0; L.order = 0; L.bump = kArena3; L.qoff = 0;
@@ -595,7 +613,7 @@ DEV void lane_prefetch(Lane& L, const uint8_t* reg, uint32_t v)
     L.nsame = L.order >= 1 && v == L.b;
     L.fromprv = !L.nsame && L.order >= 2 && !L.same && v == L.a;
     const bool ld = !L.nsame && !L.fromprv;
-    raw_load(reg, ld ? kO1Base + v * kRec : kDummyRec, L.rc);
+    raw_load(ld ? reg + kO1Base + v * kRec : L.dm, 0, L.rc);
     L.fwd = !ld;
 }
 
@@ -723,7 +741,7 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32
     const bool nsame = L.nsame, fromprv = L.fromprv;
     // (the step's last memory operation; see lane_prefetch)
     const bool st = L.order >= 2 && !L.same && !fromprv && L.prv_dirty;
-    rec1_store_at(reg, st ? kO1Base + L.a * kRec : kDummyRec, L.epoch, L.prv);
+    rec1_store_at(st ? reg + kO1Base + L.a * kRec : L.dm, 0, L.epoch, L.prv);
     // rotate: prv := cur, cur := R[v]
     Rec1 old = L.prv;
     if (L.order >= 1) {
@@ -747,7 +765,7 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32
 // ------------------------------------------------------------ one packet
 
 DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg, uint8_t* root,
-                       uint8_t* ldsb, const uint8_t* mtab)
+                       uint8_t* ldsb, const uint8_t* mtab, uint8_t* wave_reg = nullptr)
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
@@ -758,7 +776,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
     sink_init(o, bt.out + bt.out_off[pkt], cap);
     const uint32_t end = ws.lane_region;
     Lane L;
-    lane_init(L, reg);
+    lane_init(L, reg, lane_dummy(reg, wave_reg));
     Root R;
     root3_clear<true>(root, R);
     uint32_t rtot = 1 + 256;
@@ -843,7 +861,7 @@ DEV void compress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint3
 }
 
 DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uint32_t pkt, uint8_t* reg,
-                         uint8_t* root, uint8_t* ldsb, uint16_t* lc)
+                         uint8_t* root, uint8_t* ldsb, uint16_t* lc, uint8_t* wave_reg = nullptr)
 {
     const uint32_t len = bt.in_len[pkt];
     const uint32_t cap = bt.out_cap[pkt];
@@ -854,7 +872,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     ByteSrc in;
     src_init(in, bt.in + bt.in_off[pkt], len);
     Lane L;
-    lane_init(L, reg);
+    lane_init(L, reg, lane_dummy(reg, wave_reg));
     Root R;
     root3_clear<false>(root, R);
     uint32_t rtot = 1 + 256;
@@ -946,8 +964,8 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         const bool lcv = L.cur.dense != 0 && L.cext != 0 && L.cur.ext == L.cext && v < kLinkCache;
         const bool lk = L.order >= 1 && L.cur.dense != 0 && (at == 0 || (at == 2 && !lcv));
         Dense zp;
-        zp.grp = *reinterpret_cast<const uint4*>(reg + (lk ? L.cur.ext + 32 + 16 * (v >> 4) : kDummyRec));
-        zp.link = *reinterpret_cast<const uint16_t*>(reg + (lk ? L.cur.ext + 288 + 2 * v : kDummyRec));
+        zp.grp = *reinterpret_cast<const uint4*>(lk ? reg + L.cur.ext + 32 + 16 * (v >> 4) : L.dm);
+        zp.link = *reinterpret_cast<const uint16_t*>(lk ? reg + L.cur.ext + 288 + 2 * v : L.dm);
         lane_prefetch(L, reg, v);
         // the step's last code and the root's update: only the next step
         // needs them, so they run after the record load is issued (as in
@@ -1026,12 +1044,13 @@ DEV void lane3_main(const rc_batch_dev& b, const rc_workspace_dev& ws)
     const uint32_t per_block = 4 * act;
     const uint32_t slot = blockIdx.x * per_block + local;
     uint8_t* reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot) * ws.lane_region;
+    uint8_t* wave_reg = static_cast<uint8_t*>(ws.lane_pool) + static_cast<size_t>(slot - l) * ws.lane_region;
     const uint32_t* order = ws.order && !ws.bins[RC_LEN_BINS] ? ws.order : nullptr;
     const uint32_t count = ws.sub_count ? *ws.sub_count : b.n;   // a sub-list: the two-pass encoder's leftovers
     for (uint32_t i = slot; i < count; i += gridDim.x * per_block) {
         const uint32_t pkt = ws.sub_list ? ws.sub_list[i] : (order ? order[i] : i);
-        if (DECOMP) decompress_one3(b, ws, pkt, reg, root, ldsb, lc);
-        else compress_one3(b, ws, pkt, reg, root, ldsb, mtab);
+        if (DECOMP) decompress_one3(b, ws, pkt, reg, root, ldsb, lc, wave_reg);
+        else compress_one3(b, ws, pkt, reg, root, ldsb, mtab, wave_reg);
     }
 }
 

@@ -91,11 +91,13 @@ __device__ __forceinline__ uint32_t udiv_lo16(uint32_t a, uint32_t b)
     return q & 0xFFFF;
 }
 #else
-inline uint32_t udiv(uint32_t a, uint32_t b) { return a / b; }
-inline uint32_t udiv16(uint32_t a, uint32_t b) { return a / b; }
-inline uint32_t udiv16r(uint32_t a, uint32_t b, float) { return a / b; }
+// (host test build: a quotient by 0 -- computed and discarded by lanes a
+// step does not concern, as on the GPU, where it does not trap -- reads 0)
+inline uint32_t udiv(uint32_t a, uint32_t b) { return b ? a / b : 0u; }
+inline uint32_t udiv16(uint32_t a, uint32_t b) { return b ? a / b : 0u; }
+inline uint32_t udiv16r(uint32_t a, uint32_t b, float) { return b ? a / b : 0u; }
 inline float rcp16(uint32_t b) { return 1.0f / static_cast<float>(b); }
 inline double rcp64(uint32_t b) { return 1.0 / static_cast<double>(b); }
-inline uint32_t udiv16d(uint32_t a, uint32_t b, double) { return a / b; }
-inline uint32_t udiv_lo16(uint32_t a, uint32_t b) { return (a / b) & 0xFFFF; }
+inline uint32_t udiv16d(uint32_t a, uint32_t b, double) { return b ? a / b : 0u; }
+inline uint32_t udiv_lo16(uint32_t a, uint32_t b) { return b ? (a / b) & 0xFFFF : 0u; }
 #endif
