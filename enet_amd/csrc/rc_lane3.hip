@@ -128,6 +128,112 @@ DEV void ctx_clear(Ctx<NV, O2>& c)
     for (uint32_t d = 0; d < (O2 ? NV : 1); ++d) { c.oa[d] = 0u; c.ob[d] = 0u; }
 }
 
+// ------------------------------------------------------- the hot block
+// The decoder keeps the counts of the packet's first dense order-1 context
+// (the one whose first links the LDS cache holds, L.cext) in registers: its
+// 16 groups, 64 VGPRs.  On game state that context (byte 0) takes ~86 % of
+// the dense order-1 steps; its lookups (a search's group, a find's group),
+// updates and rescales then touch no memory, where each was a dependent
+// random read.  C rides in the record as for any dense
+// order-1 context; the links stay in the arena behind the LDS link cache.
+// The block's counts in the arena are left as they were when it became hot:
+// nothing reads them afterwards.
+// Measured, and off: the block lives in AGPRs (the kernel's 256 VGPRs are
+// taken), so each lookup is 64 AGPR reads and 60 selects, each update as
+// many again, for any lane of the wavefront in the hot context (most steps);
+// C3 rc_decompress_lane3 5.70 -> 6.13 ms although its fabric traffic fell
+// 16.3 -> 15.2 GB (profiles/r6/r6m_lane3_hot_block_c3.txt).  -DLANE3_HOT: on.
+#ifdef LANE3_HOT
+constexpr bool kHot = true;
+#else
+constexpr bool kHot = false;
+#endif
+struct Hot { uint4 g[16]; };
+
+DEV uint4 sel_u4(bool p, const uint4& a, const uint4& b)
+{
+    return make_uint4(p ? a.x : b.x, p ? a.y : b.y, p ? a.z : b.z, p ? a.w : b.w);
+}
+
+// p ? a : b where the compiler cannot see a select: a select between two
+// elements of the block becomes a load from a lane-varying address, which
+// would put the block in scratch memory
+#ifndef RC_LANE_HOST_TEST
+DEV uint32_t vsel(bool p, uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(__builtin_amdgcn_ballot_w64(p)));
+    return r;
+}
+#else
+DEV uint32_t vsel(bool p, uint32_t a, uint32_t b) { return p ? a : b; }
+#endif
+DEV uint4 vsel_u4(bool p, const uint4& a, const uint4& b)
+{
+    return make_uint4(vsel(p, a.x, b.x), vsel(p, a.y, b.y), vsel(p, a.z, b.z), vsel(p, a.w, b.w));
+}
+
+// group g of the hot block (a select tree on the bits of g: registers only)
+DEV uint4 hot_get(const Hot& H, uint32_t g)
+{
+    uint4 t8[8], t4[4], t2[2];
+    const bool b0 = (g & 1u) != 0, b1 = (g & 2u) != 0, b2 = (g & 4u) != 0, b3 = (g & 8u) != 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) t8[k] = vsel_u4(b0, H.g[2 * k + 1], H.g[2 * k]);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) t4[k] = vsel_u4(b1, t8[2 * k + 1], t8[2 * k]);
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) t2[k] = vsel_u4(b2, t4[2 * k + 1], t4[2 * k]);
+    return vsel_u4(b3, t2[1], t2[0]);
+}
+
+// group g := q where en
+DEV void hot_put(Hot& H, uint32_t g, const uint4& q, bool en)
+{
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) H.g[k] = sel_u4(en && g == k, q, H.g[k]);
+}
+
+// compress.c:90-112 on the hot block where en: halve, the new C; returns the sum
+DEV uint32_t hot_rescale(Hot& H, uint4& c0, uint4& c1, bool en)
+{
+    uint32_t sum = 0, cw[8];
+#pragma unroll
+    for (uint32_t g = 0; g < 16; ++g) {
+        uint4 q = H.g[g];
+        q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
+        q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
+        q.z -= (q.z >> 1) & 0x7F7F7F7Fu;
+        q.w -= (q.w >> 1) & 0x7F7F7F7Fu;
+        H.g[g] = sel_u4(en, q, H.g[g]);
+        sum = sad(q.w, sad(q.z, sad(q.y, sad(q.x, sum))));
+        if (g & 1) cw[g >> 1] |= sum << 16; else cw[g >> 1] = sum;
+    }
+    c0 = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    c1 = make_uint4(cw[4], cw[5], cw[6], cw[7]);
+    return sum;
+}
+
+// dense_add (rc_lane_common.h) on z alone where en: count[v] += d, C[g..15] += d
+DEV void dense_bump(Dense& z, uint32_t v, uint32_t d, bool en)
+{
+    const uint32_t g = v >> 4, j = v & 15, bd = en ? d << (8 * (j & 3)) : 0u, q = j >> 2;
+    z.grp.x += q == 0 ? bd : 0u; z.grp.y += q == 1 ? bd : 0u;
+    z.grp.z += q == 2 ? bd : 0u; z.grp.w += q == 3 ? bd : 0u;
+    uint32_t cw[8] = {z.c0.x, z.c0.y, z.c0.z, z.c0.w, z.c1.x, z.c1.y, z.c1.z, z.c1.w};
+    cum_add(cw, g, en ? d : 0u);
+    z.c0 = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    z.c1 = make_uint4(cw[4], cw[5], cw[6], cw[7]);
+}
+
+// is c (an order-1 context) the hot block
+// (on: the caller keeps a hot block -- a template flag, never a test of the
+// block's address, which would keep the block out of registers)
+DEV bool is_hot(bool on, uint32_t cext, uint32_t dense, uint32_t ext)
+{
+    return kHot && on && cext != 0 && dense != 0 && ext == cext;
+}
+
 // order-1 record: w0 tag | len << 16 | dense << 24, w1 esc | tot << 16, w2 ext,
 // w4..6 val, w7..9 cnt, w10..12 oa, w13..15 ob.  A tag other than the epoch
 // reads as an empty context.
@@ -352,6 +458,89 @@ DEV bool ctx_search(const uint8_t* reg, const uint8_t* ldsb, const Ctx<NV, O2>& 
     return ok;
 }
 
+// ctx_search of the decoder's order-1 context c: a dense one's group from the
+// hot block's registers where c is the hot block (else its load), and its
+// link from the LDS link cache where that holds it (else its load); either
+// load is issued only when some lane of the wavefront needs it
+DEV bool o1_search(const uint8_t* reg, const Rec1& c, const Hot& H, uint32_t cext, const uint16_t* lc,
+                   uint32_t code, Look<3>& h, uint32_t& v)
+{
+    uint32_t acc = 0, base = 0, wc = 0, wv = 0xFFFFFFFFu, j = 0;
+    bool hit = false;
+#pragma unroll
+    for (uint32_t d = 0; d < 3; ++d) {
+        const uint32_t s = sad(c.cnt[d], 0u);
+        const bool here = !hit && code < acc + s;
+        base = here ? acc : base; wc = here ? c.cnt[d] : wc; wv = here ? c.val[d] : wv; j = here ? 4 * d : j;
+        hit = hit || here;
+        acc += s;
+    }
+    uint32_t s = sad(wc & 0xFFFFu, 0u);
+    bool hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 2u : 0u;
+    wc = hi ? (wc >> 16) : wc; wv = hi ? (wv >> 16) : wv;
+    s = wc & 0xFFu;
+    hi = code >= base + s;
+    base += hi ? s : 0u; j += hi ? 1u : 0u;
+    wc = hi ? (wc >> 8) : wc; wv = hi ? (wv >> 8) : wv;
+    h.k = j; h.under = base; h.cnt = wc & 0xFFu; v = wv & 0xFFu;
+#pragma unroll
+    for (uint32_t d = 0; d < 3; ++d) h.eq[d] = byte_mask(static_cast<int>(j), d) & 0x01010101u;
+    h.info = slot_info<3, true>(c, h.eq);
+    bool ok = hit && h.cnt != 0;
+    if (any_lane(c.dense != 0)) {
+        if (c.dense != 0) {
+            const bool hot = is_hot(true, cext, c.dense, c.ext);
+            Dense z;
+            rec_c_get(c, z.c0, z.c1);
+            uint32_t g = 0, prev = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 16; ++t) {
+                const uint32_t ct = dense_c(z, t);
+                const bool below = ct <= code;
+                g += below ? 1u : 0u;
+                prev = below ? ct : prev;
+            }
+            const bool inside = g < 16;
+            g = inside ? g : 15u;
+            uint4 grp = make_uint4(0u, 0u, 0u, 0u);
+            if (any_lane(!hot)) {
+                if (!hot) grp = *reinterpret_cast<const uint4*>(reg + c.ext + 32 + 16 * g);
+            }
+            if (any_lane(hot)) grp = sel_u4(hot, hot_get(H, g), grp);
+            z.grp = grp;
+            uint32_t bs = prev, jj = 0;
+            uint32_t t = sad(grp.x, sad(grp.y, 0u));
+            bool up = code >= bs + t;
+            bs += up ? t : 0u; jj += up ? 8u : 0u;
+            const uint32_t d0 = up ? grp.z : grp.x, d1 = up ? grp.w : grp.y;
+            t = sad(d0, 0u);
+            up = code >= bs + t;
+            bs += up ? t : 0u; jj += up ? 4u : 0u;
+            uint32_t w = up ? d1 : d0;
+            t = sad(w & 0xFFFFu, 0u);
+            up = code >= bs + t;
+            bs += up ? t : 0u; jj += up ? 2u : 0u;
+            w = up ? (w >> 16) : w;
+            t = w & 0xFFu;
+            up = code >= bs + t;
+            bs += up ? t : 0u; jj += up ? 1u : 0u;
+            w = up ? (w >> 8) : w;
+            const uint32_t vv = 16 * g + jj, cnt = w & 0xFFu;
+            const bool lch = hot && vv < kLinkCache;
+            uint32_t link = lc[vv & (kLinkCache - 1)];
+            if (any_lane(!lch)) {
+                if (!lch) link = *reinterpret_cast<const uint16_t*>(reg + c.ext + 288 + 2 * vv);
+            }
+            z.link = link;
+            ok = inside && cnt != 0 && code < bs + cnt;
+            h.under = bs; h.cnt = cnt; v = vv; h.info = link; h.z = z;
+        }
+    }
+    h.found = ok ? 1u : 0u;
+    return ok;
+}
+
 // insert (v, count 2, o2 info 0) at slot k of an inline context with a free slot
 template <uint32_t NV, bool O2>
 DEV void inline_insert(Ctx<NV, O2>& c, uint32_t k, uint32_t v, bool en)
@@ -455,8 +644,8 @@ DEV bool densify(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c, ui
 }
 
 // compress.c:90-112 where `en`
-template <uint32_t NV, bool O2>
-DEV void ctx_rescale(uint8_t* reg, uint8_t* ldsb, Ctx<NV, O2>& c, bool en)
+template <uint32_t NV, bool O2, bool HOT = false>
+DEV void ctx_rescale(uint8_t* reg, uint8_t* ldsb, Ctx<NV, O2>& c, bool en, Hot* H = nullptr, uint32_t cext = 0)
 {
     if (!rare_lane(en)) return;
     uint32_t sum = 0;
@@ -466,8 +655,15 @@ DEV void ctx_rescale(uint8_t* reg, uint8_t* ldsb, Ctx<NV, O2>& c, bool en)
         c.cnt[d] = en ? h : c.cnt[d];
         sum = sad(h, sum);
     }
-    if (rare_lane(en && c.dense != 0)) {
-        if (en && c.dense != 0) {
+    const bool hot = O2 && is_hot(HOT, cext, c.dense, c.ext);
+    if (O2 && HOT && rare_lane(en && hot)) {     // (registers only)
+        uint4 c0, c1;
+        const uint32_t hs = hot_rescale(*H, c0, c1, en && hot);
+        sum = (en && hot) ? hs : sum;
+        rec_c_set(c, c0, c1, en && hot);
+    }
+    if (rare_lane(en && c.dense != 0 && !hot)) {
+        if (en && c.dense != 0 && !hot) {
             if (!O2 && c.dense == 2) sum = dense_rescale(ldsb);
             else sum = dense_rescale(reg + c.ext);
             if (O2) {                           // (the halving above hit the record's copy of C: the new C)
@@ -483,9 +679,9 @@ DEV void ctx_rescale(uint8_t* reg, uint8_t* ldsb, Ctx<NV, O2>& c, bool en)
 // compress.c:293-314 (and the decoder's patch, :598-615) where `en`, given
 // the lookup h of v: bump v or insert it, then total and rescale.  h.k stays
 // the slot of v.
-template <uint32_t NV, bool O2>
+template <uint32_t NV, bool O2, bool HOT = false>
 DEV void ctx_update(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c, Look<NV>& h, uint32_t v,
-                    uint32_t& bump, uint32_t end, bool& ovf, bool en)
+                    uint32_t& bump, uint32_t end, bool& ovf, bool en, Hot* H = nullptr, uint32_t cext = 0)
 {
     const bool ins = en && !h.found;
     const bool inl = c.dense == 0;
@@ -502,8 +698,21 @@ DEV void ctx_update(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c,
         }
         if (en && c.dense != 0 && !ovf) {                                   // (new: o2 info is 0)
             if (!O2 && c.dense == 2) dense_add(ldsb, v, kSubDelta, h.z);
-            else dense_add(reg + c.ext, v, kSubDelta, h.z);
+            else if (!(O2 && is_hot(HOT, cext, c.dense, c.ext))) dense_add(reg + c.ext, v, kSubDelta, h.z);
             rec_c_set(c, h.z.c0, h.z.c1, true);
+        }
+    }
+    // the hot block (registers): a bump or an insert, its group and C
+    if (O2 && HOT) {
+        const bool hot = en && !ovf && is_hot(HOT, cext, c.dense, c.ext);
+        if (any_lane(hot)) {
+            Dense z = h.z;
+            dense_bump(z, v, kSubDelta, hot);
+            hot_put(*H, v >> 4, z.grp, hot);
+            h.z.grp = sel_u4(hot, z.grp, h.z.grp);
+            h.z.c0 = sel_u4(hot, z.c0, h.z.c0);
+            h.z.c1 = sel_u4(hot, z.c1, h.z.c1);
+            rec_c_set(c, z.c0, z.c1, hot);
         }
     }
     if (ins && c.dense == 0) {
@@ -514,7 +723,7 @@ DEV void ctx_update(uint8_t* reg, uint8_t* ldsb, uint32_t& ldsu, Ctx<NV, O2>& c,
     c.esc += ins ? kSubEscDelta : 0u;
     const uint32_t tot = (c.tot + (ins ? kSubEscDelta : 0u) + kSubDelta) & 0xFFFF;
     c.tot = en ? tot : c.tot;
-    ctx_rescale<NV, O2>(reg, ldsb, c, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit));
+    ctx_rescale<NV, O2, HOT>(reg, ldsb, c, en && (h.cnt > 0xFF - 2 * kSubDelta || tot > kTotalLimit), H, cext);
 }
 
 // ------------------------------------------------------------ lane state
@@ -631,9 +840,9 @@ DEV void o2_stats(const Lane& L, uint32_t& esc, uint32_t& tot)
 //   1. update the o2 context (a, b): bump v (at == 2) or insert it
 //   2. update the o1 context b (at <= 1): bump or insert
 //   3. the o2 info of (b, v) and where it lives, the loads for step i+1
-template <bool HAVE_H1>
+template <bool HAVE_H1, bool HOT = false>
 DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32_t v, int at, Look<3>& h1,
-                      Look<6>& h2, bool new0, bool track, uint16_t* lc = nullptr)
+                      Look<6>& h2, bool new0, bool track, uint16_t* lc = nullptr, Hot* H = nullptr)
 {
     // nodes compress.c creates this step: v in each visited context that lacks
     // it (the order-2 context is always visited, order 1 when order 2 did not
@@ -705,7 +914,7 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32
         if (track) created += h1.found ? 0u : 1u;
         bool ovf = L.ovf != 0;
         const bool was = L.cur.dense != 0;
-        ctx_update<3, true>(reg, ldsb, L.ldsu, L.cur, h1, v, L.bump, end, ovf, true);
+        ctx_update<3, true, HOT>(reg, ldsb, L.ldsu, L.cur, h1, v, L.bump, end, ovf, true, H, L.cext);
         L.ovf = ovf;
         // the decoder's first dense order-1 block: its links for symbols below
         // kLinkCache copied to the lane's LDS cache (once per packet)
@@ -716,6 +925,16 @@ DEV void lane_advance(Lane& L, uint8_t* reg, uint8_t* ldsb, uint32_t end, uint32
                 uint4* dst = reinterpret_cast<uint4*>(lc);
 #pragma unroll
                 for (uint32_t k = 0; k < 2 * kLinkCache / 16; ++k) dst[k] = src[k];
+            }
+            // (and its counts into the registers: it is the hot block from here on)
+            if (HOT) {
+                const bool nh = !was && L.cur.dense != 0 && L.cext == L.cur.ext && !L.ovf;
+                const uint4* gp = reinterpret_cast<const uint4*>(reg + (nh ? L.cext + 32 : kDummyRec));
+                uint4 q[16];
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) q[k] = gp[nh ? k : 0];
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) H->g[k] = sel_u4(nh, q[k], H->g[k]);
             }
         }
     }
@@ -882,6 +1101,9 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
     in.na -= 4;
     src_refill(in, true);
     bool fail = false, anomaly = false;
+    Hot H;                                   // (meaningful once L.cext is set)
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) H.g[k] = make_uint4(0u, 0u, 0u, 0u);
 
     PROF_DECL
     for (;;) {
@@ -926,7 +1148,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
             if (cd < L.cur.esc) {
                 dec_code(low, code, range, 0, L.cur.esc, in, true);
             } else {
-                if (!ctx_search<3, true>(reg, ldsb, L.cur, cd - L.cur.esc, h1, v)) { fail = true; break; }
+                if (!o1_search(reg, L.cur, H, L.cext, lc, cd - L.cur.esc, h1, v)) { fail = true; break; }
                 fu = L.cur.esc + h1.under; fc = h1.cnt;
                 at = 1;
             }
@@ -963,9 +1185,12 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // before the next record (the scratch record for lanes without one)
         const bool lcv = L.cur.dense != 0 && L.cext != 0 && L.cur.ext == L.cext && v < kLinkCache;
         const bool lk = L.order >= 1 && L.cur.dense != 0 && (at == 0 || (at == 2 && !lcv));
+        // (the hot block's group from registers and, below symbol kLinkCache, its
+        // link from the LDS cache: those lanes load the scratch record)
+        const bool hotc = L.order >= 1 && is_hot(true, L.cext, L.cur.dense, L.cur.ext);
         Dense zp;
-        zp.grp = *reinterpret_cast<const uint4*>(lk ? reg + L.cur.ext + 32 + 16 * (v >> 4) : L.dm);
-        zp.link = *reinterpret_cast<const uint16_t*>(lk ? reg + L.cur.ext + 288 + 2 * v : L.dm);
+        zp.grp = *reinterpret_cast<const uint4*>(lk && !hotc ? reg + L.cur.ext + 32 + 16 * (v >> 4) : L.dm);
+        zp.link = *reinterpret_cast<const uint16_t*>(lk && !lcv ? reg + L.cur.ext + 288 + 2 * v : L.dm);
         lane_prefetch(L, reg, v);
         // the step's last code and the root's update: only the next step
         // needs them, so they run after the record load is issued (as in
@@ -981,6 +1206,8 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         // holds v
         {
             const uint32_t lcl = lc[v & (kLinkCache - 1)];     // (read by every lane: its own register)
+            if (any_lane(lk && hotc)) zp.grp = sel_u4(lk && hotc, hot_get(H, v >> 4), zp.grp);
+            zp.link = lcv ? lcl : zp.link;
             if (L.order >= 1 && (at == 0 || (at == 2 && !lcv))) h1 = ctx_find_pre(L.cur, v, zp);
             const bool ul = at == 2 && L.order >= 1 && lcv;
             h1.info = ul ? lcl : h1.info;
@@ -989,7 +1216,7 @@ DEV void decompress_one3(const rc_batch_dev& bt, const rc_workspace_dev& ws, uin
         if (at != 2 && L.order >= 2 && info_big(L.info)) h2 = ctx_find<6, false>(reg, ldsb, L.q, v);
         fail = o.n >= o.cap;                                         // compress.c:617
         PROF(4)
-        lane_advance<true>(L, reg, ldsb, end, v, at, h1, h2, new0, true, lc); // (see compress_one3)
+        lane_advance<true, kHot>(L, reg, ldsb, end, v, at, h1, h2, new0, true, lc, &H); // (see compress_one3)
         PROF(5)
         if (fail || L.ovf) break;
         if (rare_lane(L.nodes >= kNodeLimit)) {                      // compress.c:617-621 -> :148-157
