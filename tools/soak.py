@@ -1,7 +1,10 @@
 """Soak run (diagnostic, GPU box): many batches through both entry kinds
 against the oracle, counting wrong results and the record-light decoder's
 hand-off sum disagreements (enet_rc_debug_counter 7).
-usage: python tools/soak.py SECONDS [OUT.json]
+usage: python tools/soak.py SECONDS [OUT.json] [PHASE_LOG]
+PHASE_LOG: the phase about to run is written (and flushed) there before each
+step, and every step ends in a device-wide synchronize, so that an
+asynchronously reported device error is pinned to the step before it.
 Each round: a mixed batch (random packet count 20k-60k, sizes 1-1400 B or
 game state), compressed on the device and checked against the oracle by
 digest, decompressed from device memory and from host memory (gapped slots:
@@ -22,6 +25,13 @@ from oracle.pyoracle import compress_batch, fnv_digest  # noqa: E402
 
 limit = float(sys.argv[1])
 out_path = sys.argv[2] if len(sys.argv) > 2 else None
+phase_log = open(sys.argv[3], "w") if len(sys.argv) > 3 else None
+
+
+def phase(name):
+    if phase_log:
+        phase_log.write(f"{time.time() - t0:.1f} {name}\n")
+        phase_log.flush()
 rc = RangeCoder()
 P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
 rng = np.random.default_rng(int(time.time()) & 0xFFFF)
@@ -31,11 +41,14 @@ stats = {"rounds": 0, "packets": 0, "bytes": 0, "compress_mismatch": 0, "device_
 while time.time() - t0 < limit:
     seed = int(rng.integers(1, 1 << 30))
     n = int(rng.integers(20000, 60001))
-    if rng.random() < 0.25:
+    game = rng.random() < 0.25
+    phase(f"round {stats['rounds'] + 1} seed {seed} n {n} game {int(game)}: inputs")
+    if game:
         d, o, l = synth.gamestate_batch(n, 1200, seed=seed)
     else:
         d, o, l = synth.mixed_batch(n, lo=1, hi=1400, seed=seed)
     want, wo, wcap, wl = compress_batch(d, o, l, "port")
+    phase("h2d")
     din = torch.from_numpy(d).cuda()
     doff = torch.from_numpy(o.astype(np.int64)).cuda()
     dlen = torch.from_numpy(l.astype(np.int32)).cuda()
@@ -44,6 +57,8 @@ while time.time() - t0 < limit:
     coff[1:] = torch.cumsum(cap[:-1].to(torch.int64) + 5, 0)
     cout = torch.zeros(int(coff[-1] + cap[-1]), dtype=torch.uint8, device="cuda")
     clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    phase("device compress")
     rc.compress_batch(din, doff, dlen, cout, coff, cap, clen, max_len=int(l.max()))
     torch.cuda.synchronize()
     cl = clen.cpu().numpy().astype(np.uint32)
@@ -51,6 +66,8 @@ while time.time() - t0 < limit:
     cm = int(not (np.array_equal(cl, wl) and fnv_digest(cb, co, cl) == fnv_digest(want, wo, wl)))
     dout = torch.zeros_like(din)
     dl = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    phase("device decompress")
     rc.decompress_batch(cout, coff, clen, dout, doff, dlen, dl, max_len=int(cl.max()))
     torch.cuda.synchronize()
     dw = int(not (torch.equal(dl, dlen) and torch.equal(dout, din)))
@@ -59,9 +76,15 @@ while time.time() - t0 < limit:
     hout = np.zeros(d.size + 64, np.uint8)
     hl = np.zeros(n, np.uint32)
     l32 = l.astype(np.uint32)
+    torch.cuda.synchronize()
+    phase("host decompress")
     assert rc.lib.enet_rc_decompress_batch_host(rc.ctx, P(cb), P(co), P(cl), n, P(hout), P(o), P(l32), P(hl)) == 0
+    phase(f"host decompress returned, paths {rc.lib.enet_rc_last_host_paths(rc.ctx)} split {rc.lib.enet_rc_last_split(rc.ctx)}")
+    torch.cuda.synchronize()
     stats["sum_disagreements"] += rc.lib.enet_rc_debug_counter(rc.ctx, 7)
     hw = int(not (np.array_equal(hl, l32) and np.array_equal(hout[: d.size], d)))
+    torch.cuda.synchronize()
+    phase("checked")
     stats["rounds"] += 1
     stats["packets"] += 3 * n
     stats["bytes"] += 3 * int(l.sum())
