@@ -8,7 +8,9 @@ asynchronously reported device error is pinned to the step before it.
 Each round: a mixed batch (random packet count 20k-60k, sizes 1-1400 B or
 game state), compressed on the device and checked against the oracle by
 digest, decompressed from device memory and from host memory (gapped slots:
-the GPU gather over the caller's mapped range), each checked byte for byte."""
+the GPU gather over the caller's mapped range), each checked byte for byte,
+and compressed again from host memory into gapped host slots (checked
+against the oracle by digest)."""
 import ctypes as C
 import json
 import os
@@ -37,6 +39,7 @@ P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
 rng = np.random.default_rng(int(time.time()) & 0xFFFF)
 t0 = time.time()
 stats = {"rounds": 0, "packets": 0, "bytes": 0, "compress_mismatch": 0, "device_wrong": 0, "host_wrong": 0,
+         "host_compress_mismatch": 0,
          "sum_disagreements": 0, "lane_handoffs": 0, "seeds": []}
 while time.time() - t0 < limit:
     seed = int(rng.integers(1, 1 << 30))
@@ -84,15 +87,26 @@ while time.time() - t0 < limit:
     stats["sum_disagreements"] += rc.lib.enet_rc_debug_counter(rc.ctx, 7)
     hw = int(not (np.array_equal(hl, l32) and np.array_equal(hout[: d.size], d)))
     torch.cuda.synchronize()
+    phase("host compress")
+    hco = co.copy()
+    hcap = (2 * l32 + 64).astype(np.uint32)
+    hcb = np.zeros(int(hco[-1]) + int(hcap[-1]) + 64, np.uint8)
+    hcl = np.zeros(n, np.uint32)
+    assert rc.lib.enet_rc_compress_batch_host(rc.ctx, P(d), P(o), P(l32), n, P(hcb), P(hco), P(hcap), P(hcl)) == 0
+    torch.cuda.synchronize()
+    hcm = int(not (np.array_equal(hcl, wl) and fnv_digest(hcb, hco, hcl) == fnv_digest(want, wo, wl)))
+    torch.cuda.synchronize()
     phase("checked")
     stats["rounds"] += 1
-    stats["packets"] += 3 * n
-    stats["bytes"] += 3 * int(l.sum())
+    stats["packets"] += 4 * n
+    stats["bytes"] += 4 * int(l.sum())
+    stats["host_compress_mismatch"] += hcm
     stats["compress_mismatch"] += cm
     stats["device_wrong"] += dw
     stats["host_wrong"] += hw
     stats["seeds"].append(seed)
     print(f"round {stats['rounds']} seed {seed} n {n} compress_ok {not cm} device_ok {not dw} host_ok {not hw} "
+          f"host_compress_ok {not hcm} "
           f"t {time.time() - t0:.0f}s", flush=True)
 stats["seconds"] = round(time.time() - t0, 1)
 rc.close()
