@@ -2,6 +2,7 @@
 against the oracle, counting wrong results and the record-light decoder's
 hand-off sum disagreements (enet_rc_debug_counter 7).
 usage: python tools/soak.py SECONDS [OUT.json] [PHASE_LOG]
+       python tools/soak.py replay SEED N GAME   (one round with those inputs, return codes printed)
 PHASE_LOG: the phase about to run is written (and flushed) there before each
 step, and every step ends in a device-wide synchronize, so that an
 asynchronously reported device error is pinned to the step before it.
@@ -25,9 +26,12 @@ sys.path.insert(0, ROOT)
 from enet_amd import RangeCoder, synth  # noqa: E402
 from oracle.pyoracle import compress_batch, fnv_digest  # noqa: E402
 
-limit = float(sys.argv[1])
-out_path = sys.argv[2] if len(sys.argv) > 2 else None
-phase_log = open(sys.argv[3], "w") if len(sys.argv) > 3 else None
+replay = sys.argv[1] == "replay"
+limit = 1e9 if replay else float(sys.argv[1])
+out_path = sys.argv[2] if len(sys.argv) > 2 and not replay else None
+phase_log = open(sys.argv[3], "w") if len(sys.argv) > 3 and not replay else None
+if replay:
+    phase_log = sys.stdout
 
 
 def phase(name):
@@ -39,12 +43,16 @@ P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
 rng = np.random.default_rng(int(time.time()) & 0xFFFF)
 t0 = time.time()
 stats = {"rounds": 0, "packets": 0, "bytes": 0, "compress_mismatch": 0, "device_wrong": 0, "host_wrong": 0,
-         "host_compress_mismatch": 0,
+         "host_compress_mismatch": 0, "host_call_errors": [],
          "sum_disagreements": 0, "lane_handoffs": 0, "seeds": []}
 while time.time() - t0 < limit:
     seed = int(rng.integers(1, 1 << 30))
     n = int(rng.integers(20000, 60001))
     game = rng.random() < 0.25
+    if replay:
+        if stats["rounds"]:
+            break
+        seed, n, game = int(sys.argv[2]), int(sys.argv[3]), bool(int(sys.argv[4]))
     phase(f"round {stats['rounds'] + 1} seed {seed} n {n} game {int(game)}: inputs")
     if game:
         d, o, l = synth.gamestate_batch(n, 1200, seed=seed)
@@ -81,8 +89,11 @@ while time.time() - t0 < limit:
     l32 = l.astype(np.uint32)
     torch.cuda.synchronize()
     phase("host decompress")
-    assert rc.lib.enet_rc_decompress_batch_host(rc.ctx, P(cb), P(co), P(cl), n, P(hout), P(o), P(l32), P(hl)) == 0
-    phase(f"host decompress returned, paths {rc.lib.enet_rc_last_host_paths(rc.ctx)} split {rc.lib.enet_rc_last_split(rc.ctx)}")
+    hrc = rc.lib.enet_rc_decompress_batch_host(rc.ctx, P(cb), P(co), P(cl), n, P(hout), P(o), P(l32), P(hl))
+    phase(f"host decompress returned {hrc}, paths {rc.lib.enet_rc_last_host_paths(rc.ctx)} "
+          f"split {rc.lib.enet_rc_last_split(rc.ctx)}")
+    if hrc != 0:
+        stats["host_call_errors"].append([stats["rounds"] + 1, "decompress", hrc, seed, n, int(game)])
     torch.cuda.synchronize()
     stats["sum_disagreements"] += rc.lib.enet_rc_debug_counter(rc.ctx, 7)
     hw = int(not (np.array_equal(hl, l32) and np.array_equal(hout[: d.size], d)))
@@ -92,7 +103,10 @@ while time.time() - t0 < limit:
     hcap = (2 * l32 + 64).astype(np.uint32)
     hcb = np.zeros(int(hco[-1]) + int(hcap[-1]) + 64, np.uint8)
     hcl = np.zeros(n, np.uint32)
-    assert rc.lib.enet_rc_compress_batch_host(rc.ctx, P(d), P(o), P(l32), n, P(hcb), P(hco), P(hcap), P(hcl)) == 0
+    hrc = rc.lib.enet_rc_compress_batch_host(rc.ctx, P(d), P(o), P(l32), n, P(hcb), P(hco), P(hcap), P(hcl))
+    phase(f"host compress returned {hrc}, paths {rc.lib.enet_rc_last_host_paths(rc.ctx)}")
+    if hrc != 0:
+        stats["host_call_errors"].append([stats["rounds"] + 1, "compress", hrc, seed, n, int(game)])
     torch.cuda.synchronize()
     hcm = int(not (np.array_equal(hcl, wl) and fnv_digest(hcb, hco, hcl) == fnv_digest(want, wo, wl)))
     torch.cuda.synchronize()
