@@ -385,6 +385,14 @@ void enet_range_coder_destroy(void *context)
     ctx_release(c);
 }
 
+/* (as rc_fail, for the device-pointer path) */
+static int rc_fail_dev(int err, int line)
+{
+    if (err && getenv("ENET_RC_DEBUG"))
+        fprintf(stderr, "enet_rc: batch failed at rc_host.c:%d: %d (%s)\n", line, err, hipGetErrorString((hipError_t) err));
+    return err;
+}
+
 static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
                       const uint32_t *in_len, size_t n, uint32_t max_len, uint32_t max_out, uint8_t *out,
                       const uint64_t *out_off, const uint32_t *out_cap, uint32_t *out_len,
@@ -395,7 +403,7 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     if (n == 0) return 0;
     if (n > 0xFFFFFFFFu) return (int) hipErrorInvalidValue;
     if (hipSetDevice(c->device) != hipSuccess) return (int) hipErrorInvalidDevice;
-    if (ws_reserve(c, n) != 0) return (int) hipErrorOutOfMemory;
+    if (ws_reserve(c, n) != 0) return rc_fail_dev((int) hipErrorOutOfMemory, __LINE__);
     rc_batch_dev b;
     b.in = in; b.in_off = in_off; b.in_len = in_len;
     b.out = out; b.out_off = out_off; b.out_cap = out_cap; b.out_len = out_len;
@@ -405,8 +413,8 @@ static int run_device(rc_ctx *c, int decompress, const uint8_t *in, const uint64
     /* the lane pool and the encoder's record stream only for batches that run
      * on the lane path (small batches run on the wave kernel without them) */
     if (rc_hip_uses_lanes(decompress, &b, &c->ws)) {
-        if (lanes_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
-        if (!decompress && enc2_reserve(c, n, max_len) != 0) return (int) hipErrorOutOfMemory;
+        if (lanes_reserve(c, n, max_len) != 0) return rc_fail_dev((int) hipErrorOutOfMemory, __LINE__);
+        if (!decompress && enc2_reserve(c, n, max_len) != 0) return rc_fail_dev((int) hipErrorOutOfMemory, __LINE__);
     }
     /* stream is a hipStream_t; NULL is HIP's default (null) stream */
     return decompress ? rc_hip_decompress(&b, &c->ws, stream) : rc_hip_compress(&b, &c->ws, stream);
@@ -774,6 +782,17 @@ static hipError_t d2h_copy(void *dst, const void *src, size_t bytes, hipStream_t
     return err;
 }
 
+/* A host batch's failure, with the line that saw it, on stderr when
+ * ENET_RC_DEBUG is set (a failed call returns the HIP error either way) */
+static int rc_fail(int err, int line)
+{
+    static int dbg = -1;
+    if (dbg < 0) dbg = getenv("ENET_RC_DEBUG") != NULL;
+    if (dbg && err) fprintf(stderr, "enet_rc: host batch failed at rc_host.c:%d: %d (%s)\n", line, err,
+                            hipGetErrorString((hipError_t) err));
+    return err;
+}
+
 static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t *in_off,
                     const uint32_t *in_len, size_t n, uint8_t *out, const uint64_t *out_off,
                     const uint32_t *out_cap, uint32_t *out_len, int allow_pin,
@@ -869,7 +888,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
     const size_t blocks = (n + 1023) / 1024;
     if (stage_reserve(c, a_soff + n * 8) != 0 || pack_reserve(c, out_bytes + 16, blocks) != 0) {
         host_unpin(in + zc_lo, zc_pin);
-        return (int) hipErrorOutOfMemory;
+        return rc_fail((int) hipErrorOutOfMemory, __LINE__);
     }
     uint8_t *h = c->h_stage, *d = c->d_stage;
     uint64_t *hio = (uint64_t *) (h + a_ioff);
@@ -898,7 +917,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         if (r > 0) (void) hipStreamWaitEvent(c->stream, y->ev, 0);
     }
     hipError_t err = h2d_copy(d + a_ioff, h + a_ioff, a_olen - a_ioff, c->stream);
-    if (err != hipSuccess) { host_unpin(in + zc_lo, zc_pin); return (int) err; }
+    if (err != hipSuccess) { host_unpin(in + zc_lo, zc_pin); return rc_fail((int) err, __LINE__); }
     /* the payload: straight from the caller's memory when it is one range and
      * can be page-locked; else in four packet groups through pinned staging,
      * the staging copy of group k+1 overlapping the DMA of group k */
@@ -923,7 +942,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         if (pin_in || zc_pin) hipStreamSynchronize(c->stream);
         host_unpin(in + in_lo, pin_in);
         host_unpin(in + zc_lo, zc_pin);
-        return (int) err;
+        return rc_fail((int) err, __LINE__);
     }
     c->last_paths = zc_dev ? 4u : pitch ? 3u : pin_in ? 2u : 1u;
     const int ig = pin_in || zc_pin ? 0 : in_bytes >= (16u << 20) ? 4 : 1;
@@ -935,7 +954,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         else if (packed_in) par_memcpy(h + a_in + b0, in + in_lo + b0, b1 - b0);
         else par_scatter(h + a_in, hio, in, in_off, in_len, lo, hi, b1 - b0);
         if (b1 > b0) err = hipMemcpyAsync(d + a_in + b0, h + a_in + b0, b1 - b0, hipMemcpyHostToDevice, c->stream);
-        if (err != hipSuccess) return (int) err;
+        if (err != hipSuccess) return rc_fail((int) err, __LINE__);
     }
     if (c->sync_sig) {              /* its input DMA is enqueued: the next piece's may follow */
         h2d_sync_set(c->sync_sig, hipEventRecord(c->sync_sig->ev, c->stream) == hipSuccess ? 1 : -1);
@@ -952,7 +971,7 @@ static int run_host(rc_ctx *c, int decompress, const uint8_t *in, const uint64_t
         host_unpin(in + in_lo, pin_in);
         host_unpin(in + zc_lo, zc_pin);
     }
-    return rc;
+    return rc ? rc_fail(rc, __LINE__) : 0;
 }
 
 /* The results of run_host's kernels into the caller's slots; returns after
@@ -972,7 +991,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
         err = hipMemcpyAsync(h + a_olen, d + a_olen, total - 16 - a_olen, hipMemcpyDeviceToHost, c->stream);
         if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
-        if (err != hipSuccess) return (int) err;
+        if (err != hipSuccess) return rc_fail((int) err, __LINE__);
         memcpy(out_len, h + a_olen, n * 4);
         for (size_t i = 0; i < n; ++i)
             if (out_len[i]) memcpy(out + out_off[i], h + a_out + out_off[i], out_len[i]);
@@ -1005,7 +1024,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
          * batch finds its range registered already) */
         err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
         if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
-        if (err != hipSuccess) return (int) err;
+        if (err != hipSuccess) return rc_fail((int) err, __LINE__);
         const uint32_t *ol = (const uint32_t *) (h + a_olen);
         for (size_t i = 0; i < n && contig_out; ++i) contig_out = ol[i] == out_cap[i];
     }
@@ -1019,7 +1038,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
             const hipError_t e2 = hipStreamSynchronize(c->stream);
             host_unpin(out + out_off[0], pin_out);
             if (err == hipSuccess) err = e2;
-            if (err != hipSuccess) return (int) err;
+            if (err != hipSuccess) return rc_fail((int) err, __LINE__);
             memcpy(out_len, h + a_olen, n * 4);
             if (prof) {
                 tp[5] = now_ms();
@@ -1054,7 +1073,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
             const hipError_t e2 = hipStreamSynchronize(c->stream);
             host_unpin(out + lo, op);
             if (err == hipSuccess) err = e2;
-            if (err != hipSuccess) return (int) err;
+            if (err != hipSuccess) return rc_fail((int) err, __LINE__);
             memcpy(out_len, h + a_olen, n * 4);
             if (prof) {
                 tp[5] = now_ms();
@@ -1070,18 +1089,18 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
     }
     rc = rc_hip_pack(d + a_out, (const uint64_t *) (d + a_ooff), (const uint32_t *) (d + a_olen), (uint32_t) n,
                      c->d_bsum, c->d_pack, (void *) c->stream);
-    if (rc != 0) return rc;
+    if (rc != 0) return rc_fail(rc, __LINE__);
     uint64_t packed = 0;
     err = hipMemcpyAsync(h + a_olen, d + a_olen, n * 4, hipMemcpyDeviceToHost, c->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(&c->last_exact, c->ws.counters, 4, hipMemcpyDeviceToHost, c->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(&packed, c->d_bsum + blocks, 8, hipMemcpyDeviceToHost, c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
-    if (err != hipSuccess) return (int) err;
+    if (err != hipSuccess) return rc_fail((int) err, __LINE__);
     if (prof) tp[4] = now_ms();
-    if (packed > out_bytes) return (int) hipErrorUnknown;
+    if (packed > out_bytes) return rc_fail((int) hipErrorUnknown, __LINE__);
     memcpy(out_len, h + a_olen, n * 4);
     uint64_t *poff = (uint64_t *) malloc((n + 1) * sizeof(uint64_t));
-    if (!poff) return (int) hipErrorOutOfMemory;
+    if (!poff) return rc_fail((int) hipErrorOutOfMemory, __LINE__);
     uint64_t acc = 0;
     for (size_t i = 0; i < n; ++i) { poff[i] = acc; acc += out_len[i]; }
     poff[n] = acc;
@@ -1113,7 +1132,7 @@ static int host_results(rc_ctx *c, int decompress, size_t n, uint8_t *out, const
                 tp[5] - tp[4], tp[5] - tp[0]);
     }
     c->last_paths |= 4u << 4;
-    return err == hipSuccess ? 0 : (int) err;
+    return err == hipSuccess ? 0 : rc_fail((int) err, __LINE__);
 }
 
 /* ---- a large host batch in pieces, on this context and further contexts
