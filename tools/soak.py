@@ -3,6 +3,9 @@ against the oracle, counting wrong results and the record-light decoder's
 hand-off sum disagreements (enet_rc_debug_counter 7).
 usage: python tools/soak.py SECONDS [OUT.json] [PHASE_LOG]
        python tools/soak.py replay SEED N GAME   (one round with those inputs, return codes printed)
+SOAK_POOL=k: the rounds draw from k batches made (with their oracle outputs)
+at the start instead of a new batch each round -- the same calls, many more
+rounds per minute (the oracle's compress on the CPU is most of a round).
 PHASE_LOG: the phase about to run is written (and flushed) there before each
 step, and every step ends in a device-wide synchronize, so that an
 asynchronously reported device error is pinned to the step before it.
@@ -42,6 +45,14 @@ rc = RangeCoder()
 P = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
 rng = np.random.default_rng(int(time.time()) & 0xFFFF)
 t0 = time.time()
+pool = []
+for i in range(int(os.environ.get("SOAK_POOL", "0"))):
+    sd, nn, gm = int(rng.integers(1, 1 << 30)), int(rng.integers(20000, 60001)), bool(rng.random() < 0.25)
+    dd, oo, ll = synth.gamestate_batch(nn, 1200, seed=sd) if gm else synth.mixed_batch(nn, lo=1, hi=1400, seed=sd)
+    pool.append((sd, nn, gm, dd, oo, ll, compress_batch(dd, oo, ll, "port")))
+if pool:
+    print(f"pool of {len(pool)} batches ready", flush=True)
+    t0 = time.time()
 stats = {"rounds": 0, "packets": 0, "bytes": 0, "compress_mismatch": 0, "device_wrong": 0, "host_wrong": 0,
          "host_compress_mismatch": 0, "host_call_errors": [],
          "sum_disagreements": 0, "lane_handoffs": 0, "seeds": []}
@@ -53,12 +64,15 @@ while time.time() - t0 < limit:
         if stats["rounds"]:
             break
         seed, n, game = int(sys.argv[2]), int(sys.argv[3]), bool(int(sys.argv[4]))
+    if pool:
+        seed, n, game, d, o, l, (want, wo, wcap, wl) = pool[int(rng.integers(0, len(pool)))]
     phase(f"round {stats['rounds'] + 1} seed {seed} n {n} game {int(game)}: inputs")
-    if game:
-        d, o, l = synth.gamestate_batch(n, 1200, seed=seed)
-    else:
-        d, o, l = synth.mixed_batch(n, lo=1, hi=1400, seed=seed)
-    want, wo, wcap, wl = compress_batch(d, o, l, "port")
+    if not pool:
+        if game:
+            d, o, l = synth.gamestate_batch(n, 1200, seed=seed)
+        else:
+            d, o, l = synth.mixed_batch(n, lo=1, hi=1400, seed=seed)
+        want, wo, wcap, wl = compress_batch(d, o, l, "port")
     phase("h2d")
     din = torch.from_numpy(d).cuda()
     doff = torch.from_numpy(o.astype(np.int64)).cuda()
