@@ -6,7 +6,11 @@ oracle's.  Stops at the first failed call or wrong result and prints it.
 usage: python tools/hoststress.py SECONDS [OUT.json]
 (ENET_RC_DEBUG=1 adds the failing call site in rc_host.c to stderr;
 ENET_RC_NO_HOST_PIN=1 runs the same calls with caller memory never
-page-locked -- the A/B this tool exists for)"""
+page-locked -- the A/B this tool exists for, DESIGN.md §2a.
+HOSTSTRESS_MMAP=1: each call's output buffer is a fresh anonymous mapping
+the process has never touched, as a large new allocation from the C library
+often is.)"""
+import mmap
 import ctypes as C
 import json
 import os
@@ -50,7 +54,11 @@ while time.time() - t0 < limit:
     # decompress from gapped host slots (a fresh copy of the oracle's streams in them)
     # into a fresh back-to-back buffer
     cb = cb0.copy()
-    hout = np.zeros(d.size + 64, np.uint8)
+    if os.environ.get("HOSTSTRESS_MMAP") == "1":
+        mo = mmap.mmap(-1, d.size + 64)
+        hout = np.frombuffer(mo, dtype=np.uint8)
+    else:
+        hout = np.zeros(d.size + 64, np.uint8)
     hl = np.zeros(n, np.uint32)
     r = rc.lib.enet_rc_decompress_batch_host(rc.ctx, P(cb), P(co), P(wl), n, P(hout), P(o), P(l), P(hl))
     stats["calls"] += 1
@@ -60,7 +68,11 @@ while time.time() - t0 < limit:
                           "split": int(rc.lib.enet_rc_last_split(rc.ctx))}
         break
     # compress into fresh gapped host slots
-    hcb = np.zeros(int(co[-1]) + int(2 * l[-1]) + 128, np.uint8)
+    if os.environ.get("HOSTSTRESS_MMAP") == "1":
+        mc = mmap.mmap(-1, int(co[-1]) + int(2 * l[-1]) + 128)
+        hcb = np.frombuffer(mc, dtype=np.uint8)
+    else:
+        hcb = np.zeros(int(co[-1]) + int(2 * l[-1]) + 128, np.uint8)
     hcl = np.zeros(n, np.uint32)
     hcap = (2 * l + 64).astype(np.uint32)
     r = rc.lib.enet_rc_compress_batch_host(rc.ctx, P(d), P(o), P(l), n, P(hcb), P(co), P(hcap), P(hcl))
