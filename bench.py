@@ -604,17 +604,18 @@ def pcie_inclusive(coder, d, o, l, args):
     bc, bd, ok = measure(lambda k: np.zeros(k, np.uint8))
     res = {"value": round(nb / (bc + bd) / GIB, 4), "unit": "GiB/s",
            "compress_GiBps": round(nb / bc / GIB, 4), "decompress_GiBps": round(nb / bd / GIB, 4),
-           "bit_exact": ok, "note": "enet_rc_*_batch_host from pageable caller buffers, page-locked for the call: "
-                   "a back-to-back input DMA'd directly, slots at a uniform pitch one strided DMA, other gapped "
-                   "inputs gathered by a GPU kernel over PCIe; kernels; outputs that fill their slots DMA'd into "
-                   "place, others written from their device slots into the caller's slots by a GPU kernel "
-                   "over PCIe; best of 5 (the first call creates the pieces' contexts, and one of the next few often "
-                   "meets a 15-20 ms stall in a copy)"}
+           "bit_exact": ok, "note": "enet_rc_*_batch_host from pageable caller buffers, through the library's "
+                   "pinned staging (host copies on the pieces' threads, DMA, kernels, DMA, host copies; caller "
+                   "memory is not page-locked per call by default, DESIGN.md 2a); best of 5 (the first call "
+                   "creates the pieces' contexts)"}
     pc, pd, pok = measure(lambda k: torch.zeros(k, dtype=torch.uint8).pin_memory().numpy())
     res["pinned_caller"] = {"value": round(nb / (pc + pd) / GIB, 4), "compress_GiBps": round(nb / pc / GIB, 4),
                             "decompress_GiBps": round(nb / pd / GIB, 4), "bit_exact": pok,
                             "note": "the same calls with the caller's data buffers page-locked beforehand "
-                                    "(pinned host memory): no per-call registration; best of 5"}
+                                    "(pinned host memory): a back-to-back input DMA'd directly, other gapped "
+                                    "inputs gathered by a GPU kernel over PCIe; outputs that fill their slots "
+                                    "DMA'd into place, others written into the caller's slots by a GPU kernel; "
+                                    "best of 5"}
     return res
 
 

@@ -664,8 +664,8 @@ static int pack_reserve(rc_ctx *c, size_t bytes, size_t blocks)
  * whole range lies inside that one allocation or registration: DMA'd
  * directly, left registered; 0: not usable (the call failed, or the range
  * only touches memory some other caller registered, whose registration may
- * end during our transfer) -- the staging path then.  The batch calls on
- * host pointers page-lock caller memory for the length of the call. */
+ * end during our transfer) -- the staging path then.  Pageable caller memory
+ * is page-locked for the call only with ENET_RC_HOST_REGISTER=1 (below). */
 static int host_pin(const void *p, size_t bytes)
 {
     static int off = -1;
@@ -684,6 +684,17 @@ static int host_pin(const void *p, size_t bytes)
         return 0;
     }
     (void) hipGetLastError();
+    /* Pageable caller memory is page-locked for the call only on request
+     * (ENET_RC_HOST_REGISTER=1): soak runs interleaving host and device calls
+     * met a GPU memory fault in the one-DMA result copy into such a range
+     * (about one call in 6000), and none in 24308 calls with it off
+     * (profiles/r6/r6z*); the pinned staging serves instead. */
+    static int reg = -1;
+    if (reg < 0) {
+        const char *e = getenv("ENET_RC_HOST_REGISTER");
+        reg = e && atoi(e) == 1;
+    }
+    if (!reg) return 0;
     const uintptr_t a = (uintptr_t) p & ~(uintptr_t) 4095, e = ((uintptr_t) p + bytes + 4095) & ~(uintptr_t) 4095;
     if (hipHostRegister((void *) a, e - a, hipHostRegisterDefault) == hipSuccess) return 1;
     (void) hipGetLastError();
@@ -1200,16 +1211,18 @@ static int run_host_split(rc_ctx *c, int decompress, const uint8_t *in, const ui
             else { k = i + 1; break; }
         }
     const int pi = k > 1 ? host_pin(in + ilo, ihi - ilo) : 0;
-    const int po = pi ? host_pin(out + olo, ohi - olo) : 0;
+    const int po = host_pin(out + olo, ohi - olo);
     struct h2d_sync y[SPLIT_MAX - 1];
     int ny = 0;
-    for (; po && ny < k - 1; ++ny) {
+    /* (pieces of pageable caller memory, pi = po = 0, take each piece's pinned
+     * staging: their host copies then run on the pieces' threads side by side) */
+    for (; ny < k - 1; ++ny) {
         if (hipEventCreateWithFlags(&y[ny].ev, hipEventDisableTiming) != hipSuccess) break;
         pthread_mutex_init(&y[ny].m, NULL);
         pthread_cond_init(&y[ny].cv, NULL);
         y[ny].ready = 0;
     }
-    if (ny < k - 1) {               /* (no further context, pinning or event: one piece) */
+    if (ny < k - 1) {               /* (no further context or event: one piece) */
         for (int i = 0; i < ny; ++i) {
             hipEventDestroy(y[i].ev);
             pthread_cond_destroy(&y[i].cv);

@@ -2,10 +2,12 @@
 host_results), against the oracle:
 
 - the GPU gather of a gapped compressed input over the caller's mapped,
-  page-locked range (rc_gather16, registered per call with hipHostRegister)
-  when the CPU rewrites that buffer between calls, and when the buffer is
-  freed and a new one takes its pages -- the round-5 review's candidate (b)
-  for the r5a wrong decode (stale lines of re-registered pages);
+  page-locked range (rc_gather16 over a buffer the caller page-locked) when
+  the CPU rewrites that buffer between calls, and when the buffer is freed
+  and a new one takes its place -- the round-5 review's candidate (b) for the
+  r5a wrong decode (stale lines of mapped pages); the same batches from
+  pageable memory take the pinned staging (pageable caller memory is not
+  page-locked per call unless ENET_RC_HOST_REGISTER=1, DESIGN.md §2a);
 - back-to-back output slots that some packets do not fill (corrupt streams):
   the caller's bytes past each out_len stay as they were, as compress.c
   writes only what it decodes (round-5 ADVICE: the one-DMA result path).
@@ -33,13 +35,22 @@ def rc():
     c.close()
 
 
+def _pinned(nbytes, fill=None):
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8).pin_memory().numpy()
+    if fill is not None:
+        a[:] = fill
+    return a
+
+
 def _oracle_streams(d, o, l):
     from oracle.pyoracle import compress_batch
     out, oo, cap, ol = compress_batch(d, o, l, "port")
     return [out[int(oo[i]): int(oo[i]) + int(ol[i])] for i in range(len(l))]
 
 
-def test_zero_copy_input_rewritten_between_calls(rc):
+@pytest.mark.parametrize("mem", ["pinned", "pageable"])
+def test_zero_copy_input_rewritten_between_calls(rc, mem):
     n = 30000
     a = synth.mixed_batch(n, seed=0x5A31)
     b = synth.mixed_batch(n, seed=0x5A32)
@@ -66,7 +77,8 @@ def test_zero_copy_input_rewritten_between_calls(rc):
         got = np.zeros(n, np.uint32)
         assert rc.lib.enet_rc_decompress_batch_host(rc.ctx, P(buf), P(coff), P(lens), n, P(dout), P(oo), P(ln),
                                                     P(got)) == 0
-        assert rc.lib.enet_rc_last_host_paths(rc.ctx) & 0xF == 4        # the GPU gather over the mapped range
+        # the GPU gather over the caller's mapped range, or the pinned staging
+        assert rc.lib.enet_rc_last_host_paths(rc.ctx) & 0xF == (4 if mem == "pinned" else 1)
         assert np.array_equal(got, ln), (np.nonzero(got != ln)[0][:8], rc.last_lane_count())
         bad = []
         for i in range(n):
@@ -76,7 +88,7 @@ def test_zero_copy_input_rewritten_between_calls(rc):
                 bad.append(i)
         assert not bad, bad[:8]
 
-    buf = np.full(total, 0xEE, np.uint8)
+    buf = _pinned(total, 0xEE) if mem == "pinned" else np.full(total, 0xEE, np.uint8)
     which = np.zeros(n, np.int8)
     check(buf, fill(buf, which), which)
     which = np.ones(n, np.int8)                   # every stream rewritten by the CPU in place
@@ -84,13 +96,13 @@ def test_zero_copy_input_rewritten_between_calls(rc):
     which = (np.arange(n) % 2).astype(np.int8)    # half of them back
     check(buf, fill(buf, which), which)
     del buf                                        # a new buffer, likely on the same pages
-    buf = np.empty(total, np.uint8)
-    buf[:] = 0x11
+    buf = _pinned(total, 0x11) if mem == "pinned" else np.full(total, 0x11, np.uint8)
     which = np.zeros(n, np.int8)
     check(buf, fill(buf, which), which)
 
 
-def test_back_to_back_slots_keep_bytes_past_out_len(rc):
+@pytest.mark.parametrize("mem", ["pinned", "pageable"])
+def test_back_to_back_slots_keep_bytes_past_out_len(rc, mem):
     from oracle.pyoracle import compress_batch, decompress_batch
     n, size = 4000, 1200
     d, o, l = synth.random_batch(n, size, seed=0x5A33)
@@ -106,14 +118,15 @@ def test_back_to_back_slots_keep_bytes_past_out_len(rc):
         if trial == "clean":
             out, oo, ocap, ol = compress_batch(d, o, l, "port")
             want, wo, wl = decompress_batch(out, oo, ol, l)
-        dout = np.full(n * size + 64, 0x3C, np.uint8)
+        dout = _pinned(n * size + 64, 0x3C) if mem == "pinned" else np.full(n * size + 64, 0x3C, np.uint8)
         got = np.zeros(n, np.uint32)
         l32 = l.astype(np.uint32)
         assert rc.lib.enet_rc_decompress_batch_host(rc.ctx, P(out), P(oo), P(ol), n, P(dout), P(o), P(l32),
                                                     P(got)) == 0
         assert np.array_equal(got, wl)
         paths = rc.lib.enet_rc_last_host_paths(rc.ctx) >> 4
-        assert (paths == 2) == (trial == "clean"), paths     # one DMA of the span only when every slot is full
+        # one DMA of the span into a page-locked buffer only when every slot is full
+        assert (paths == 2) == (trial == "clean" and mem == "pinned"), paths
         for i in range(n):
             s = int(o[i])
             assert np.array_equal(dout[s: s + int(got[i])], want[int(wo[i]): int(wo[i]) + int(wl[i])]), i
