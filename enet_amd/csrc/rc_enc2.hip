@@ -1567,24 +1567,41 @@ DEV uint32_t wa_of(uint32_t w) { return (w >> kWA) & 255; }
 constexpr uint32_t kWRst = 1u << 18, kWLeft = 1u << 19;
 [[maybe_unused]] constexpr uint32_t kWideLong = 4096;          // rc_enc2_wscan_l: segments of up to this many positions
 
-// L: the longest packet of the launch (its positions); two sizes are built,
-// 2048 and 1216 -- the smaller one leaves room for 9 wavefronts per CU
-// instead of 6 (the scan is latency-bound: LDS and ballots)
+// L: the longest packet of the launch (its positions); three sizes are built,
+// 4096, 2048 and 1216.  The scan is latency-bound (LDS round trips and
+// ballots on each wavefront's own path), so its speed is the number of
+// resident wavefronts, which LDS sets: the 1216 layout is 13.2 KB, 12 per CU
+// (17.7 KB and 9 per CU before the bucket padding was dropped and the walk
+// tables moved into x).
+//
+// A big bucket's long runs: a run is the elements j of bucket p with one a =
+// x[j-2]; an element j with a != p has x[j-2] != p, so j - 1 is no element of
+// the bucket -- at most L / 2 elements have a != p, so at most L / 66 runs
+// with a != p exceed kWideDense (32) visits, plus the run a = p.
+template <uint32_t L>
+constexpr uint32_t wide_runs_max() { return L / 64 + 2; }
+
 template <uint32_t L>
 struct WScanLdsT {
-    // the window's bytes at x[16 + mis + i]; then a big bucket's run sizes / starts (2 KB)
-    uint8_t  x[L <= 2048 ? 16 + 2048 + 16 : 16 + L + 16];
-    uint32_t cnt[256];                // bucket sizes, then fill pointers
-    uint32_t start[256];              // bucket starts (4-aligned)
-    uint32_t e[L + 768];              // elements in bucket order (wide element words)
+    // the window's bytes at x[16 + mis + i]; while the big buckets are walked
+    // (x is not read then) the walk's table, the long runs and their count
+    // (wtab / wruns / wnruns)
+    uint8_t  x[16 + L + 16];
+    uint32_t cnt[256];                // bucket sizes, then fill pointers; a big bucket's run sizes by a
+    uint32_t start[256];              // bucket starts; a big bucket's run starts, then run ends
+    uint32_t e[L];                    // elements in bucket order (wide element words), buckets back to back
     uint32_t sw[L];                   // a big bucket's element words by a, then its order-1 visits
     uint32_t f2bits[L / 32];          // positions found at order 2 (big buckets; every bucket in a
                                       // packet that can reach the model reset)
-    uint32_t rootbits[L / 32];        // ... positions coded at the root (a packet that can reset)
-    uint32_t tab[64];                 // dense walk: a round's updated counts (256 bytes); rank counts
-    uint32_t runs[64];                // a big bucket's long runs (a keys)
-    uint32_t nruns;
+    uint32_t rootbits[L > kE2MaxLen ? L / 32 : 1];   // ... positions coded at the root (a packet that can reset)
 };
+static_assert(sizeof(WScanLdsT<kWideSmallL>) <= 13312, "12 wide-scan wavefronts per CU");
+
+// dense walk: a round's updated counts (256 bytes); the lane-order probe
+template <uint32_t L> DEV uint32_t* wtab(WScanLdsT<L>& s) { return reinterpret_cast<uint32_t*>(s.x); }
+template <uint32_t L> DEV uint32_t* wruns(WScanLdsT<L>& s) { return reinterpret_cast<uint32_t*>(s.x) + 64; }
+template <uint32_t L> DEV uint32_t* wnruns(WScanLdsT<L>& s) { return reinterpret_cast<uint32_t*>(s.x) + 64 + wide_runs_max<L>(); }
+static_assert(4 * (64 + wide_runs_max<kWideSmallL>() + 1) <= 16 + kWideSmallL + 16, "walk tables inside x");
 
 
 // cnt[key] += 1 for every lane with ok: one LDS atomic per distinct key (its
@@ -1609,7 +1626,7 @@ DEV uint32_t group_add(uint32_t* cnt, uint32_t key, bool ok)
 // the identity interval: a code that changes nothing
 constexpr uint32_t kNoCodeLo = 1u << 16;        // under 0, count 1
 constexpr uint32_t kNoCodeTot = 1u;
-constexpr uint32_t kPadWord = 0xFFFFFFFFu;      // bucket padding in WScanLds::e
+constexpr uint32_t kPadWord = 0xFFFFFFFFu;      // no element (a lane past WScanLds::e's elements)
 
 // explicit interval of a sub-context visit from its statistics (t earlier
 // visits, dist of them new, same / less earlier visits of this / a smaller
@@ -1667,8 +1684,8 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec, bool
             const uint32_t ld = static_cast<uint32_t>(__builtin_ctzll(nt));
             const uint32_t lbs = __builtin_amdgcn_readlane(bs, ld), lbe = __builtin_amdgcn_readlane(be, ld);
             const uint32_t lsm = __builtin_amdgcn_readlane(small ? 1u : 0u, ld);
-            nextW = lsm ? lbs : (lbe + 3) & ~3u;
-            nextW = max(nextW, W + (ld ? 0u : 4u));  // (progress: a first lane never taken is a big bucket's)
+            nextW = lsm ? lbs : lbe;
+            nextW = max(nextW, W + (ld ? 0u : 1u));  // (progress: a first lane never taken is a big bucket's)
         }
         const uint64_t am = __builtin_amdgcn_ballot_w64(act);
         if (am) {
@@ -1783,10 +1800,11 @@ template <class S>
 DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, uint2* wrec, bool track = false)
 {
     const uint32_t t = lane_id();
-    uint8_t* sc = reinterpret_cast<uint8_t*>(s.tab);   // a round's final counts of its symbols (0: untouched)
+    uint32_t* tab = wtab(s);
+    uint8_t* sc = reinterpret_cast<uint8_t*>(tab);     // a round's final counts of its symbols (0: untouched)
     uint32_t tabr = 0, pre = 0;
     uint32_t esc = 0, tot = 0;                        // (wave-uniform)
-    s.tab[t] = 0;
+    tab[t] = 0;
     wave_sync();
 #pragma unroll 1
     for (uint32_t base = 0; base < m;) {
@@ -1838,8 +1856,8 @@ DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, ui
         const uint64_t later = t == 63 ? 0ull : (m_mine & cm) >> (t + 1);
         if (commit && later == 0) sc[v] = static_cast<uint8_t>(c + kSubDelta);
         wave_sync();
-        const uint32_t nw = s.tab[t];
-        s.tab[t] = 0;
+        const uint32_t nw = tab[t];
+        tab[t] = 0;
         tabr = (tabr & ~nonzero_bytes(nw)) | nw;
         const uint32_t ncm = popc64(cm), nnew = popc64(nm & cm);
         esc += kSubEscDelta * nnew;
@@ -1865,14 +1883,16 @@ DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, ui
 
 // a big bucket of a wide packet (> kE2Bucket elements, [bs, bs + k) in
 // position order), the whole wavefront
-template <class S>
-DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp, bool ordered, bool track)
+template <uint32_t L>
+DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp, bool ordered, bool track)
 {
     const uint32_t t = lane_id();
-    uint32_t* hist = reinterpret_cast<uint32_t*>(s.x);          // [256] run sizes by a
-    uint32_t* rst = hist + 256;                                  // [256] run starts, then run ends
+    uint32_t* hist = s.cnt;                                      // [256] run sizes by a
+    uint32_t* rst = s.start;                                     // [256] run starts, then run ends
+    uint32_t* runs = wruns(s);
+    uint32_t* nruns = wnruns(s);
     *reinterpret_cast<uint4*>(&hist[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
-    if (t == 0) s.nruns = 0;
+    if (t == 0) *nruns = 0;
     wave_sync();
     // order 2: the elements' a (position 1 has none: its record half A is the identity)
 #pragma unroll 1
@@ -1923,14 +1943,14 @@ DEV void wide_big_bucket(S& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp,
 #pragma unroll 1
     for (uint32_t r = 0; r < 4; ++r) {
         const uint32_t a = 4 * t + r;
-        if (hist[a] > kWideDense) s.runs[atomicAdd(&s.nruns, 1u)] = a;
+        if (hist[a] > kWideDense) runs[min(atomicAdd(nruns, 1u), wide_runs_max<L>() - 1)] = a;   // (bound: WScanLdsT)
     }
     wave_sync();
     W2P(6)
-    const uint32_t nr = s.nruns;
+    const uint32_t nr = *nruns;
 #pragma unroll 1
     for (uint32_t r = 0; r < nr; ++r) {
-        const uint32_t a = s.runs[r];
+        const uint32_t a = runs[r];
         const uint32_t len = hist[a], st = rst[a] - len;
         wide_dense_walk(s, s.sw + st, len, true, wrec);
     }
@@ -2063,7 +2083,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
     // same-address atomics apply in lane order (as in scan_main: gfx950,
     // checked by the probe once per wavefront), else the key-match ranks.
 #if defined(__gfx950__)
-    const bool ordered = lane_order_probe(s.tab, t);
+    const bool ordered = lane_order_probe(wtab(s), t);
 #else
     const bool ordered = false;
 #endif
@@ -2075,7 +2095,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         const uint32_t q = wq_of(e, wr, d);           // the list position
         const uint32_t len = cur.n;                   // (1 <= len <= slot_len: rc_enc2_scan)
         uint2* wrec0 = reinterpret_cast<uint2*>(e.wide + static_cast<size_t>(q) * e.wslot_bytes);
-        const bool track = len > kE2MaxLen;           // (wave-uniform) the model can reset
+        const bool track = L > kE2MaxLen && len > kE2MaxLen;   // (wave-uniform) the model can reset
         uint32_t s0 = 0, mis = cur.mis;
         uintptr_t src0 = 0;
         if (len + mis > 2048 || track) {
@@ -2088,10 +2108,16 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         const uint32_t n = min(len - s0, L);         // the window: positions s0 .. s0 + n - 1
         uint2* wrec = wrec0 + 2 * s0;
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
-        for (uint32_t k = t; k < L / 32; k += kScanThreads) { s.f2bits[k] = 0u; s.rootbits[k] = 0u; }
+        for (uint32_t k = t; k < L / 32; k += kScanThreads) {
+            s.f2bits[k] = 0u;
+            if (L > kE2MaxLen) s.rootbits[k] = 0u;
+        }
         if (s0 == 0) {
             *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = cur.r0;
-            *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = cur.r1;
+            // (x holds L + 16 bytes past its first 16: chunks up to L / 16, the last a
+            // packet of <= L bytes at any alignment needs; later ones repeat it)
+            if (L >= 2048 || 16 * (t + kScanThreads) <= L)
+                *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = cur.r1;
         }
         if (s0 > 0 || n + mis > 2048) {
             // the window's bytes past the prefetched 2 KB (or a later window's): aligned 16-B chunks
@@ -2113,21 +2139,15 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         }
         wave_sync();
         W2P(1)
+        // bucket starts, buckets back to back (total = n - 1 elements)
         const uint4 c4 = *reinterpret_cast<const uint4*>(&s.cnt[4 * t]);
-        const uint32_t a0 = (c4.x + 3) & ~3u, a1 = (c4.y + 3) & ~3u, a2 = (c4.z + 3) & ~3u, a3 = (c4.w + 3) & ~3u;
-        const uint32_t mine = a0 + a1 + a2 + a3;
+        const uint32_t mine = c4.x + c4.y + c4.z + c4.w;
         const uint32_t incl = wave_incl_scan(mine);
         const uint32_t st = incl - mine;
         const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-        const uint4 s4 = make_uint4(st, st + a0, st + a0 + a1, st + a0 + a1 + a2);
+        const uint4 s4 = make_uint4(st, st + c4.x, st + c4.x + c4.y, st + c4.x + c4.y + c4.z);
         *reinterpret_cast<uint4*>(&s.start[4 * t]) = s4;
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = s4;
-        // the buckets' padding (to 4) marked, for the element-parallel passes
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-            const uint32_t e0 = pick4(r, s4) + pick4(r, c4), e1 = pick4(r, s4) + ((pick4(r, c4) + 3) & ~3u);
-            for (uint32_t j = e0; j < e1; ++j) s.e[j] = kPadWord;
-        }
         wave_sync();
         W2P(2)
         // scatter into buckets, position order (two positions per lane and iteration)
@@ -2165,7 +2185,8 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         wide_small_buckets(s, q0, total, wrec, track);
         wave_sync();
         W2P(4)
-        // big ones: the wavefront, one at a time
+        // big ones: the wavefront, one at a time (their extents from registers:
+        // a big bucket's walk reuses cnt and start)
         uint32_t bigm = 0;
 #pragma unroll
         for (uint32_t r = 0; r < 4; ++r) bigm |= pick4(r, c4) > kE2Bucket ? 1u << r : 0u;
@@ -2176,8 +2197,9 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
 #pragma unroll 1
             for (uint32_t r = 0; r < 4; ++r) {
                 if (!((bm >> r) & 1u)) continue;
-                const uint32_t bk = 4 * ld + r;
-                wide_big_bucket(s, s.start[bk], s.cnt[bk] - s.start[bk], wrec, wp, ordered, track);
+                const uint32_t bs = __builtin_amdgcn_readlane(pick4(r, s4), ld);
+                const uint32_t bn = __builtin_amdgcn_readlane(pick4(r, c4), ld);
+                wide_big_bucket(s, bs, bn, wrec, wp, ordered, track);
             }
             bl &= bl - 1;
         }
