@@ -202,7 +202,10 @@ constexpr uint32_t kWideSmallL = 1216;     // the smaller LDS layouts: packets u
 template <uint32_t L>
 struct ScanLdsT {
     static constexpr uint32_t kDummyE = L + 768 - 1;   // element slot of lanes past the packet
-    uint8_t  x[16 + 2048];            // packet bytes at x[16 + mis + i] (128 chunks of 16 B)
+    // packet bytes at x[16 + mis + i] (128 chunks of 16 B; the 1216 layout: the 77
+    // chunks a packet of <= L bytes at any alignment needs -- 14.2 -> 13.4 KB, 12
+    // scan wavefronts per CU instead of 11, as many as its 149 VGPRs allow)
+    uint8_t  x[L + 32 < 16 + 2048 ? 16 + L + 16 : 16 + 2048];
     uint32_t cnt[256];                // bucket sizes, then fill pointers
     uint32_t start[256];              // bucket starts (4-aligned)
     union {
@@ -715,7 +718,8 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
         const uint32_t n = min(len - s0, 2048u - mis);
         // the window into LDS: aligned 16-B chunks, x = s.x + 16 + misalignment
         *reinterpret_cast<uint4*>(s.x + 16 + 16 * t) = c0;
-        *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = c1;
+        if (16 + 16 * (t + kScanThreads) + 16 <= sizeof(s.x))   // (chunks past the layout's repeat the last)
+            *reinterpret_cast<uint4*>(s.x + 16 + 16 * (t + kScanThreads)) = c1;
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
         *reinterpret_cast<uint4*>(&s.cnt[4 * t]) = z;
         if (t < 16) *reinterpret_cast<uint4*>(&s.excm[4 * t]) = z;
