@@ -1574,9 +1574,11 @@ constexpr uint32_t kWRst = 1u << 18, kWLeft = 1u << 19;
 // L: the longest packet of the launch (its positions); three sizes are built,
 // 4096, 2048 and 1216.  The scan is latency-bound (LDS round trips and
 // ballots on each wavefront's own path), so its speed is the number of
-// resident wavefronts, which LDS sets: the 1216 layout is 13.2 KB, 12 per CU
-// (17.7 KB and 9 per CU before the bucket padding was dropped and the walk
-// tables moved into x).
+// resident wavefronts, which LDS sets: the 1216 layout is 8.7 KB, 18 per CU
+// (17.7 KB and 9 per CU with 32-bit element words and buckets padded to 4).
+// The element lists hold positions (u16); a word is rebuilt from the
+// window's bytes where it is read (wword: one LDS read of x, which the
+// window keeps for the whole packet).
 //
 // A big bucket's long runs: a run is the elements j of bucket p with one a =
 // x[j-2]; an element j with a != p has x[j-2] != p, so j - 1 is no element of
@@ -1587,25 +1589,30 @@ constexpr uint32_t wide_runs_max() { return L / 64 + 2; }
 
 template <uint32_t L>
 struct WScanLdsT {
-    // the window's bytes at x[16 + mis + i]; while the big buckets are walked
-    // (x is not read then) the walk's table, the long runs and their count
-    // (wtab / wruns / wnruns)
-    uint8_t  x[16 + L + 16];
+    uint8_t  x[16 + L + 16];          // the window's bytes at x[16 + mis + i]
     uint32_t cnt[256];                // bucket sizes, then fill pointers; a big bucket's run sizes by a
     uint32_t start[256];              // bucket starts; a big bucket's run starts, then run ends
-    uint32_t e[L];                    // elements in bucket order (wide element words), buckets back to back
-    uint32_t sw[L];                   // a big bucket's element words by a, then its order-1 visits
+    uint32_t tab[64];                 // dense walk: a round's updated counts (256 bytes); the lane-order probe
+    uint16_t sw[L];                   // a big bucket's positions by a, then its order-1 visits (the small
+                                      // buckets' 2-KB order-2 lane-mask table before)
+    uint16_t e[L];                    // positions in bucket order, buckets back to back
     uint32_t f2bits[L / 32];          // positions found at order 2 (big buckets; every bucket in a
                                       // packet that can reach the model reset)
     uint32_t rootbits[L > kE2MaxLen ? L / 32 : 1];   // ... positions coded at the root (a packet that can reset)
+    uint32_t runs[wide_runs_max<L>()];   // a big bucket's long runs (a keys)
+    uint32_t nruns;
 };
-static_assert(sizeof(WScanLdsT<kWideSmallL>) <= 13312, "12 wide-scan wavefronts per CU");
+static_assert(sizeof(WScanLdsT<kWideSmallL>) <= 163840 / 18, "18 wide-scan wavefronts per CU");
+static_assert(2 * kWideSmallL >= 256 * 8, "the order-2 lane-mask table inside sw");
 
-// dense walk: a round's updated counts (256 bytes); the lane-order probe
-template <uint32_t L> DEV uint32_t* wtab(WScanLdsT<L>& s) { return reinterpret_cast<uint32_t*>(s.x); }
-template <uint32_t L> DEV uint32_t* wruns(WScanLdsT<L>& s) { return reinterpret_cast<uint32_t*>(s.x) + 64; }
-template <uint32_t L> DEV uint32_t* wnruns(WScanLdsT<L>& s) { return reinterpret_cast<uint32_t*>(s.x) + 64 + wide_runs_max<L>(); }
-static_assert(4 * (64 + wide_runs_max<kWideSmallL>() + 1) <= 16 + kWideSmallL + 16, "walk tables inside x");
+// the element word of position pos (>= 1) from the window's bytes: pos |
+// v = x[pos] | a = x[pos - 2] with its flag (position 1 has no a); p, the
+// bucket key x[pos - 1], in bits 8-15 of b3
+DEV uint32_t wword_b3(uint32_t pos, uint32_t b3)
+{
+    return pos | ((b3 >> 16) & 255) << kWV | (pos >= 2 ? ((b3 & 255) | 256u) << kWA : 0u);
+}
+DEV uint32_t wword(const uint8_t* x, uint32_t q0, uint32_t pos) { return wword_b3(pos, bytes3(x, q0 + pos)); }
 
 
 // cnt[key] += 1 for every lane with ok: one LDS atomic per distinct key (its
@@ -1671,11 +1678,13 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec, bool
 #pragma unroll 1
     for (uint32_t W = 0; W < total;) {
         const uint32_t ei = W + t;
-        const uint32_t w = ei < total ? s.e[ei] : kPadWord;
-        const bool pad = w == kPadWord;
-        uint32_t bs = 0, be = 0, p = 0;
+        const bool pad = ei >= total;
+        uint32_t w = kPadWord, bs = 0, be = 0, p = 0;
         if (!pad) {
-            p = s.x[q0 + (w & kWPos) - 1];
+            const uint32_t pos = s.e[ei];
+            const uint32_t b3 = bytes3(s.x, q0 + pos);
+            w = wword_b3(pos, b3);
+            p = (b3 >> 8) & 255;
             bs = s.start[p];
             be = s.cnt[p];
         }
@@ -1750,7 +1759,7 @@ DEV void wide_small_buckets(S& s, uint32_t q0, uint32_t total, uint2* wrec, bool
 // counted over lanes as in wide_small_buckets: record half A, and the
 // position's order-2 hit bit.
 template <class S>
-DEV void wide_short_runs(S& s, uint32_t ks, const uint32_t* hist, const uint32_t* rend, uint2* wrec)
+DEV void wide_short_runs(S& s, uint32_t q0, uint32_t ks, const uint32_t* hist, const uint32_t* rend, uint2* wrec)
 {
     const uint32_t t = lane_id();
     const uint64_t below = below_mask();
@@ -1758,7 +1767,7 @@ DEV void wide_short_runs(S& s, uint32_t ks, const uint32_t* hist, const uint32_t
     for (uint32_t W = 0; W < ks;) {
         const uint32_t j = W + t;
         const bool in = j < ks;
-        const uint32_t w = s.sw[in ? j : ks - 1];
+        const uint32_t w = wword(s.x, q0, s.sw[in ? j : ks - 1]);
         const uint32_t a = wa_of(w), v = wv_of(w);
         const uint32_t re = rend[a], rs = re - hist[a];
         const bool act = in && re <= W + 64;
@@ -1801,10 +1810,11 @@ DEV uint32_t nonzero_bytes(uint32_t x)
 // position's order-2 hit bit and closes half B; else half B with the root
 // flag.
 template <class S>
-DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, uint2* wrec, bool track = false)
+DEV void wide_dense_walk(S& s, uint32_t q0, const uint16_t* list, uint32_t m, bool order2, uint2* wrec,
+                         bool track = false)
 {
     const uint32_t t = lane_id();
-    uint32_t* tab = wtab(s);
+    uint32_t* tab = s.tab;
     uint8_t* sc = reinterpret_cast<uint8_t*>(tab);     // a round's final counts of its symbols (0: untouched)
     uint32_t tabr = 0, pre = 0;
     uint32_t esc = 0, tot = 0;                        // (wave-uniform)
@@ -1814,8 +1824,8 @@ DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, ui
     for (uint32_t base = 0; base < m;) {
         const uint32_t j = base + t;
         const bool act = j < m;
-        const uint32_t w = list[act ? j : m - 1];
-        const uint32_t pos = w & kWPos, v = wv_of(w);
+        const uint32_t pos = list[act ? j : m - 1];
+        const uint32_t v = s.x[q0 + pos];
         const uint32_t dw = __shfl(tabr, static_cast<int>(v >> 2), 64);
         const uint32_t pd = __shfl(pre, static_cast<int>(v >> 2), 64);
         const uint32_t sh = 8 * (v & 3);
@@ -1888,13 +1898,14 @@ DEV void wide_dense_walk(S& s, const uint32_t* list, uint32_t m, bool order2, ui
 // a big bucket of a wide packet (> kE2Bucket elements, [bs, bs + k) in
 // position order), the whole wavefront
 template <uint32_t L>
-DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp, bool ordered, bool track)
+DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t q0, uint32_t bs, uint32_t k, uint2* wrec, W2Prof& wp,
+                         bool ordered, bool track)
 {
     const uint32_t t = lane_id();
     uint32_t* hist = s.cnt;                                      // [256] run sizes by a
     uint32_t* rst = s.start;                                     // [256] run starts, then run ends
-    uint32_t* runs = wruns(s);
-    uint32_t* nruns = wnruns(s);
+    uint32_t* runs = s.runs;
+    uint32_t* nruns = &s.nruns;
     *reinterpret_cast<uint4*>(&hist[4 * t]) = make_uint4(0u, 0u, 0u, 0u);
     if (t == 0) *nruns = 0;
     wave_sync();
@@ -1902,7 +1913,7 @@ DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t bs, uint32_t k, uint2* wrec, 
 #pragma unroll 1
     for (uint32_t q = 0; q < k; q += 64) {
         const bool ok0 = q + t < k;
-        const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
+        const uint32_t w = wword(s.x, q0, s.e[bs + (ok0 ? q + t : k - 1)]);
         const bool has = (w & kWHas) != 0;
         if (ok0 && has) atomicAdd(&hist[wa_of(w)], 1u);
         if (ok0 && !has) wrec[2 * (w & kWPos)] = make_uint2(kNoCodeLo, kNoCodeTot | (wv_of(w)) << 16);
@@ -1930,7 +1941,7 @@ DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t bs, uint32_t k, uint2* wrec, 
 #pragma unroll 1
     for (uint32_t q = 0; q < k; q += 64) {
         const bool ok0 = q + t < k;
-        const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
+        const uint32_t w = wword(s.x, q0, s.e[bs + (ok0 ? q + t : k - 1)]);
         const bool has = ok0 && (w & kWHas) != 0;
         uint32_t rk = 0;
         if (ordered) {
@@ -1938,12 +1949,12 @@ DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t bs, uint32_t k, uint2* wrec, 
         } else {
             rk = group_add<true>(rst, wa_of(w), has);
         }
-        if (has) s.sw[rk] = w;
+        if (has) s.sw[rk] = static_cast<uint16_t>(w & kWPos);
     }
     wave_sync();
     W2P(5)
     // short runs: the closed form, element-parallel; long runs: dense walks
-    wide_short_runs(s, ks, hist, rst, wrec);
+    wide_short_runs(s, q0, ks, hist, rst, wrec);
 #pragma unroll 1
     for (uint32_t r = 0; r < 4; ++r) {
         const uint32_t a = 4 * t + r;
@@ -1956,7 +1967,7 @@ DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t bs, uint32_t k, uint2* wrec, 
     for (uint32_t r = 0; r < nr; ++r) {
         const uint32_t a = runs[r];
         const uint32_t len = hist[a], st = rst[a] - len;
-        wide_dense_walk(s, s.sw + st, len, true, wrec);
+        wide_dense_walk(s, q0, s.sw + st, len, true, wrec);
     }
     wave_sync();
     W2P(7)
@@ -1965,16 +1976,15 @@ DEV void wide_big_bucket(WScanLdsT<L>& s, uint32_t bs, uint32_t k, uint2* wrec, 
 #pragma unroll 1
     for (uint32_t q = 0; q < k; q += 64) {
         const bool ok0 = q + t < k;
-        const uint32_t w = s.e[bs + (ok0 ? q + t : k - 1)];
-        const uint32_t pos = w & kWPos;
+        const uint32_t pos = s.e[bs + (ok0 ? q + t : k - 1)];
         const bool vis = ok0 && !bit_at(s.f2bits, pos);
         const uint64_t vm = __builtin_amdgcn_ballot_w64(vis);
-        if (vis) s.sw[m1 + popc64(vm & below_mask())] = w;
+        if (vis) s.sw[m1 + popc64(vm & below_mask())] = static_cast<uint16_t>(pos);
         m1 += popc64(vm);
     }
     wave_sync();
     W2P(8)
-    wide_dense_walk(s, s.sw, m1, false, wrec, track);
+    wide_dense_walk(s, q0, s.sw, m1, false, wrec, track);
     wave_sync();
     W2P(9)
 }
@@ -2018,7 +2028,7 @@ DEV WPf wide_prefetch(const rc_batch_dev& b, const E2Params& e, const WRegs& w, 
 // window position after whose byte the count reaches 4094 (compress.c:148-157),
 // or n.  After the walks; s.sw and s.cnt are reused.
 template <uint32_t L, class S>
-DEV uint32_t wreset_after(S& s, uint32_t n, uint32_t total, uint32_t x0, uint32_t t)
+DEV uint32_t wreset_after(S& s, uint32_t q0, uint32_t n, uint32_t total, uint32_t x0, uint32_t t)
 {
     uint8_t* inc = reinterpret_cast<uint8_t*>(s.sw);     // per position: nodes | 0x80 = root visit
     uint32_t* first = s.cnt;                             // the first root visit per byte value
@@ -2027,21 +2037,18 @@ DEV uint32_t wreset_after(S& s, uint32_t n, uint32_t total, uint32_t x0, uint32_
     if (t == 0) { first[x0] = 0u; inc[0] = 1; }
 #pragma unroll 1
     for (uint32_t k = t; k < total; k += kScanThreads) {
-        const uint32_t w = s.e[k];
-        if (w == kPadWord) continue;
-        const uint32_t pos = w & kWPos;
+        const uint32_t pos = s.e[k];
+        const uint32_t v = s.x[q0 + pos];
         const bool rv = bit_at(s.rootbits, pos), f2 = bit_at(s.f2bits, pos);
         const uint32_t c = rv ? (pos >= 1 ? 1u : 0u) + (pos >= 2 ? 1u : 0u) : (f2 ? 0u : (pos >= 2 ? 1u : 0u));
         inc[pos] = static_cast<uint8_t>(c | (rv ? 0x80u : 0u));
-        if (rv) atomicMin(&first[wv_of(w)], pos);
+        if (rv) atomicMin(&first[v], pos);
     }
     wave_sync();
 #pragma unroll 1
     for (uint32_t k = t; k < total; k += kScanThreads) {
-        const uint32_t w = s.e[k];
-        if (w == kPadWord) continue;
-        const uint32_t pos = w & kWPos;
-        if (bit_at(s.rootbits, pos) && first[wv_of(w)] == pos) inc[pos] = static_cast<uint8_t>(inc[pos] + 1);
+        const uint32_t pos = s.e[k];
+        if (bit_at(s.rootbits, pos) && first[s.x[q0 + pos]] == pos) inc[pos] = static_cast<uint8_t>(inc[pos] + 1);
     }
     wave_sync();
     // positions C t .. C t + C - 1: their sum, the prefix over the lanes, the first crossing
@@ -2087,7 +2094,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
     // same-address atomics apply in lane order (as in scan_main: gfx950,
     // checked by the probe once per wavefront), else the key-match ranks.
 #if defined(__gfx950__)
-    const bool ordered = lane_order_probe(wtab(s), t);
+    const bool ordered = lane_order_probe(s.tab, t);
 #else
     const bool ordered = false;
 #endif
@@ -2163,11 +2170,8 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
             for (uint32_t h = 0; h < 2; ++h) {
                 const uint32_t i2 = i + h * kScanThreads;
                 ok[h] = i2 < n;
-                const uint32_t ii = ok[h] ? i2 : 1u;
-                const uint32_t b3 = bytes3(s.x, q0 + max(ii, 2u));   // (position 1: its a byte unused)
-                p[h] = s.x[q0 + ii - 1];
-                const uint32_t v = s.x[q0 + ii];
-                w[h] = ii | v << kWV | (ii >= 2 ? ((b3 & 255) | 256u) << kWA : 0u);
+                w[h] = ok[h] ? i2 : 1u;                    // (the position)
+                p[h] = s.x[q0 + w[h] - 1];
             }
 #pragma unroll
             for (uint32_t h = 0; h < 2; ++h) {
@@ -2177,7 +2181,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
                 } else {
                     slot = group_add<true>(s.cnt, p[h], ok[h]);
                 }
-                if (ok[h]) s.e[slot] = w[h];
+                if (ok[h]) s.e[slot] = static_cast<uint16_t>(w[h]);
             }
         }
         const uint32_t x0 = s.x[q0];
@@ -2203,7 +2207,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
                 if (!((bm >> r) & 1u)) continue;
                 const uint32_t bs = __builtin_amdgcn_readlane(pick4(r, s4), ld);
                 const uint32_t bn = __builtin_amdgcn_readlane(pick4(r, c4), ld);
-                wide_big_bucket(s, bs, bn, wrec, wp, ordered, track);
+                wide_big_bucket(s, q0, bs, bn, wrec, wp, ordered, track);
             }
             bl &= bl - 1;
         }
@@ -2214,7 +2218,7 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
         wave_sync();
         W2P(10)
         if (!track) break;                            // (no reset: <= 2 * 1918 + 256 nodes, compress.c:150)
-        const uint32_t r = wreset_after<L>(s, n, total, x0, t);
+        const uint32_t r = wreset_after<L>(s, q0, n, total, x0, t);
         if (r >= n) {                                 // no reset in the window
             if (s0 + n < len) {
                 // a model segment longer than the window: the lane kernels take the packet
