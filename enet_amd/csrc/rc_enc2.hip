@@ -2247,7 +2247,13 @@ void rc_enc2_wscan(rc_batch_dev b, E2Params e)
 }
 
 // the same for launches whose packets are at most kWideSmallL bytes
-extern "C" __global__ __launch_bounds__(kScanThreads)
+// (five wavefronts per SIMD: 96 VGPRs, a few spilled; with 8.7 KB of LDS 18
+// fit per CU instead of the 16 that 105 VGPRs allowed -- 1.166 -> 1.147 ms on
+// C3, profiles/r6/s7f_wscan_w5_c3.txt)
+#ifndef WSCAN_S_ATTR
+#define WSCAN_S_ATTR __attribute__((amdgpu_waves_per_eu(5)))
+#endif
+extern "C" __global__ __launch_bounds__(kScanThreads) WSCAN_S_ATTR
 void rc_enc2_wscan_s(rc_batch_dev b, E2Params e)
 {
     __shared__ __attribute__((aligned(16))) WScanLdsT<kWideSmallL> s;
