@@ -1277,8 +1277,13 @@ void rc_enc2_code(rc_batch_dev b, E2Params e)
 constexpr uint32_t kQPart = 4;                                   // positions per part
 constexpr uint32_t kQEntry = 16;                                 // bytes per queued position
 constexpr uint32_t kQSlots = 4;                                  // parts in the queue: two filled while two drain
-constexpr uint32_t kC2Root = 304;                                // helper root stride (76 dwords: b128 conflict-free)
-constexpr uint32_t kC2Mtab = 256 * kC2Root;                      // helper roots, then tables
+// The helpers' roots, transposed (rc_root3.h rofs): row g of lane l's root at
+// kC2Row g + 16 l -- a lane's group read, count read and update and its D copy
+// hit banks of its own.  (Before: 256 roots at a 304-B stride, where random
+// groups put a wavefront's b128 reads on random banks: SQ_LDS_BANK_CONFLICT
+// 140 M cycles per C2 launch.)
+constexpr uint32_t kC2Row = 256 * 16;
+constexpr uint32_t kC2Mtab = 18 * kC2Row;                        // helper roots, then tables
 constexpr uint32_t kC2Itab = kC2Mtab + 256;
 constexpr uint32_t kC2Ring = kC2Itab + 544;                      // (row 16 of the increment table: zeros); coder rings, 32 B per packet
 constexpr uint32_t kC2Queue = kC2Ring + 256 * 32;                // [kQSlots parts][kQPart][256 packets] entries
@@ -1309,19 +1314,19 @@ DEV void help_pos(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, uint3
 {
     if (en && (w0 & kRst)) {                          // compress.c:148-157, after the previous byte
         Root R;
-        root3_clear<true>(root, R);
+        root3_clear<true, kC2Row>(root, R);
         rtot = 1 + 256;
     }
     const uint32_t v = w1 >> 24;
     uint32_t under0, cnt0;
-    root3_lookup(root, mtab, v, under0, cnt0);
-    const RootAddPre ra = root3_add_read(root, itab, v);
+    root3_lookup<kC2Row>(root, mtab, v, under0, cnt0);
+    const RootAddPre ra = root3_add_read<kC2Row>(root, itab, v);
     const bool e0 = en && root_codes(w0);
-    if (e0) root3_add_write(root, v, cnt0, ra);
+    if (e0) root3_add_write<kC2Row>(root, v, cnt0, ra);
     uint32_t rt = e0 ? ((rtot + kRootDelta) & 0xFFFF) : rtot;
     const bool rs = e0 && (1 + cnt0 > 0xFF - 2 * kRootDelta + 1 || rt > kTotalLimit);
     if (any_lane(rs)) {
-        if (rs) { Root R; rt = root3_rescale<true>(root, R); }
+        if (rs) { Root R; rt = root3_rescale<true, kC2Row>(root, R); }
     }
     *reinterpret_cast<uint4*>(qe) = make_uint4(w0, w1, under0 | cnt0 << 16, rtot);
     rtot = rt;
@@ -1345,13 +1350,13 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
     for (uint32_t j = 0; j < 4; ++j) {
         v[j] = w1[j] >> 24;
         e0[j] = i + j < len && root_codes(w0[j]);
-        lk[j] = root3_lookup_read(root, mtab, v[j]);
+        lk[j] = root3_lookup_read<kC2Row>(root, mtab, v[j]);
         const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (e0[j] ? v[j] >> 4 : 16u));   // (row 16: no update)
         inc[j][0] = ip[0];
         inc[j][1] = ip[1];
     }
-    const uint4* dp = reinterpret_cast<const uint4*>(root + kRootD);
-    uint4 d0 = dp[0], d1 = dp[1];
+    uint4 d0 = *reinterpret_cast<const uint4*>(root + rdofs<kC2Row>(0));
+    uint4 d1 = *reinterpret_cast<const uint4*>(root + rdofs<kC2Row>(1));
     bool rs = false;
     uint32_t t = rtot;
 #pragma unroll
@@ -1377,13 +1382,12 @@ DEV void help_part(uint8_t* root, const uint8_t* mtab, const uint8_t* itab, cons
     // last write holds its final count) and the D copy
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
-        if (e0[j]) root[v[j]] = static_cast<uint8_t>(cnt[j] + kRootDelta);
+        if (e0[j]) root[rofs<kC2Row>(v[j])] = static_cast<uint8_t>(cnt[j] + kRootDelta);
         d0.x += inc[j][0].x; d0.y += inc[j][0].y; d0.z += inc[j][0].z; d0.w += inc[j][0].w;
         d1.x += inc[j][1].x; d1.y += inc[j][1].y; d1.z += inc[j][1].z; d1.w += inc[j][1].w;
     }
-    uint4* dw = reinterpret_cast<uint4*>(root + kRootD);
-    dw[0] = d0;
-    dw[1] = d1;
+    *reinterpret_cast<uint4*>(root + rdofs<kC2Row>(0)) = d0;
+    *reinterpret_cast<uint4*>(root + rdofs<kC2Row>(1)) = d1;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j)
         *reinterpret_cast<uint4*>(q_entry(smem, part, j, lane)) = make_uint4(w0[j], w1[j], under[j] | cnt[j] << 16, rt[j]);
@@ -1435,10 +1439,10 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     // the other two, one block barrier per pair (one per part before round 5:
     // the coders then waited ~0.5 k cycles a part at the barrier)
     if (helper) {
-        uint8_t* root = smem + lane * kC2Root;
+        uint8_t* root = smem + lane * 16;
         {
             Root R;
-            root3_clear<true>(root, R);
+            root3_clear<true, kC2Row>(root, R);
         }
         uint32_t rtot = 1 + 256;
         // records: a part is two 16-B chunks; two register sets (even and odd
@@ -2447,10 +2451,10 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
     __syncthreads();
     const uint32_t parts = (*bmax + kQPart - 1) / kQPart;
     if (helper) {
-        uint8_t* root = smem + lane * kC2Root;
+        uint8_t* root = smem + lane * 16;
         {
             Root R;
-            root3_clear<true>(root, R);
+            root3_clear<true, kC2Row>(root, R);
         }
         uint32_t rtot = 1 + 256;
         uint4 x[4], y[4];                             // even and odd parts' records

@@ -23,6 +23,16 @@ constexpr uint32_t kRootD = 256;
 
 struct Root { uint32_t d[8]; };
 
+// Layout of one lane's root: ROW is the distance between its 16-B rows (the
+// 16 count groups, then the two rows of the D copy).  ROW = 16: the rows back
+// to back (the lane kernels, the decoders, the one-wavefront code pass).
+// The two-wavefront code pass's helpers keep their roots transposed, row g
+// of every lane side by side (ROW = 16 x the block's lanes): a lane's random
+// group read then hits banks of its own, where 256 roots at one stride put
+// the lanes of a wavefront on random banks (rc_enc2.hip kC2Row).
+template <uint32_t ROW> DEV uint32_t rofs(uint32_t v) { return ROW * (v >> 4) + (v & 15); }   // count of v
+template <uint32_t ROW> DEV uint32_t rdofs(uint32_t h) { return ROW * (16 + h); }             // D row h
+
 // the block-wide table of prefix masks: entry j has bytes 0..j-1 set
 DEV void root3_mask_init(uint8_t* tab, uint32_t j)
 {
@@ -35,25 +45,24 @@ DEV void root3_mask_init(uint8_t* tab, uint32_t j)
     reinterpret_cast<uint4*>(tab)[j] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <bool COPY>
+template <bool COPY, uint32_t ROW = 16>
 DEV void root3_store_d(uint8_t* r, const Root& R)
 {
     if (COPY) {
-        uint4* p = reinterpret_cast<uint4*>(r + kRootD);
-        p[0] = make_uint4(R.d[0], R.d[1], R.d[2], R.d[3]);
-        p[1] = make_uint4(R.d[4], R.d[5], R.d[6], R.d[7]);
+        *reinterpret_cast<uint4*>(r + rdofs<ROW>(0)) = make_uint4(R.d[0], R.d[1], R.d[2], R.d[3]);
+        *reinterpret_cast<uint4*>(r + rdofs<ROW>(1)) = make_uint4(R.d[4], R.d[5], R.d[6], R.d[7]);
     }
 }
 
-template <bool COPY>
+template <bool COPY, uint32_t ROW = 16>
 DEV void root3_clear(uint8_t* r, Root& R)
 {
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) reinterpret_cast<uint4*>(r)[i] = z;
+    for (uint32_t i = 0; i < 16; ++i) *reinterpret_cast<uint4*>(r + ROW * i) = z;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) R.d[i] = (32 * i + 16) | ((32 * i + 32) << 16);
-    root3_store_d<COPY>(r, R);
+    root3_store_d<COPY, ROW>(r, R);
 }
 
 // Encoder: the block-wide table of D increments, entry g = +3 in every D[t]
@@ -86,30 +95,41 @@ DEV void root3_add_tab(uint8_t* r, const uint8_t* itab, uint32_t v, uint32_t cnt
 // root3_add_tab in two halves: the reads, issued early in a step, and the
 // writes, after the step's codes (no wait for the reads on the coder's chain)
 struct RootAddPre { uint4 d0, d1, i0, i1; };
+template <uint32_t ROW = 16>
 DEV RootAddPre root3_add_read(const uint8_t* r, const uint8_t* itab, uint32_t v)
 {
     const uint4* ip = reinterpret_cast<const uint4*>(itab + 32 * (v >> 4));
-    const uint4* dp = reinterpret_cast<const uint4*>(r + kRootD);
-    return RootAddPre{dp[0], dp[1], ip[0], ip[1]};
+    return RootAddPre{*reinterpret_cast<const uint4*>(r + rdofs<ROW>(0)), *reinterpret_cast<const uint4*>(r + rdofs<ROW>(1)),
+                      ip[0], ip[1]};
 }
+template <uint32_t ROW = 16>
 DEV void root3_add_write(uint8_t* r, uint32_t v, uint32_t cnt, RootAddPre a)
 {
-    r[v] = static_cast<uint8_t>(cnt + kRootDelta);
-    uint4* dp = reinterpret_cast<uint4*>(r + kRootD);
+    r[rofs<ROW>(v)] = static_cast<uint8_t>(cnt + kRootDelta);
     a.d0.x += a.i0.x; a.d0.y += a.i0.y; a.d0.z += a.i0.z; a.d0.w += a.i0.w;
     a.d1.x += a.i1.x; a.d1.y += a.i1.y; a.d1.z += a.i1.z; a.d1.w += a.i1.w;
-    dp[0] = a.d0;
-    dp[1] = a.d1;
+    *reinterpret_cast<uint4*>(r + rdofs<ROW>(0)) = a.d0;
+    *reinterpret_cast<uint4*>(r + rdofs<ROW>(1)) = a.d1;
+}
+
+// D[g - 1] from the lane's D copy (g >= 1; g = 0 reads D[15], unused)
+template <uint32_t ROW>
+DEV uint32_t root3_dprev(const uint8_t* r, uint32_t g)
+{
+    if (ROW == 16) return reinterpret_cast<const uint16_t*>(r + kRootD)[static_cast<int>(g) - 1];
+    const uint32_t t = (g - 1) & 15;
+    return *reinterpret_cast<const uint16_t*>(r + rdofs<ROW>(t >> 3) + 2 * (t & 7));
 }
 
 // under = cumulative frequency below v, cnt = count[v] (compress.c:159-199, minimum 1)
+template <uint32_t ROW = 16>
 DEV void root3_lookup(const uint8_t* r, const uint8_t* mtab, uint32_t v, uint32_t& under, uint32_t& cnt)
 {
     const uint32_t g = v >> 4, j = v & 15;
-    const uint4 q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    const uint4 q = *reinterpret_cast<const uint4*>(r + ROW * g);
     const uint4 m = *reinterpret_cast<const uint4*>(mtab + 16 * j);
-    const uint32_t dprev = reinterpret_cast<const uint16_t*>(r + kRootD)[static_cast<int>(g) - 1];   // (g = 0: unused)
-    cnt = r[v];
+    const uint32_t dprev = root3_dprev<ROW>(r, g);
+    cnt = r[rofs<ROW>(v)];
     const uint32_t within = sad(q.w & m.w, sad(q.z & m.z, sad(q.y & m.y, sad(q.x & m.x, 0u))));
     under = (g ? dprev : 0u) + j + within;
 }
@@ -117,14 +137,15 @@ DEV void root3_lookup(const uint8_t* r, const uint8_t* mtab, uint32_t v, uint32_
 // root3_lookup in two halves: the LDS reads (several issued together by the
 // encoder's helper) and the sums
 struct RootLk { uint4 q, m; uint32_t dprev, cnt; };
+template <uint32_t ROW = 16>
 DEV RootLk root3_lookup_read(const uint8_t* r, const uint8_t* mtab, uint32_t v)
 {
     const uint32_t g = v >> 4, j = v & 15;
     RootLk l;
-    l.q = *reinterpret_cast<const uint4*>(r + 16 * g);
+    l.q = *reinterpret_cast<const uint4*>(r + ROW * g);
     l.m = *reinterpret_cast<const uint4*>(mtab + 16 * j);
-    l.dprev = reinterpret_cast<const uint16_t*>(r + kRootD)[static_cast<int>(g) - 1];   // (g = 0: unused)
-    l.cnt = r[v];
+    l.dprev = root3_dprev<ROW>(r, g);
+    l.cnt = r[rofs<ROW>(v)];
     return l;
 }
 DEV void root3_lookup_sum(const RootLk& l, uint32_t v, uint32_t& under, uint32_t& cnt)
@@ -250,23 +271,23 @@ DEV void root3_add_pre(uint8_t* r, Root& R, uint32_t v, uint32_t cnt, const uint
 }
 
 // compress.c:90-112 for the root: halve the counts, rebuild D; returns the new total
-template <bool COPY>
+template <bool COPY, uint32_t ROW = 16>
 DEV uint32_t root3_rescale(uint8_t* r, Root& R)
 {
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t g = 0; g < 16; ++g) {
-        uint4 q = reinterpret_cast<uint4*>(r)[g];
+        uint4 q = *reinterpret_cast<uint4*>(r + ROW * g);
         q.x -= (q.x >> 1) & 0x7F7F7F7Fu;
         q.y -= (q.y >> 1) & 0x7F7F7F7Fu;
         q.z -= (q.z >> 1) & 0x7F7F7F7Fu;
         q.w -= (q.w >> 1) & 0x7F7F7F7Fu;
-        reinterpret_cast<uint4*>(r)[g] = q;
+        *reinterpret_cast<uint4*>(r + ROW * g) = q;
         sum = sad(q.w, sad(q.z, sad(q.y, sad(q.x, sum))));
         const uint32_t dg = sum + 16 * (g + 1);
         if (g & 1) R.d[g >> 1] |= dg << 16; else R.d[g >> 1] = dg;
     }
-    root3_store_d<COPY>(r, R);
+    root3_store_d<COPY, ROW>(r, R);
     return (sum + 1 + 256) & 0xFFFF;
 }
 
