@@ -199,6 +199,7 @@ DEV uint32_t packet_of(const E2Params& e, uint32_t idx)
 // element array fits the bigram set's space (14 KB instead of 17 KB per
 // wavefront)
 constexpr uint32_t kWideSmallL = 1216;     // the smaller LDS layouts: packets up to this many bytes
+[[maybe_unused]] constexpr uint32_t kScanMidL = 1408;       // the narrow scan's middle layout (ENet's default MTU: <= 1392 B)
 template <uint32_t L>
 struct ScanLdsT {
     static constexpr uint32_t kDummyE = L + 768 - 1;   // element slot of lanes past the packet
@@ -919,6 +920,15 @@ extern "C" __global__ __launch_bounds__(kScanThreads)
 void rc_enc2_scan_s(rc_batch_dev b, E2Params e)
 {
     __shared__ __attribute__((aligned(16))) ScanLdsT<kWideSmallL> s;
+    scan_main(b, e, s);
+}
+
+// ... and for launches of MTU-bounded packets (C4: 64-1392 B): 13.6 KB of LDS,
+// 12 wavefronts per CU where the 2048 layout (17.3 KB) fits 9
+extern "C" __global__ __launch_bounds__(kScanThreads)
+void rc_enc2_scan_m(rc_batch_dev b, E2Params e)
+{
+    __shared__ __attribute__((aligned(16))) ScanLdsT<kScanMidL> s;
     scan_main(b, e, s);
 }
 #endif
@@ -2665,6 +2675,9 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         }
         if (e.slot_len <= kWideSmallL)
             hipLaunchKernelGGL(rc_enc2_scan_s, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
+                               0, st, *b, e);
+        else if (e.slot_len <= kScanMidL)
+            hipLaunchKernelGGL(rc_enc2_scan_m, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
                                0, st, *b, e);
         else
             hipLaunchKernelGGL(rc_enc2_scan, dim3(cnt < scan_blocks_max ? cnt : scan_blocks_max), dim3(kScanThreads),
