@@ -2657,6 +2657,12 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
     static const char* bpc_env = getenv("ENET_RC_SCAN_BPC");
     const int bpc = bpc_env ? atoi(bpc_env) : 0;
     const uint32_t scan_blocks_max = ws->cus * (bpc > 0 ? static_cast<uint32_t>(bpc) : 64u);
+    // The wide scan's grid: 128 workgroups per CU since it fits 18 per CU
+    // (C3 rc_enc2_wscan_s 1.142 -> 1.094 ms against 64; 1.238 at 32;
+    // profiles/r6/s7i_scan_grid.txt).  ENET_RC_WSCAN_BPC: per CU instead.
+    static const char* wbpc_env = getenv("ENET_RC_WSCAN_BPC");
+    const int wbpc = wbpc_env ? atoi(wbpc_env) : 0;
+    const uint32_t wscan_blocks_max = ws->cus * (wbpc > 0 ? static_cast<uint32_t>(wbpc) : 128u);
     static const char* lanes = getenv("ENET_RC_ENC2_LANES");      // experiment: 32 packets per wavefront
     e.act = (lanes && atoi(lanes) == 32) ? 32u : 64u;
     e.slow = ws->enc2_slow;
@@ -2689,7 +2695,7 @@ extern "C" int rc_hip_enc2_launch(const rc_batch_dev* b, const rc_workspace_dev*
         else
             hipLaunchKernelGGL(rc_enc2_code2, dim3((cnt + 255) / 256), dim3(512), kC2Lds, st, *b, e);
         if (e.wide) {
-            const int rc = rc_hip_enc2_wide_launch(b, &e, cnt < scan_blocks_max ? cnt : scan_blocks_max, cnt, stream);
+            const int rc = rc_hip_enc2_wide_launch(b, &e, cnt < wscan_blocks_max ? cnt : wscan_blocks_max, cnt, stream);
             if (rc != 0) return rc;
         }
     }
