@@ -2103,6 +2103,8 @@ DEV void wscan_main(const rc_batch_dev& b, const E2Params& e, WScanLdsT<L>& s)
     const uint32_t t = threadIdx.x;
     const WRegs wr = wregs(e);                        // the live list positions: d < nw
     const uint32_t nw = wr.pre[RC_WSHARDS];
+    if (blockIdx.x >= nw) return;                     // (no packet for this workgroup: no probe, no prefetch --
+                                                      // a batch with no wide packet, C2, launches the grid for nothing)
     // The stable scatters (elements into buckets in position order, a big
     // bucket's elements into runs) take one LDS atomic per lane where
     // same-address atomics apply in lane order (as in scan_main: gfx950,
