@@ -33,16 +33,17 @@ def _coder(**env):
                 os.environ[k] = v
 
 
-def _wide_packets(n, seed):
+def _wide_packets(n, seed, max_len=1919):
     """Low-entropy packets of every shape the wide path has to get right:
     single-byte runs (one context, rescales every 127 visits), alternations,
     small alphabets, mostly-zero with random bytes, game state, lengths up to
-    1919 B (the longest without a model reset)."""
+    1919 B (the longest without a model reset) or max_len, every 11th packet
+    exactly max_len long."""
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
         k = i % 7
-        ln = int(rng.integers(66, 1920))
+        ln = max_len if i % 11 == 0 else int(rng.integers(66, max_len + 1))
         if k == 0:
             p = np.full(ln, rng.integers(0, 256), np.uint8)
         elif k == 1:
@@ -98,6 +99,22 @@ def test_wide_packets_vs_oracle():
     _check(c, pk, lambda n: 2 * n + 64)
     assert c.last_lane_count() == 0                   # every packet on the wide path
     _check(c, pk, lambda n: n)                        # protocol mode: outLimit = N (overflows included)
+    c.close()
+
+
+@pytest.mark.parametrize("slow", ["0", "1"])
+def test_wide_small_layout_vs_oracle(slow):
+    """Launches whose packets are at most 1216 B take rc_enc2_wscan_s, whose
+    LDS layout is sized for them (WScanLdsT<1216>: u16 position lists, the
+    window's bytes exactly as long as such a packet at any alignment needs):
+    the adversarial shapes at every length up to 1216 and back-to-back
+    offsets (all 16 alignments), with and without the lane-order shortcut."""
+    c = _coder(ENET_RC_ENC2_SLOW=slow)
+    pk = _wide_packets(3000, 21, max_len=1216)
+    assert max(len(p) for p in pk) == 1216
+    _check(c, pk, lambda n: 2 * n + 64)
+    assert c.last_lane_count() == 0
+    _check(c, pk, lambda n: n)
     c.close()
 
 
