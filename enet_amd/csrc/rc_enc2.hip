@@ -202,16 +202,16 @@ constexpr uint32_t kWideSmallL = 1216;     // the smaller LDS layouts: packets u
 [[maybe_unused]] constexpr uint32_t kScanMidL = 1408;       // the narrow scan's middle layout (ENet's default MTU: <= 1392 B)
 template <uint32_t L>
 struct ScanLdsT {
-    static constexpr uint32_t kDummyE = L + 768 - 1;   // element slot of lanes past the packet
+    static constexpr uint32_t kDummyE = L;             // element slot of lanes past the packet
     // packet bytes at x[16 + mis + i] (128 chunks of 16 B; the 1216 layout: the 77
     // chunks a packet of <= L bytes at any alignment needs -- 14.2 -> 13.4 KB, 12
     // scan wavefronts per CU instead of 11, as many as its 149 VGPRs allow)
     uint8_t  x[L + 32 < 16 + 2048 ? 16 + L + 16 : 16 + 2048];
     uint32_t cnt[256];                // bucket sizes, then fill pointers
-    uint32_t start[256];              // bucket starts (4-aligned)
+    uint32_t start[256];              // bucket starts
     union {
         uint32_t seen[2048];          // bigrams (x[i-1], x[i]) seen, 64 Ki bits
-        uint32_t e[L + 768];          // elements in bucket order (below), buckets 4-aligned
+        uint32_t e[L + 1];            // elements in bucket order (below), buckets back to back; the dummy slot
     };
     uint32_t excm[64];                // exceptional positions: i or i - 1 repeats an earlier bigram (2048 bits)
     uint32_t probe[16];               // lane-order probe (rc_enc2_scan)
@@ -778,7 +778,9 @@ DEV void scan_main(const rc_batch_dev& b, const E2Params& e, S& s)
             if (!fetched) pf = scan_prefetch(b, e, idx + gridDim.x);
             break;
         }
-        const uint32_t a0 = (c4.x + 3) & ~3u, a1 = (c4.y + 3) & ~3u, a2 = (c4.z + 3) & ~3u, a3 = (c4.w + 3) & ~3u;
+        // (buckets back to back: with the old padding to 4 the elements of an
+        // MTU-bounded packet outgrew the bigram set they share LDS with)
+        const uint32_t a0 = c4.x, a1 = c4.y, a2 = c4.z, a3 = c4.w;
         const uint32_t mine = a0 + a1 + a2 + a3;
         const uint32_t st = wave_incl_scan(mine) - mine;
         const uint4 s4 = make_uint4(st, st + a0, st + a0 + a1, st + a0 + a1 + a2);
