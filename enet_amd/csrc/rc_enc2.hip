@@ -1298,7 +1298,10 @@ constexpr uint32_t kC2Row = 256 * 16;
 constexpr uint32_t kC2Mtab = 18 * kC2Row;                        // helper roots, then tables
 constexpr uint32_t kC2Itab = kC2Mtab + 256;
 constexpr uint32_t kC2Ring = kC2Itab + 544;                      // (row 16 of the increment table: zeros); coder rings, 32 B per packet
-constexpr uint32_t kC2Queue = kC2Ring + 256 * 32;                // [kQSlots parts][kQPart][256 packets] entries
+// (rings at a 48-B stride: 16 lanes' 16-B ring chunks then cover the 64 banks
+// once; at 32 B lanes l and l + 8 read the same four banks)
+constexpr uint32_t kC2RingStride = 48;
+constexpr uint32_t kC2Queue = kC2Ring + 256 * kC2RingStride;     // [kQSlots parts][kQPart][256 packets] entries
 constexpr uint32_t kC2Max = kC2Queue + kQSlots * kQPart * 256 * kQEntry;   // the block's longest packet
 constexpr uint32_t kC2Rcp = kC2Max + 16;                         // rcp64 of the sub-context totals
 constexpr uint32_t kC2Lds = kC2Rcp + 8 * kRcpTab;
@@ -1490,7 +1493,7 @@ void rc_enc2_code2(rc_batch_dev b, E2Params e)
     // coder
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(e.dummy) + ((blockIdx.x * 256u + lane) & 65535u) * 16u;
     Ring o;
-    o.r = smem + kC2Ring + 32 * lane;
+    o.r = smem + kC2Ring + kC2RingStride * lane;
     o.lo = reinterpret_cast<uintptr_t>(b.out + (live ? b.out_off[pkt] : 0));
     o.n = 0;
     o.cap = live ? b.out_cap[pkt] : 0u;
@@ -2498,7 +2501,7 @@ void rc_enc2_wcode2(rc_batch_dev b, E2Params e)
     // coder
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(e.dummy) + ((blockIdx.x * 256u + lane) & 65535u) * 16u;
     Ring o;
-    o.r = smem + kC2Ring + 32 * lane;
+    o.r = smem + kC2Ring + kC2RingStride * lane;
     o.lo = reinterpret_cast<uintptr_t>(b.out + (live ? b.out_off[pkt] : 0));
     o.n = 0;
     o.cap = live ? b.out_cap[pkt] : 0u;
