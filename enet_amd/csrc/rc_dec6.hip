@@ -736,10 +736,27 @@ DEV void verify_fast(const rc_batch_dev& b, const rc_workspace_dev& ws, uint32_t
             // (no branch: a position outside ORs nothing into a word of the lane's own,
             // so the four atomics issue back to back and their returns are awaited once)
             const uint32_t bg = (pv << 8) | x, bit = 1u << (bg & 31);
+#ifdef VERIFY_RETURNS
             const uint32_t old = atomicOr(&set[in ? bg >> 5 : l], in ? bit : 0u);
             cnt += (in && !(old & bit)) ? 1u : 0u;
+#else
+            atomicOr(&set[in ? bg >> 5 : l], in ? bit : 0u);
+#endif
         }
     }
+#ifndef VERIFY_RETURNS
+    // the distinct bigrams are the set's bits: the ORs go without returns (no
+    // wait per round), and one pass counts them.  (A wavefront's LDS
+    // operations complete in order, so the reads see every lane's ORs.)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t i = 0; i < 512 / 64; ++i) {
+        const uint4 q = set4[i * 64 + l];
+        cnt += static_cast<uint32_t>(__builtin_popcount(q.x) + __builtin_popcount(q.y) + __builtin_popcount(q.z) +
+                                     __builtin_popcount(q.w));
+    }
+#endif
     vresult(b, ws, k, h.cl, cnt, h.cks, l);
 }
 
